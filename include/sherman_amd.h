@@ -1,0 +1,142 @@
+/*
+ * sherman_amd.h — C-ABI of the MI355X-native Sherman B+tree hot path.
+ *
+ * Plain C: opaque handle, plain pointers and sizes, int status codes. No HIP,
+ * torch or C++ types appear in the signatures (streams are passed as void*,
+ * i.e. a hipStream_t cast, NULL = the handle's own stream).
+ *
+ * Every batch entry point takes DEVICE pointers (HBM of the tree's GPU). The
+ * host C++ facade (sherman_amd/csrc/Tree.hpp) provides the reference's
+ * single-op, host-pointer Tree API on top of these.
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * Sherman source tree, cmemory/Sherman):
+ *   shm_tree_create     Tree::Tree(DSM*, uint16_t)        include/Tree.h:45,  src/Tree.cpp:27-61
+ *                       + DSM::getInstance / alloc        include/DSM.h:33-40, 198-224
+ *   shm_tree_destroy    (process teardown; DSM is a singleton, src/DSM.cpp:23-35)
+ *   shm_search_batch    Tree::search(const Key&, Value&)  include/Tree.h:49-50, src/Tree.cpp:405-459
+ *   shm_insert_batch    Tree::insert(const Key&, const Value&)
+ *                                                         include/Tree.h:47-48, src/Tree.cpp:353-403
+ *   shm_del_batch       Tree::del(const Key&)             include/Tree.h:51,   src/Tree.cpp:542-591
+ *   shm_range_query     Tree::range_query(from, to, Value*)
+ *                                                         include/Tree.h:53-54, src/Tree.cpp:461-540
+ *   shm_stats           Tree::print_and_check_tree / index_cache_statistics
+ *                                                         include/Tree.h:56, 62; src/Tree.cpp:151-203
+ *   shm_dump_image / shm_load_image
+ *                       the MN arena + root pointer (src/DSM.cpp:37-53, src/Tree.cpp:90-114)
+ *   shm_route_*         (no reference counterpart: the multi-GPU key routing
+ *                        that replaces DSM chunk round-robin, include/DSM.h:198-224)
+ */
+#ifndef SHERMAN_AMD_H
+#define SHERMAN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHM_ABI_VERSION 1
+
+/* status codes (negative errno style) */
+#define SHM_OK 0
+#define SHM_EINVAL (-22)   /* bad argument, key == UINT64_MAX (kKeyMax) */
+#define SHM_ENOMEM (-12)   /* page arena or workspace exhausted */
+#define SHM_EIO (-5)       /* HIP failure or tree inconsistency detected */
+#define SHM_EAGAIN (-11)   /* optimistic version/lock check failed */
+#define SHM_E2BIG (-7)     /* batch larger than cfg.max_batch */
+
+/* flags for shm_config.flags */
+#define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key before the walk */
+
+typedef struct shm_tree shm_tree;
+
+typedef struct shm_config {
+  uint32_t struct_size;  /* sizeof(shm_config) */
+  int32_t device;        /* HIP device ordinal */
+  uint16_t node_id;      /* GlobalAddress.nodeID of this shard (= GPU id) */
+  uint16_t reserved0;
+  uint32_t flags;        /* SHM_FLAG_* */
+  uint64_t arena_bytes;  /* HBM page arena (1 KB pages) */
+  uint64_t max_batch;    /* largest n accepted by a batch call */
+  uint32_t num_locks;    /* HBM lock table words (reference: 16384) */
+  uint32_t sort_bits;    /* top key bits used to order gets (0 = default) */
+} shm_config;
+
+typedef struct shm_stats_t {
+  uint64_t root_ptr;      /* GlobalAddress of the root page */
+  uint32_t root_level;    /* level of the root (leaves are level 0) */
+  uint32_t height;        /* root_level + 1 */
+  uint64_t pages_used;    /* allocated 1 KB pages (excluding superblock) */
+  uint64_t pages_capacity;
+  uint64_t arena_bytes;
+  uint64_t batches;       /* mutating batches applied */
+  uint64_t splits;        /* leaf + internal pages created by splits */
+  uint32_t last_error;    /* sticky device error bits (0 = none) */
+  uint32_t reserved;
+} shm_stats_t;
+
+/* lifecycle ------------------------------------------------------------------ */
+int shm_config_init(shm_config *cfg);
+int shm_tree_create(const shm_config *cfg, shm_tree **out);
+int shm_tree_destroy(shm_tree *t);
+const char *shm_strerror(int status);
+int shm_abi_version(void);
+
+/* batched hot path (device pointers) ------------------------------------------ */
+/* vals_out[i] = value of keys[i] (0 if absent); found_out[i] = 1/0.
+ * found_out may be NULL. Reads only; safe to call concurrently on distinct
+ * streams with other searches. */
+int shm_search_batch(shm_tree *t, const uint64_t *keys, uint64_t n,
+                     uint64_t *vals_out, uint8_t *found_out, void *stream);
+/* Upsert keys[i] -> vals[i] in batch order (last writer in the batch wins).
+ * vals[i] == 0 (kValueNull) deletes keys[i]. Mutating calls on one handle are
+ * serialised internally. Returns after the batch is applied on `stream`. */
+int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
+                     uint64_t n, void *stream);
+/* Tree::del for every key. */
+int shm_del_batch(shm_tree *t, const uint64_t *keys, uint64_t n, void *stream);
+/* Batched inclusive range scans [from[i], to[i]]: values of valid entries in
+ * leaf order then slot order.  counts_out[i] = number of matches; values are
+ * written to vals_out[offsets[i] ...] only when offsets != NULL (call once
+ * with offsets == NULL to size, then again with an exclusive scan). */
+int shm_range_query(shm_tree *t, const uint64_t *from, const uint64_t *to,
+                    uint64_t n, uint64_t *counts_out, const uint64_t *offsets,
+                    uint64_t *vals_out, void *stream);
+
+/* introspection / images (host pointers) ------------------------------------- */
+int shm_stats(shm_tree *t, shm_stats_t *out);
+/* Copy the arena (superblock + pages) to host memory. *bytes_used receives
+ * the number of bytes that hold pages; *root_ptr the root GlobalAddress. */
+int shm_dump_image(shm_tree *t, void *host_buf, uint64_t cap,
+                   uint64_t *bytes_used, uint64_t *root_ptr);
+/* Replace the tree with a page image laid out by the reference format
+ * (pages at GlobalAddress offsets, nodeID == cfg.node_id). */
+int shm_load_image(shm_tree *t, const void *host_buf, uint64_t bytes,
+                   uint64_t root_ptr);
+/* Structural check on device data: fences, ordering, occupancy. */
+int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
+              uint64_t *n_keys);
+int shm_synchronize(shm_tree *t);
+
+/* multi-GPU routing helpers (range shards: shard s owns
+ * [s * 2^64 / P, (s+1) * 2^64 / P)) ------------------------------------------ */
+/* Bucket n keys by owning shard: writes per-shard counts[P], the keys grouped
+ * by shard into keys_out, and perm[i] = source position of keys_out[i]. */
+int shm_route_bucket(shm_tree *t, const uint64_t *keys, uint64_t n,
+                     uint32_t num_shards, uint64_t *counts_out,
+                     uint64_t *keys_out, uint32_t *perm_out, void *stream);
+/* out[perm[i]] = in[i] (reverse of the bucket permutation). */
+int shm_route_unpermute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
+                        uint64_t n, uint64_t *out, void *stream);
+
+/* workload generators on device (test/benchmark.cpp:43-46, zipf.h) ----------- */
+/* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */
+int shm_gen_keys(shm_tree *t, uint64_t first, uint64_t n, uint64_t keyspace,
+                 uint64_t *keys_out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHERMAN_AMD_H */

@@ -1,0 +1,297 @@
+"""sherman_amd — MI355X-native Sherman B+tree hot path (batched get / insert).
+
+Python view of the C-ABI in include/sherman_amd.h (libsherman_amd.so, built
+in-tree by `make -C sherman_amd`).  The host interface mirrors the reference
+`Tree` (include/Tree.h:42-63): `search`, `insert`, `del_`, `range_query`,
+plus the batched forms the GPU path is built around.  Batch methods take
+torch CUDA (HIP) tensors or raw device pointers; torch is used only as the
+device-memory / stream plumbing.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is
+visible, constructing a Tree raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsherman_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sherman_amd.h")
+
+SHM_OK = 0
+SHM_EINVAL = -22
+SHM_ENOMEM = -12
+SHM_EIO = -5
+SHM_EAGAIN = -11
+SHM_E2BIG = -7
+SHM_FLAG_SORT_GETS = 0x1
+
+KEY_MAX = (1 << 64) - 1
+PAGE_SIZE = 1024
+LEAF_CARDINALITY = 54       # include/Tree.h:193-195
+INTERNAL_CARDINALITY = 61   # include/Tree.h:189-191
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+
+
+class ShmConfig(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("node_id", ctypes.c_uint16),
+        ("reserved0", ctypes.c_uint16),
+        ("flags", ctypes.c_uint32),
+        ("arena_bytes", u64),
+        ("max_batch", u64),
+        ("num_locks", u32),
+        ("sort_bits", u32),
+    ]
+
+
+class ShmStats(ctypes.Structure):
+    _fields_ = [
+        ("root_ptr", u64),
+        ("root_level", u32),
+        ("height", u32),
+        ("pages_used", u64),
+        ("pages_capacity", u64),
+        ("arena_bytes", u64),
+        ("batches", u64),
+        ("splits", u64),
+        ("last_error", u32),
+        ("reserved", u32),
+    ]
+
+
+class ShermanError(RuntimeError):
+    def __init__(self, rc, what=""):
+        self.rc = rc
+        msg = lib().shm_strerror(rc).decode()
+        super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
+
+
+_lib = None
+
+# (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
+_SIGNATURES = [
+    ("shm_config_init", ctypes.c_int, [ctypes.POINTER(ShmConfig)]),
+    ("shm_tree_create", ctypes.c_int, [ctypes.POINTER(ShmConfig), ctypes.POINTER(vp)]),
+    ("shm_tree_destroy", ctypes.c_int, [vp]),
+    ("shm_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("shm_abi_version", ctypes.c_int, []),
+    ("shm_search_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
+    ("shm_insert_batch", ctypes.c_int, [vp, vp, vp, u64, vp]),
+    ("shm_del_batch", ctypes.c_int, [vp, vp, u64, vp]),
+    ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
+    ("shm_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmStats)]),
+    ("shm_dump_image", ctypes.c_int, [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+    ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
+    ("shm_check", ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+    ("shm_synchronize", ctypes.c_int, [vp]),
+    ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
+    ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
+    ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
+]
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE, "-j8"])
+
+
+def lib():
+    """Load libsherman_amd.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} missing: build it with `make -C sherman_amd` "
+                "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != SHM_OK:
+        raise ShermanError(rc, what)
+
+
+def _ptr(x):
+    """Device pointer of a torch tensor / int / None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class Tree:
+    """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
+
+    def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
+                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=24):
+        L = lib()
+        cfg = ShmConfig()
+        _check(L.shm_config_init(ctypes.byref(cfg)), "config")
+        cfg.device = device
+        cfg.node_id = node_id
+        cfg.arena_bytes = arena_bytes
+        cfg.max_batch = max_batch
+        cfg.num_locks = num_locks
+        cfg.sort_bits = sort_bits
+        cfg.flags = SHM_FLAG_SORT_GETS if sort_gets else 0
+        h = vp()
+        _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")
+        self.h = h
+        self.device = device
+        self.node_id = node_id
+        self.max_batch = max_batch
+        self._scratch = {}
+
+    # -- lifecycle ----------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            lib().shm_tree_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- batched hot path (device tensors) -----------------------------------
+    def search_batch(self, keys, vals_out, found_out=None, stream=None):
+        _check(lib().shm_search_batch(self.h, _ptr(keys), keys.numel(),
+                                      _ptr(vals_out), _ptr(found_out),
+                                      _stream_ptr(stream)), "search_batch")
+
+    def insert_batch(self, keys, vals, stream=None):
+        _check(lib().shm_insert_batch(self.h, _ptr(keys), _ptr(vals), keys.numel(),
+                                      _stream_ptr(stream)), "insert_batch")
+
+    def del_batch(self, keys, stream=None):
+        _check(lib().shm_del_batch(self.h, _ptr(keys), keys.numel(),
+                                   _stream_ptr(stream)), "del_batch")
+
+    def range_query_batch(self, lo, hi, stream=None):
+        """Returns (counts, values concatenated in query order)."""
+        import torch
+        n = lo.numel()
+        counts = torch.empty(n, dtype=torch.int64, device=lo.device)
+        _check(lib().shm_range_query(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
+                                     None, None, _stream_ptr(stream)), "range_query")
+        self.synchronize()
+        offs = torch.cumsum(counts, 0) - counts
+        total = int(counts.sum().item()) if n else 0
+        vals = torch.empty(max(total, 1), dtype=torch.int64, device=lo.device)
+        _check(lib().shm_range_query(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
+                                     _ptr(offs), _ptr(vals), _stream_ptr(stream)),
+               "range_query")
+        self.synchronize()
+        return counts, vals[:total]
+
+    # -- reference single-op API (Tree.h:47-54) -------------------------------
+    def _dev(self, name, n):
+        import torch
+        t = self._scratch.get(name)
+        if t is None or t.numel() < n:
+            t = torch.empty(max(n, 1), dtype=torch.int64, device=f"cuda:{self.device}")
+            self._scratch[name] = t
+        return t[:n]
+
+    def insert(self, k, v):
+        import torch
+        ks = torch.tensor([to_i64(k)], dtype=torch.int64, device=f"cuda:{self.device}")
+        vs = torch.tensor([to_i64(v)], dtype=torch.int64, device=f"cuda:{self.device}")
+        self.insert_batch(ks, vs)
+
+    def search(self, k):
+        import torch
+        ks = torch.tensor([to_i64(k)], dtype=torch.int64, device=f"cuda:{self.device}")
+        vs = self._dev("sv", 1)
+        fs = torch.empty(1, dtype=torch.uint8, device=f"cuda:{self.device}")
+        self.search_batch(ks, vs, fs)
+        self.synchronize()
+        return bool(fs.item()), from_i64(vs.item())
+
+    def del_(self, k):
+        import torch
+        ks = torch.tensor([to_i64(k)], dtype=torch.int64, device=f"cuda:{self.device}")
+        self.del_batch(ks)
+
+    # -- introspection ---------------------------------------------------------
+    def synchronize(self):
+        _check(lib().shm_synchronize(self.h), "synchronize")
+
+    def stats(self):
+        s = ShmStats()
+        _check(lib().shm_stats(self.h, ctypes.byref(s)), "stats")
+        return {f: getattr(s, f) for f, _ in ShmStats._fields_}
+
+    def check(self):
+        a, b, c = u64(), u64(), u64()
+        _check(lib().shm_check(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+               "check")
+        return dict(leaves=a.value, internal=b.value, keys=c.value)
+
+    def dump_image(self):
+        import numpy as np
+        used, root = u64(), u64()
+        _check(lib().shm_dump_image(self.h, None, 0, ctypes.byref(used), ctypes.byref(root)),
+               "dump")
+        buf = np.zeros(used.value, dtype=np.uint8)
+        _check(lib().shm_dump_image(self.h, buf.ctypes.data_as(vp), used.value,
+                                    ctypes.byref(used), ctypes.byref(root)), "dump")
+        return buf, root.value
+
+    def load_image(self, image, root_ptr):
+        import numpy as np
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        _check(lib().shm_load_image(self.h, image.ctypes.data_as(vp), image.nbytes,
+                                    root_ptr), "load_image")
+
+    # -- routing / generators ---------------------------------------------------
+    def route_bucket(self, keys, num_shards, keys_out, perm_out, counts_out, stream=None):
+        _check(lib().shm_route_bucket(self.h, _ptr(keys), keys.numel(), num_shards,
+                                      _ptr(counts_out), _ptr(keys_out), _ptr(perm_out),
+                                      _stream_ptr(stream)), "route_bucket")
+
+    def route_unpermute(self, vals_in, perm, out, stream=None):
+        _check(lib().shm_route_unpermute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
+                                         _ptr(out), _stream_ptr(stream)), "unpermute")
+
+    def gen_keys(self, first, n, out, keyspace=0, stream=None):
+        _check(lib().shm_gen_keys(self.h, first, n, keyspace, _ptr(out),
+                                  _stream_ptr(stream)), "gen_keys")
+
+
+def to_i64(x):
+    """u64 -> signed int64 bit pattern (torch has no uint64 arithmetic)."""
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def from_i64(x):
+    return x & ((1 << 64) - 1)
+
+
+def header_symbols(path=HEADER_PATH):
+    """Names of every function declared in include/sherman_amd.h."""
+    import re
+    txt = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(shm_\w+)\s*\(", txt, re.M)))

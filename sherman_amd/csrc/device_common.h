@@ -1,0 +1,237 @@
+// device_common.h — wave64 helpers and page (de)serialisation for gfx950.
+//
+// A 1 KB Sherman page is moved as ONE global_load_dwordx4 per lane: lane l
+// holds bytes [16l, 16l+16) in a u32x4.  Header fields come out with
+// v_readlane (they live in lanes 0..2 and 63), internal records are lane
+// aligned (record j = lane j+3 after a one-lane shift), and the 18-byte leaf
+// entries (2-byte aligned) are staged through a per-wave 1 KB LDS slot.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+namespace shm {
+namespace dev {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;  // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kPageDwords = 256;
+constexpr int kMaxRounds = 4096;   // walk rounds per wave before giving up
+constexpr int kMaxRetries = 1000;  // version-mismatch re-reads (Tree.cpp:600)
+constexpr uint32_t kMaxLockSpins = 1u << 22;
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  return (uint64_t)rl32((uint32_t)v, l) |
+         ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32);
+}
+__device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+  return (uint32_t)__shfl((int)v, src);
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  return (uint64_t)shfl32((uint32_t)v, src) |
+         ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32);
+}
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+// order this wave's LDS traffic (LDS executes in order per wave; this keeps
+// the compiler from moving accesses across and drains the counter)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ u32x4 load_page_slice(const uint8_t* arena,
+                                                  uint64_t off) {
+  return *reinterpret_cast<const u32x4*>(arena + off + 16 * lane_id());
+}
+
+// Header (Tree.h:130-160) + page versions, wave-uniform.
+struct Hdr {
+  uint64_t leftmost, sibling, lowest, highest;
+  uint32_t level;
+  int32_t last_index;
+  uint32_t fver, rver_internal, rver_leaf;
+};
+
+__device__ __forceinline__ Hdr parse_hdr(const u32x4 w) {
+  const uint32_t a2 = rl32(w.z, 0), a3 = rl32(w.w, 0);
+  const uint32_t b0 = rl32(w.x, 1), b1 = rl32(w.y, 1), b2 = rl32(w.z, 1),
+                 b3 = rl32(w.w, 1);
+  const uint32_t c0 = rl32(w.x, 2), c1 = rl32(w.y, 2), c2 = rl32(w.z, 2);
+  const uint32_t z2 = rl32(w.z, 63), z3 = rl32(w.w, 63);
+  Hdr h;
+  h.fver = a2 & 0xFF;  // byte 8
+  h.leftmost = (uint64_t)((a2 >> 8) | (a3 << 24)) |  // bytes 9..16
+               ((uint64_t)((a3 >> 8) | (b0 << 24)) << 32);
+  h.sibling = (uint64_t)((b0 >> 8) | (b1 << 24)) |  // bytes 17..24
+              ((uint64_t)((b1 >> 8) | (b2 << 24)) << 32);
+  h.level = (b2 >> 8) & 0xFF;                   // byte 25
+  h.last_index = (int32_t)(int16_t)(b2 >> 16);  // bytes 26..27
+  h.lowest = (uint64_t)b3 | ((uint64_t)c0 << 32);   // bytes 28..35
+  h.highest = (uint64_t)c1 | ((uint64_t)c2 << 32);  // bytes 36..43
+  h.rver_internal = z3 & 0xFF;                       // byte 1020
+  h.rver_leaf = z2 & 0xFF;                           // byte 1016
+  return h;
+}
+
+// Internal record j = lane - 3 (Tree.h:163-172): key straddles lanes j+2/j+3.
+struct IntRec {
+  uint64_t key, ptr;
+};
+__device__ __forceinline__ IntRec internal_record(const u32x4 w) {
+  const uint32_t prev_w3 = (uint32_t)__shfl_up((int)w.w, 1);
+  IntRec r;
+  r.key = ((uint64_t)w.x << 32) | prev_w3;
+  r.ptr = (uint64_t)w.y | ((uint64_t)w.z << 32);
+  return r;
+}
+
+// Leaf entry i = lane (Tree.h:174-187), read from the wave's LDS page image.
+struct LeafEnt {
+  uint64_t key, val;
+  uint32_t fraw, rraw;  // full bytes; versions are the low nibbles
+};
+__device__ __forceinline__ void stage_page(uint32_t* lp, const u32x4 w) {
+  *reinterpret_cast<u32x4*>(lp + 4 * lane_id()) = w;
+}
+__device__ __forceinline__ LeafEnt leaf_entry(const uint32_t* lp, int i) {
+  const int s = kOffRecords + kLeafEntry * i;
+  const int d = s >> 2;
+  const uint32_t sh = (uint32_t)(s & 3);
+  const uint32_t a0 = lp[d], a1 = lp[d + 1], a2 = lp[d + 2], a3 = lp[d + 3],
+                 a4 = lp[d + 4];
+  const uint32_t e0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
+  const uint32_t e1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+  const uint32_t e2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
+  const uint32_t e3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+  const uint32_t e4 = __builtin_amdgcn_alignbyte(0u, a4, sh);
+  LeafEnt e;
+  e.fraw = e0 & 0xFF;
+  e.key = (uint64_t)((e0 >> 8) | (e1 << 24)) |
+          ((uint64_t)((e1 >> 8) | (e2 << 24)) << 32);
+  e.val = (uint64_t)((e2 >> 8) | (e3 << 24)) |
+          ((uint64_t)((e3 >> 8) | (e4 << 24)) << 32);
+  e.rraw = (e4 >> 8) & 0xFF;
+  return e;
+}
+// write an 18 B entry at its 2-byte aligned slot (9 halfword stores)
+__device__ __forceinline__ void put_leaf_entry(uint32_t* lp, int i,
+                                               uint64_t key, uint64_t val,
+                                               uint32_t fraw, uint32_t rraw) {
+  uint16_t* h = reinterpret_cast<uint16_t*>(
+      reinterpret_cast<uint8_t*>(lp) + kOffRecords + kLeafEntry * i);
+  h[0] = (uint16_t)((fraw & 0xFF) | ((key & 0xFF) << 8));
+  h[1] = (uint16_t)(key >> 8);
+  h[2] = (uint16_t)(key >> 24);
+  h[3] = (uint16_t)(key >> 40);
+  h[4] = (uint16_t)((key >> 56) | ((val & 0xFF) << 8));
+  h[5] = (uint16_t)(val >> 8);
+  h[6] = (uint16_t)(val >> 24);
+  h[7] = (uint16_t)(val >> 40);
+  h[8] = (uint16_t)((val >> 56) | ((rraw & 0xFF) << 8));
+}
+
+// Header dword d (0..10) of a page image (bytes 0..43); lock word = 0.
+__device__ __forceinline__ uint32_t header_dword(int d, uint32_t fver,
+                                                 uint64_t leftmost,
+                                                 uint64_t sibling,
+                                                 uint32_t level,
+                                                 int32_t last_index,
+                                                 uint64_t lowest,
+                                                 uint64_t highest) {
+  switch (d) {
+    case 2: return (fver & 0xFF) | (uint32_t)((leftmost & 0xFFFFFF) << 8);
+    case 3: return (uint32_t)(leftmost >> 24);
+    case 4: return (uint32_t)(leftmost >> 56) | (uint32_t)((sibling & 0xFFFFFF) << 8);
+    case 5: return (uint32_t)(sibling >> 24);
+    case 6:
+      return (uint32_t)(sibling >> 56) | ((level & 0xFF) << 8) |
+             ((uint32_t)(last_index & 0xFFFF) << 16);
+    case 7: return (uint32_t)lowest;
+    case 8: return (uint32_t)(lowest >> 32);
+    case 9: return (uint32_t)highest;
+    case 10: return (uint32_t)(highest >> 32);
+    default: return 0;
+  }
+}
+
+// zero the slot and write a fresh header (all lanes call)
+__device__ __forceinline__ void init_page_image(uint32_t* lp, uint32_t fver,
+                                                uint64_t leftmost,
+                                                uint64_t sibling,
+                                                uint32_t level,
+                                                int32_t last_index,
+                                                uint64_t lowest,
+                                                uint64_t highest) {
+  const int l = lane_id();
+  *reinterpret_cast<u32x4*>(lp + 4 * l) = u32x4{0, 0, 0, 0};
+  wave_lds_sync();
+  if (l < 11)
+    lp[l] = header_dword(l, fver, leftmost, sibling, level, last_index, lowest,
+                         highest);
+}
+
+__device__ __forceinline__ void store_page(uint8_t* arena, uint64_t off,
+                                           const uint32_t* lp) {
+  wave_lds_sync();
+  const u32x4 w = *reinterpret_cast<const u32x4*>(lp + 4 * lane_id());
+  *reinterpret_cast<u32x4*>(arena + off + 16 * lane_id()) = w;
+}
+
+__device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,
+                                       uint64_t arena_bytes) {
+  const uint64_t off = ga_offset(ga);
+  return ga != 0 && ga_node(ga) == node && (off & (kPageSize - 1)) == 0 &&
+         off >= kPageSize && off + kPageSize <= arena_bytes;
+}
+
+// in-wave ascending bitonic sort of (key, tag) over 64 lanes
+__device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& tag) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t pk = shfl64(key, l ^ j);
+      const uint32_t pt = shfl32(tag, l ^ j);
+      const bool up = (l & k) == 0;
+      const bool lower = (l & j) == 0;
+      const bool take = lower == up ? (pk < key) : (pk > key);
+      if (take) {
+        key = pk;
+        tag = pt;
+      }
+    }
+  }
+}
+
+// lower_bound over a sorted global u64 array [lo, hi)
+__device__ __forceinline__ uint64_t lower_bound64(const uint64_t* a,
+                                                  uint64_t lo, uint64_t hi,
+                                                  uint64_t k) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+}  // namespace dev
+}  // namespace shm

@@ -1,0 +1,100 @@
+// kernels.h — launch interface between the host runtime (tree.cpp) and the
+// HIP kernels (walk.hip, insert.hip, util.hip).  Host-only types; no torch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shm {
+namespace dev {
+
+struct WalkArgs {
+  const uint8_t* arena;
+  uint64_t arena_bytes;
+  uint16_t node;
+  uint64_t root;
+  const uint64_t* keys;
+  const uint32_t* perm;   // GET: output position of keys[i] (nullable)
+  const uint64_t* n_dev;  // device count (nullable -> use n)
+  uint64_t n;
+  uint64_t* out_val;      // GET
+  uint8_t* out_found;     // GET (nullable)
+  uint64_t* out_page;     // LOCATE
+  int target_level;       // LOCATE
+  uint32_t* err;
+};
+
+void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
+                 hipStream_t s);
+
+// ---- insert pipeline -------------------------------------------------------
+struct SegArgs {
+  uint8_t* arena;
+  uint64_t arena_bytes;
+  uint16_t node;
+  // sorted unique operation keys / values of this level (values: leaf values
+  // or child GlobalAddresses for internal levels)
+  const uint64_t* op_key;
+  const uint64_t* op_val;
+  uint64_t n_ops;
+  // segments (runs of ops targeting one page)
+  const uint32_t* seg_start;  // [num_seg + 1]
+  const uint64_t* seg_page;   // [num_seg]
+  uint32_t num_seg;
+  uint32_t* seg_T;            // entries after applying
+  uint32_t* seg_P;            // pages after applying (1 = in place)
+  uint32_t* seg_newpages;     // P - 1
+  uint32_t* seg_ver;          // front_version observed by plan
+  const uint32_t* seg_pbase;  // exclusive scan of seg_newpages
+  uint64_t first_new_page;    // arena page index of the first new page
+  uint64_t* sep_key;          // separators for the parent level
+  uint64_t* sep_ptr;
+  uint64_t* locks;
+  uint32_t num_locks;
+  uint64_t tag_base;
+  int level;
+  int is_delete;
+  uint32_t* err;
+};
+
+void launch_leaf_plan(const SegArgs& a, hipStream_t s);
+void launch_leaf_build(const SegArgs& a, uint32_t total_new, hipStream_t s);
+void launch_leaf_update(const SegArgs& a, hipStream_t s);
+void launch_leaf_delete(const SegArgs& a, hipStream_t s);
+void launch_int_plan(const SegArgs& a, hipStream_t s);
+void launch_int_build(const SegArgs& a, uint32_t total_new, hipStream_t s);
+void launch_int_update(const SegArgs& a, hipStream_t s);
+void launch_new_root(uint8_t* arena, uint64_t page_off, uint64_t old_root,
+                     uint32_t level, hipStream_t s);
+void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
+
+// ---- utilities (util.hip) -----------------------------------------------------
+void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);
+// flags[i] = (last of equal-key run) * (v != 0 ? 1 : 1 << 32), key checks
+void launch_mark_unique(const uint64_t* sk, const uint32_t* sidx,
+                        const uint64_t* vals, uint64_t n, uint64_t* flags,
+                        uint32_t* err, hipStream_t s);
+void launch_compact_unique(const uint64_t* sk, const uint32_t* sidx,
+                           const uint64_t* vals, const uint64_t* flags,
+                           const uint64_t* pos, uint64_t n, uint64_t* uk,
+                           uint64_t* uv, uint64_t* dk, uint64_t* counts,
+                           hipStream_t s);
+void launch_seg_heads(const uint64_t* page, uint64_t n, uint32_t* heads,
+                      hipStream_t s);
+void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
+                     const uint32_t* pos, uint64_t n, uint32_t* seg_start,
+                     uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
+void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
+                     uint64_t* out, hipStream_t s);
+void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
+                         uint64_t* counts, uint64_t* keys_out, uint32_t* perm,
+                         uint32_t* cursor, hipStream_t s);
+void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
+                      uint64_t* out, hipStream_t s);
+void launch_range_count(const uint8_t* arena, uint64_t arena_bytes,
+                        uint16_t node, uint64_t root, const uint64_t* from,
+                        const uint64_t* to, uint64_t n, uint64_t* counts,
+                        const uint64_t* offsets, uint64_t* vals,
+                        uint32_t* err, hipStream_t s);
+
+}  // namespace dev
+}  // namespace shm

@@ -1,0 +1,112 @@
+// layout.h — Sherman page layout, constants and GlobalAddress, shared by the
+// HIP kernels and the host runtime.  Byte offsets restate the packed C++ layout
+// of include/Tree.h:130-336 (probe-verified in SURVEY.md Appendix A); they are
+// spelled out as offsets because the kernels move whole 1 KB pages through
+// registers/LDS and never materialise the packed structs.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SHM_HD __host__ __device__ __forceinline__
+#else
+#define SHM_HD inline
+#endif
+
+namespace shm {
+
+// include/Common.h:113-121
+constexpr uint64_t kKeyMin = 0;
+constexpr uint64_t kKeyMax = ~0ull;
+constexpr uint64_t kValueNull = 0;
+constexpr uint32_t kPageSize = 1024;  // kInternalPageSize == kLeafPageSize
+
+// include/Tree.h:189-195
+constexpr int kInternalCardinality = 61;
+constexpr int kLeafCardinality = 54;
+constexpr int kMaxLevelOfTree = 7;  // include/Common.h:96
+
+// Batched multi-way split targets (reference splits one page at a time at
+// exactly 54 / 61 and leaves halves of 27 / 30, src/Tree.cpp:939, 779).  A
+// batch may overflow a page by many entries; it is then cut into
+// ceil(T / fill) pages so a 54-entry overflow still yields 27 + 27.
+constexpr int kLeafSplitFill = 36;      // entries per leaf after a k-way split
+constexpr int kInternalSplitFill = 40;  // records per internal page
+
+// byte offsets inside a page (Tree.h:197-336)
+constexpr int kOffLock = 0;        // union {crc, embedding_lock, freq}
+constexpr int kOffFrontVer = 8;    // front_version
+constexpr int kOffLeftmost = 9;    // Header.leftmost_ptr
+constexpr int kOffSibling = 17;    // Header.sibling_ptr
+constexpr int kOffLevel = 25;      // Header.level
+constexpr int kOffLastIndex = 26;  // Header.last_index (int16)
+constexpr int kOffLowest = 28;     // Header.lowest
+constexpr int kOffHighest = 36;    // Header.highest
+constexpr int kOffRecords = 44;    // records[]
+constexpr int kOffInternalRear = 1020;
+constexpr int kOffLeafRear = 1016;
+constexpr int kInternalEntry = 16;  // {key, ptr}
+constexpr int kLeafEntry = 18;      // {f:4, key, value, r:4}
+
+static_assert(kOffRecords + kInternalCardinality * kInternalEntry ==
+                  kOffInternalRear,
+              "internal layout");
+static_assert(kOffRecords + kLeafCardinality * kLeafEntry == kOffLeafRear,
+              "leaf layout");
+
+// GlobalAddress{nodeID:16, offset:48} (include/GlobalAddress.h:7-16).
+// nodeID = GPU / shard id, offset = byte offset into that GPU's page arena.
+SHM_HD uint64_t ga_make(uint16_t node, uint64_t off) {
+  return (uint64_t)node | (off << 16);
+}
+SHM_HD uint64_t ga_offset(uint64_t ga) { return ga >> 16; }
+SHM_HD uint16_t ga_node(uint64_t ga) { return (uint16_t)(ga & 0xFFFF); }
+
+// Superblock in page 0 of the arena (offset 0 is Null, like chunk 0 in
+// GlobalAllocator.h:24-26); it plays the role of root_ptr_ptr
+// (src/Tree.cpp:90-97) and of the Directory's g_root_ptr / g_root_level
+// (src/Directory.cpp:72-79).
+struct Superblock {
+  uint64_t magic;
+  uint64_t root_ptr;
+  uint64_t root_level;
+  uint64_t next_page;  // bump allocator, in pages (page 0 = superblock)
+  uint64_t capacity_pages;
+  uint64_t node_id;
+  uint64_t batches;
+  uint64_t splits;
+};
+constexpr uint64_t kSuperMagic = 0x5348524d414d4431ull;  // "SHRMAMD1"
+
+// device error bits
+constexpr uint32_t kErrBadPtr = 1u << 0;       // pointer outside arena / node
+constexpr uint32_t kErrInconsistent = 1u << 1; // version mismatch persisted
+constexpr uint32_t kErrRounds = 1u << 2;       // walk did not converge
+constexpr uint32_t kErrFence = 1u << 3;        // k < lowest on a walk
+constexpr uint32_t kErrLock = 1u << 4;         // lock spin bound exceeded
+constexpr uint32_t kErrPlan = 1u << 5;         // page changed between plan/apply
+constexpr uint32_t kErrOverflow = 1u << 6;     // page overfull at apply
+
+// CityHash64 v1.1 (google/cityhash, city.cc HashLen0to16 for len == 8).
+// Third-party dependency of the reference (script/installLibs.sh:16-20, HEAD,
+// unpinned); used by to_key (test/benchmark.cpp:43-46) and the lock index
+// (src/Tree.cpp:832-833).
+SHM_HD uint64_t rot64(uint64_t v, int s) {
+  return s == 0 ? v : ((v >> s) | (v << (64 - s)));
+}
+SHM_HD uint64_t cityhash64_u64(uint64_t x) {
+  const uint64_t k2 = 0x9ae16a3b2f90404full;
+  const uint64_t len = 8;
+  const uint64_t mul = k2 + len * 2;
+  const uint64_t a = x + k2;
+  const uint64_t b = x;  // Fetch64(s + len - 8) == Fetch64(s)
+  const uint64_t c = rot64(b, 37) * mul + a;
+  const uint64_t d = (rot64(a, 25) + b) * mul;
+  uint64_t h = (c ^ d) * mul;  // HashLen16(c, d, mul)
+  h ^= (h >> 47);
+  uint64_t g = (d ^ h) * mul;
+  g ^= (g >> 47);
+  g *= mul;
+  return g;
+}
+
+}  // namespace shm

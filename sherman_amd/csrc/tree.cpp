@@ -1,0 +1,676 @@
+// tree.cpp — host runtime behind the C-ABI (include/sherman_amd.h).
+//
+// Owns one shard's HBM page arena, lock table and batch workspace, and drives
+// the kernels of walk.hip / insert.hip / util.hip.  The roles of the
+// reference's DSM (include/DSM.h:33-176: remote read/write/CAS, alloc), the
+// Directory's root publication (src/Directory.cpp:72-83) and the
+// Local/GlobalAllocator (include/LocalAllocator.h, GlobalAllocator.h) are
+// taken by: plain HBM pointers, a host-authoritative bump allocator over the
+// arena (mirrored into the superblock in page 0) and a root register.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <mutex>
+#include <vector>
+
+#include "../../include/sherman_amd.h"
+#include "kernels.h"
+#include "layout.h"
+#include "sort.h"
+
+using namespace shm;
+
+namespace {
+
+constexpr uint64_t kSortMinGets = 8192;   // below this, walk in input order
+constexpr uint32_t kDefaultSortBits = 24; // top key bits that order gets
+constexpr int kWalkDepth = 8;             // pages in flight per wave
+
+}  // namespace
+
+struct shm_tree {
+  shm_config cfg{};
+  hipStream_t stream = nullptr;
+  uint8_t* arena = nullptr;
+  uint64_t arena_bytes = 0;
+  uint64_t cap_pages = 0;
+  uint64_t* locks = nullptr;
+  uint32_t* d_err = nullptr;
+  uint64_t* d_counts = nullptr;  // 16 words of device scratch
+  uint32_t* route_scratch = nullptr;
+  uint64_t* h_pin = nullptr;     // 16 words pinned host scratch
+  // host-authoritative tree metadata (superblock mirror)
+  uint64_t root = 0;
+  uint32_t root_level = 0;
+  uint64_t next_page = 0;
+  uint64_t batches = 0;
+  uint64_t splits = 0;
+  uint32_t sticky_err = 0;
+  // workspace (sized for cfg.max_batch)
+  uint64_t nmax = 0, sep_cap = 0;
+  uint64_t *ka = nullptr, *kb = nullptr;
+  uint32_t *ia = nullptr, *ib = nullptr;
+  uint64_t *flags = nullptr, *pos = nullptr;
+  uint64_t *uk = nullptr, *uv = nullptr, *dk = nullptr;
+  uint64_t* pages = nullptr;
+  uint32_t *heads = nullptr, *hpos = nullptr;
+  uint32_t* seg_start = nullptr;
+  uint64_t* seg_page = nullptr;
+  uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr,
+           *seg_pbase = nullptr, *seg_ver = nullptr;
+  uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+#define HIP_OK(expr)                                                         \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) {                                                  \
+      fprintf(stderr, "sherman_amd: %s failed: %s (%s:%d)\n", #expr,         \
+              hipGetErrorString(_e), __FILE__, __LINE__);                    \
+      return SHM_EIO;                                                        \
+    }                                                                        \
+  } while (0)
+
+template <class T>
+int dalloc(T** p, uint64_t count) {
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) {
+    *p = nullptr;
+    return SHM_ENOMEM;
+  }
+  return SHM_OK;
+}
+
+hipStream_t pick(shm_tree* t, void* s) {
+  return s ? (hipStream_t)s : t->stream;
+}
+
+dev::WalkArgs walk_args(shm_tree* t) {
+  dev::WalkArgs a{};
+  a.arena = t->arena;
+  a.arena_bytes = t->arena_bytes;
+  a.node = t->cfg.node_id;
+  a.root = t->root;
+  a.err = t->d_err;
+  return a;
+}
+
+dev::SegArgs seg_args(shm_tree* t) {
+  dev::SegArgs a{};
+  a.arena = t->arena;
+  a.arena_bytes = t->arena_bytes;
+  a.node = t->cfg.node_id;
+  a.seg_start = t->seg_start;
+  a.seg_page = t->seg_page;
+  a.seg_T = t->seg_T;
+  a.seg_P = t->seg_P;
+  a.seg_newpages = t->seg_np;
+  a.seg_ver = t->seg_ver;
+  a.seg_pbase = t->seg_pbase;
+  a.locks = t->locks;
+  a.num_locks = t->cfg.num_locks;
+  a.tag_base = (t->batches + 1) << 32;
+  a.err = t->d_err;
+  return a;
+}
+
+// read `n` device words into pinned host scratch and wait
+int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
+  HIP_OK(hipMemcpyAsync(t->h_pin, src, bytes, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return SHM_OK;
+}
+
+int write_superblock(shm_tree* t, hipStream_t s) {
+  Superblock sb{};
+  sb.magic = kSuperMagic;
+  sb.root_ptr = t->root;
+  sb.root_level = t->root_level;
+  sb.next_page = t->next_page;
+  sb.capacity_pages = t->cap_pages;
+  sb.node_id = t->cfg.node_id;
+  sb.batches = t->batches;
+  sb.splits = t->splits;
+  memcpy(t->h_pin, &sb, sizeof(sb));
+  HIP_OK(hipMemcpyAsync(t->arena, t->h_pin, sizeof(sb), hipMemcpyHostToDevice, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return SHM_OK;
+}
+
+int check_err(shm_tree* t, hipStream_t s) {
+  int rc = readback(t, s, t->d_err, sizeof(uint32_t));
+  if (rc) return rc;
+  const uint32_t e = (uint32_t)t->h_pin[0];
+  if (e) {
+    t->sticky_err |= e;
+    HIP_OK(hipMemsetAsync(t->d_err, 0, sizeof(uint32_t), s));
+    fprintf(stderr, "sherman_amd: device error bits 0x%x\n", e);
+    return SHM_EIO;
+  }
+  return SHM_OK;
+}
+
+// Segment a sorted op list by the page its walk ends on at `level`.
+// Returns the segment count (or negative status).
+int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
+                uint64_t n_ops, int level) {
+  dev::WalkArgs w = walk_args(t);
+  w.keys = op_key;
+  w.n = n_ops;
+  w.out_page = t->pages;
+  w.target_level = level;
+  dev::launch_walk(w, n_ops, 4, true, s);
+  dev::launch_seg_heads(t->pages, n_ops, t->heads, s);
+  HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
+  uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
+  dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, t->seg_start,
+                       t->seg_page, d_ns, s);
+  int rc = readback(t, s, d_ns, sizeof(uint32_t));
+  if (rc) return rc;
+  return (int64_t)(uint32_t)t->h_pin[0];
+}
+
+// plan + scan + capacity check; returns new page count (or negative status)
+int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
+                   uint64_t reserve) {
+  if (leaf)
+    dev::launch_leaf_plan(a, s);
+  else
+    dev::launch_int_plan(a, s);
+  HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
+                                 a.num_seg, s));
+  // total = pbase[last] + np[last]
+  uint32_t* d_tot = reinterpret_cast<uint32_t*>(t->d_counts + 10);
+  HIP_OK(hipMemcpyAsync(d_tot, t->seg_pbase + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_tot + 1, t->seg_np + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_tot + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
+  int rc = readback(t, s, d_tot, 3 * sizeof(uint32_t));
+  if (rc) return rc;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(t->h_pin);
+  const uint64_t total = (uint64_t)h[0] + h[1];
+  if (h[2]) return check_err(t, s);
+  if (total > t->sep_cap) return SHM_ENOMEM;
+  if (t->next_page + total + reserve > t->cap_pages) return SHM_ENOMEM;
+  return (int64_t)total;
+}
+
+// Apply one level: ops sorted/unique; returns separators produced (written to
+// sep[out]) or a negative status.
+int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
+                    const uint64_t* op_val, uint64_t n_ops, int level,
+                    bool is_delete, int out) {
+  const int64_t ns = segment(t, s, op_key, n_ops, level);
+  if (ns < 0) return ns;
+  if (ns == 0) return 0;
+  dev::SegArgs a = seg_args(t);
+  a.op_key = op_key;
+  a.op_val = op_val;
+  a.n_ops = n_ops;
+  a.num_seg = (uint32_t)ns;
+  a.level = level;
+  a.is_delete = is_delete ? 1 : 0;
+  a.sep_key = t->sep_key[out];
+  a.sep_ptr = t->sep_ptr[out];
+  if (is_delete) {
+    dev::launch_leaf_delete(a, s);
+    return 0;
+  }
+  const bool leaf = level == 0;
+  // head-room for the parent levels a split of this level can trigger
+  const uint64_t reserve = 2 * (uint64_t)kMaxLevelOfTree;
+  const int64_t total = plan_level(t, s, a, leaf, reserve);
+  if (total < 0) return total;
+  a.first_new_page = t->next_page;
+  if (leaf) {
+    dev::launch_leaf_build(a, (uint32_t)total, s);
+    dev::launch_leaf_update(a, s);
+  } else {
+    dev::launch_int_build(a, (uint32_t)total, s);
+    dev::launch_int_update(a, s);
+  }
+  t->next_page += (uint64_t)total;
+  t->splits += (uint64_t)total;
+  return total;
+}
+
+int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                 const uint64_t* vals, uint64_t n) {
+  // 1. stable sort (key, batch index)
+  dev::launch_iota(t->ia, n, s);
+  HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, t->ka, t->ia, t->ib, n, 0, s));
+  // 2. keep the last writer of each key; split upserts / deletes
+  dev::launch_mark_unique(t->ka, t->ib, vals, n, t->flags, t->d_err, s);
+  HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, t->flags, t->pos, n, s));
+  dev::launch_compact_unique(t->ka, t->ib, vals, t->flags, t->pos, n, t->uk,
+                             t->uv, t->dk, t->d_counts, s);
+  HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
+  int rc = readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
+  if (rc) return rc;
+  const uint64_t n_up = t->h_pin[0], n_del = t->h_pin[1];
+  const uint32_t e = (uint32_t)t->h_pin[2];
+  if (e & (1u << 31)) {  // kKeyMax in the batch: reject before mutating
+    HIP_OK(hipMemsetAsync(t->d_err, 0, 4, s));
+    return SHM_EINVAL;
+  }
+  if (e) return check_err(t, s);
+  // 3. deletes (never split), then upserts
+  if (n_del) {
+    const int64_t r = apply_level(t, s, t->dk, nullptr, n_del, 0, true, 0);
+    if (r < 0) return (int)r;
+  }
+  if (!n_up) return SHM_OK;
+  int cur = 0;
+  int64_t nsep = apply_level(t, s, t->uk, t->uv, n_up, 0, false, cur);
+  int level = 1;
+  while (nsep > 0) {
+    if (level > kMaxLevelOfTree) return SHM_EIO;
+    if ((uint32_t)(level - 1) == t->root_level) {
+      // the root split: new root above it (update_new_root, Tree.cpp:126-149)
+      if (t->next_page + 1 > t->cap_pages) return SHM_ENOMEM;
+      const uint64_t off = t->next_page * kPageSize;
+      dev::launch_new_root(t->arena, off, t->root, (uint32_t)level, s);
+      t->next_page += 1;
+      t->root = ga_make(t->cfg.node_id, off);
+      t->root_level = (uint32_t)level;
+    }
+    const int nxt = 1 - cur;
+    nsep = apply_level(t, s, t->sep_key[cur], t->sep_ptr[cur], (uint64_t)nsep,
+                       level, false, nxt);
+    cur = nxt;
+    ++level;
+  }
+  if (nsep < 0) return (int)nsep;
+  return SHM_OK;
+}
+
+void free_all(shm_tree* t) {
+  auto F = [](void* p) {
+    if (p) (void)hipFree(p);
+  };
+  F(t->arena); F(t->locks); F(t->d_err); F(t->d_counts); F(t->route_scratch);
+  F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
+  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos);
+  F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
+  F(t->seg_pbase); F(t->seg_ver);
+  for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
+  F(t->temp);
+  if (t->h_pin) (void)hipHostFree(t->h_pin);
+  if (t->stream) (void)hipStreamDestroy(t->stream);
+}
+
+// host-side structural check of an image (same invariants as SURVEY App. A)
+int check_image(const uint8_t* img, uint64_t bytes, uint64_t root, uint16_t node,
+                uint64_t* n_leaves, uint64_t* n_internal, uint64_t* n_keys) {
+  auto rd64 = [&](uint64_t off) {
+    uint64_t v;
+    memcpy(&v, img + off, 8);
+    return v;
+  };
+  auto page_off = [&](uint64_t ga) -> int64_t {
+    if (ga == 0 || ga_node(ga) != node) return -1;
+    const uint64_t o = ga_offset(ga);
+    if (o < kPageSize || o + kPageSize > bytes || (o & (kPageSize - 1))) return -1;
+    return (int64_t)o;
+  };
+  uint64_t leaves = 0, internals = 0, keys = 0;
+  int64_t ro = page_off(root);
+  if (ro < 0) return -1;
+  int top = img[ro + kOffLevel];
+  uint64_t head = root;
+  for (int lvl = top; lvl >= 0; --lvl) {
+    uint64_t p = head, expect_low = 0, next_head = 0;
+    uint64_t guard = 0;
+    while (p) {
+      if (++guard > bytes / kPageSize + 1) return -20;
+      const int64_t o = page_off(p);
+      if (o < 0) return -2;
+      const uint8_t* pg = img + o;
+      const uint64_t leftmost = rd64(o + kOffLeftmost);
+      const bool is_leaf = leftmost == 0;
+      if (pg[kOffLevel] != lvl) return -3;
+      if ((lvl == 0) != is_leaf) return -4;
+      if (pg[kOffFrontVer] != pg[is_leaf ? kOffLeafRear : kOffInternalRear]) return -5;
+      const uint64_t lo = rd64(o + kOffLowest), hi = rd64(o + kOffHighest);
+      if (lo != expect_low || hi <= lo) return -6;
+      if (is_leaf) {
+        int c = 0;
+        for (int i = 0; i < kLeafCardinality; ++i) {
+          const uint64_t e = o + kOffRecords + (uint64_t)kLeafEntry * i;
+          if (rd64(e + 9) == kValueNull) continue;
+          const uint64_t k = rd64(e + 1);
+          if (k < lo || k >= hi) return -7;
+          ++c;
+        }
+        if (c > kLeafCardinality - 1) return -8;
+        keys += (uint64_t)c;
+        ++leaves;
+      } else {
+        int16_t li;
+        memcpy(&li, pg + kOffLastIndex, 2);
+        const int cnt = li + 1;
+        if (cnt < 0 || cnt > kInternalCardinality - 1) return -9;
+        if (!next_head) next_head = leftmost;
+        int64_t co = page_off(leftmost);
+        if (co < 0 || rd64(co + kOffLowest) != lo) return -10;
+        uint64_t prev = lo;
+        for (int j = 0; j < cnt; ++j) {
+          const uint64_t k = rd64(o + kOffRecords + 16ull * j);
+          const uint64_t c = rd64(o + kOffRecords + 16ull * j + 8);
+          if (k <= prev || k >= hi) return -11;
+          prev = k;
+          co = page_off(c);
+          if (co < 0 || rd64(co + kOffLowest) != k) return -12;
+          if ((int)img[co + kOffLevel] != lvl - 1) return -13;
+        }
+        ++internals;
+      }
+      expect_low = hi;
+      p = rd64(o + kOffSibling);
+    }
+    if (expect_low != kKeyMax) return -14;
+    head = next_head;
+  }
+  if (n_leaves) *n_leaves = leaves;
+  if (n_internal) *n_internal = internals;
+  if (n_keys) *n_keys = keys;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shm_abi_version(void) { return SHM_ABI_VERSION; }
+
+const char* shm_strerror(int s) {
+  switch (s) {
+    case SHM_OK: return "ok";
+    case SHM_EINVAL: return "invalid argument (key == kKeyMax or bad config)";
+    case SHM_ENOMEM: return "page arena or workspace exhausted";
+    case SHM_EIO: return "HIP failure or tree inconsistency";
+    case SHM_EAGAIN: return "optimistic check failed";
+    case SHM_E2BIG: return "batch larger than max_batch";
+    default: return "unknown status";
+  }
+}
+
+int shm_config_init(shm_config* c) {
+  if (!c) return SHM_EINVAL;
+  memset(c, 0, sizeof(*c));
+  c->struct_size = sizeof(shm_config);
+  c->device = 0;
+  c->node_id = 0;
+  c->flags = SHM_FLAG_SORT_GETS;
+  c->arena_bytes = 1ull << 30;
+  c->max_batch = 1ull << 20;
+  c->num_locks = 1u << 16;
+  c->sort_bits = kDefaultSortBits;
+  return SHM_OK;
+}
+
+int shm_tree_create(const shm_config* cfg, shm_tree** out) {
+  if (!cfg || !out || cfg->struct_size != sizeof(shm_config)) return SHM_EINVAL;
+  if (cfg->arena_bytes < 4 * kPageSize || cfg->max_batch == 0 ||
+      cfg->max_batch > (1ull << 31) || cfg->num_locks == 0)
+    return SHM_EINVAL;
+  shm_tree* t = new shm_tree();
+  t->cfg = *cfg;
+  if (!t->cfg.sort_bits || t->cfg.sort_bits > 64) t->cfg.sort_bits = kDefaultSortBits;
+  auto fail = [&](int rc) {
+    free_all(t);
+    delete t;
+    return rc;
+  };
+  if (hipSetDevice(cfg->device) != hipSuccess) return fail(SHM_EIO);
+  if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(SHM_EIO);
+  t->cap_pages = cfg->arena_bytes / kPageSize;
+  t->arena_bytes = t->cap_pages * kPageSize;
+  const uint64_t n = cfg->max_batch;
+  t->nmax = n;
+  t->sep_cap = 2 * n + 1024;
+  const uint64_t segcap = t->sep_cap;
+  int rc = SHM_OK;
+  rc |= dalloc(&t->arena, t->arena_bytes);
+  rc |= dalloc(&t->locks, cfg->num_locks);
+  rc |= dalloc(&t->d_err, 4);
+  rc |= dalloc(&t->d_counts, 16);
+  rc |= dalloc(&t->route_scratch, 256);
+  rc |= dalloc(&t->ka, n);
+  rc |= dalloc(&t->kb, n);
+  rc |= dalloc(&t->ia, n);
+  rc |= dalloc(&t->ib, n);
+  rc |= dalloc(&t->flags, n);
+  rc |= dalloc(&t->pos, n);
+  rc |= dalloc(&t->uk, n);
+  rc |= dalloc(&t->uv, n);
+  rc |= dalloc(&t->dk, n);
+  rc |= dalloc(&t->pages, segcap);
+  rc |= dalloc(&t->heads, segcap);
+  rc |= dalloc(&t->hpos, segcap);
+  rc |= dalloc(&t->seg_start, segcap + 1);
+  rc |= dalloc(&t->seg_page, segcap);
+  rc |= dalloc(&t->seg_T, segcap);
+  rc |= dalloc(&t->seg_P, segcap);
+  rc |= dalloc(&t->seg_np, segcap);
+  rc |= dalloc(&t->seg_pbase, segcap);
+  rc |= dalloc(&t->seg_ver, segcap);
+  for (int i = 0; i < 2; ++i) {
+    rc |= dalloc(&t->sep_key[i], t->sep_cap);
+    rc |= dalloc(&t->sep_ptr[i], t->sep_cap);
+  }
+  if (rc) return fail(SHM_ENOMEM);
+  t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n), dev::scan_temp_bytes(segcap));
+  if (hipMalloc(&t->temp, t->temp_bytes) != hipSuccess) return fail(SHM_ENOMEM);
+  if (hipHostMalloc((void**)&t->h_pin, 4096, 0) != hipSuccess) return fail(SHM_ENOMEM);
+  hipStream_t s = t->stream;
+  if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
+      hipMemsetAsync(t->d_err, 0, 16, s) ||
+      hipMemsetAsync(t->arena, 0, kPageSize, s))
+    return fail(SHM_EIO);
+  // Tree::Tree (Tree.cpp:44-60): empty leaf root
+  t->next_page = 1;
+  const uint64_t root_off = t->next_page * kPageSize;
+  dev::launch_empty_leaf(t->arena, root_off, s);
+  t->next_page += 1;
+  t->root = ga_make(cfg->node_id, root_off);
+  t->root_level = 0;
+  if (write_superblock(t, s)) return fail(SHM_EIO);
+  *out = t;
+  return SHM_OK;
+}
+
+int shm_tree_destroy(shm_tree* t) {
+  if (!t) return SHM_EINVAL;
+  (void)hipSetDevice(t->cfg.device);
+  (void)hipStreamSynchronize(t->stream);
+  free_all(t);
+  delete t;
+  return SHM_OK;
+}
+
+int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
+                     uint64_t* vals_out, uint8_t* found_out, void* stream) {
+  if (!t || (n && (!keys || !vals_out))) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(t, stream);
+  for (uint64_t off = 0; off < n; off += t->nmax) {
+    const uint64_t m = std::min(t->nmax, n - off);
+    dev::WalkArgs a = walk_args(t);
+    a.out_val = vals_out + off;
+    a.out_found = found_out ? found_out + off : nullptr;
+    a.n = m;
+    if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
+      // order the batch by its top key bits so queries that share pages are
+      // walked by the same wave (one page read per group, not per query)
+      dev::launch_iota(t->ia, m, s);
+      HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys + off, t->ka, t->ia,
+                             t->ib, m, 64u - t->cfg.sort_bits, s));
+      a.keys = t->ka;
+      a.perm = t->ib;
+    } else {
+      a.keys = keys + off;
+      a.perm = nullptr;
+    }
+    dev::launch_walk(a, m, kWalkDepth, false, s);
+  }
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_insert_batch(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
+                     uint64_t n, void* stream) {
+  if (!t || (n && (!keys || !vals))) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(t, stream);
+  int rc = SHM_OK;
+  for (uint64_t off = 0; off < n && rc == SHM_OK; off += t->nmax) {
+    const uint64_t m = std::min(t->nmax, n - off);
+    rc = insert_chunk(t, s, keys + off, vals + off, m);
+  }
+  if (rc == SHM_OK) {
+    t->batches += 1;
+    rc = write_superblock(t, s);
+    if (rc == SHM_OK) rc = check_err(t, s);
+  }
+  return rc;
+}
+
+int shm_del_batch(shm_tree* t, const uint64_t* keys, uint64_t n, void* stream) {
+  if (!t || (n && !keys)) return SHM_EINVAL;
+  if (n == 0) return SHM_OK;
+  // deletes are upserts of kValueNull (Tree.cpp:1040-1043)
+  uint64_t* zeros = nullptr;
+  const uint64_t m = std::min<uint64_t>(n, t->nmax);
+  if (hipMalloc((void**)&zeros, m * sizeof(uint64_t)) != hipSuccess) return SHM_ENOMEM;
+  hipStream_t s = pick(t, stream);
+  int rc = SHM_OK;
+  if (hipMemsetAsync(zeros, 0, m * sizeof(uint64_t), s) != hipSuccess) rc = SHM_EIO;
+  for (uint64_t off = 0; off < n && rc == SHM_OK; off += m) {
+    rc = shm_insert_batch(t, keys + off, zeros, std::min(m, n - off), stream);
+  }
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(zeros);
+  return rc;
+}
+
+int shm_range_query(shm_tree* t, const uint64_t* from, const uint64_t* to,
+                    uint64_t n, uint64_t* counts_out, const uint64_t* offsets,
+                    uint64_t* vals_out, void* stream) {
+  if (!t || (n && (!from || !to || !counts_out))) return SHM_EINVAL;
+  if (offsets && !vals_out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(t, stream);
+  dev::launch_range_count(t->arena, t->arena_bytes, t->cfg.node_id, t->root,
+                          from, to, n, counts_out, offsets, vals_out, t->d_err, s);
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_stats(shm_tree* t, shm_stats_t* o) {
+  if (!t || !o) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  memset(o, 0, sizeof(*o));
+  o->root_ptr = t->root;
+  o->root_level = t->root_level;
+  o->height = t->root_level + 1;
+  o->pages_used = t->next_page - 1;
+  o->pages_capacity = t->cap_pages - 1;
+  o->arena_bytes = t->arena_bytes;
+  o->batches = t->batches;
+  o->splits = t->splits;
+  o->last_error = t->sticky_err;
+  return SHM_OK;
+}
+
+int shm_synchronize(shm_tree* t) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  HIP_OK(hipDeviceSynchronize());
+  return check_err(t, t->stream);
+}
+
+int shm_dump_image(shm_tree* t, void* host_buf, uint64_t cap,
+                   uint64_t* bytes_used, uint64_t* root_ptr) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  const uint64_t used = t->next_page * kPageSize;
+  if (bytes_used) *bytes_used = used;
+  if (root_ptr) *root_ptr = t->root;
+  if (!host_buf) return SHM_OK;
+  if (cap < used) return SHM_EINVAL;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(host_buf, t->arena, used, hipMemcpyDeviceToHost));
+  return SHM_OK;
+}
+
+int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
+                   uint64_t root_ptr) {
+  if (!t || !host_buf || bytes < 2 * kPageSize) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  const uint64_t pages = (bytes + kPageSize - 1) / kPageSize;
+  if (pages > t->cap_pages || ga_node(root_ptr) != t->cfg.node_id) return SHM_EINVAL;
+  const uint64_t ro = ga_offset(root_ptr);
+  if (ro < kPageSize || ro + kPageSize > bytes) return SHM_EINVAL;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(t->arena, host_buf, bytes, hipMemcpyHostToDevice));
+  t->root = root_ptr;
+  t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
+  t->next_page = pages;
+  return write_superblock(t, t->stream);
+}
+
+int shm_check(shm_tree* t, uint64_t* n_leaves, uint64_t* n_internal,
+              uint64_t* n_keys) {
+  if (!t) return SHM_EINVAL;
+  uint64_t used = 0, root = 0;
+  int rc = shm_dump_image(t, nullptr, 0, &used, &root);
+  if (rc) return rc;
+  std::vector<uint8_t> img(used);
+  rc = shm_dump_image(t, img.data(), used, &used, &root);
+  if (rc) return rc;
+  rc = check_image(img.data(), used, root, t->cfg.node_id, n_leaves, n_internal, n_keys);
+  if (rc) {
+    fprintf(stderr, "sherman_amd: structural check failed (%d)\n", rc);
+    return SHM_EIO;
+  }
+  return SHM_OK;
+}
+
+int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
+                     uint32_t num_shards, uint64_t* counts_out,
+                     uint64_t* keys_out, uint32_t* perm_out, void* stream) {
+  if (!t || num_shards == 0 || num_shards > 64 || !counts_out) return SHM_EINVAL;
+  if (n && (!keys || !keys_out || !perm_out)) return SHM_EINVAL;
+  if (n > 0xFFFFFFFFull) return SHM_E2BIG;
+  hipStream_t s = pick(t, stream);
+  dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out,
+                           t->route_scratch, s);
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_route_unpermute(shm_tree* t, const uint64_t* in, const uint32_t* perm,
+                        uint64_t n, uint64_t* out, void* stream) {
+  if (!t || (n && (!in || !perm || !out))) return SHM_EINVAL;
+  dev::launch_unpermute(in, perm, n, out, pick(t, stream));
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_gen_keys(shm_tree* t, uint64_t first, uint64_t n, uint64_t keyspace,
+                 uint64_t* keys_out, void* stream) {
+  if (!t || (n && !keys_out)) return SHM_EINVAL;
+  dev::launch_gen_keys(first, n, keyspace, keys_out, pick(t, stream));
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+}  // extern "C"
