@@ -3,7 +3,7 @@
  *
  * Plain C: opaque handle, plain pointers and sizes, int status codes. No HIP,
  * torch or C++ types appear in the signatures (streams are passed as void*,
- * i.e. a hipStream_t cast, NULL = the handle's own stream).
+ * i.e. a hipStream_t cast; NULL = the HIP null/default stream).
  *
  * Every batch entry point takes DEVICE pointers (HBM of the tree's GPU). The
  * host C++ facade (sherman_amd/csrc/Tree.hpp) provides the reference's

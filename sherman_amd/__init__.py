@@ -132,11 +132,14 @@ def _ptr(x):
 
 
 def _stream_ptr(stream):
+    """hipStream_t for the C-ABI; default = torch's current stream so the
+    library is ordered after the torch ops that produced its inputs."""
     if stream is None:
-        return None
+        import torch
+        stream = torch.cuda.current_stream()
     if isinstance(stream, int):
-        return stream
-    return stream.cuda_stream
+        return stream or None
+    return stream.cuda_stream or None
 
 
 class Tree:

@@ -13,7 +13,7 @@ struct WalkArgs {
   uint16_t node;
   uint64_t root;
   const uint64_t* keys;
-  const uint32_t* perm;   // GET: output position of keys[i] (nullable)
+  const uint32_t* perm;   // walk order: query i is keys[perm[i]] (nullable)
   const uint64_t* n_dev;  // device count (nullable -> use n)
   uint64_t n;
   uint64_t* out_val;      // GET
@@ -69,6 +69,9 @@ void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
 
 // ---- utilities (util.hip) -----------------------------------------------------
 void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);
+// out[i] = (uint32_t)(keys[i] >> 32), idx[i] = i
+void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
+                  uint32_t* idx, hipStream_t s);
 // flags[i] = (last of equal-key run) * (v != 0 ? 1 : 1 << 32), key checks
 void launch_mark_unique(const uint64_t* sk, const uint32_t* sidx,
                         const uint64_t* vals, uint64_t n, uint64_t* flags,

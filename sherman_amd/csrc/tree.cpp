@@ -8,6 +8,7 @@
 // taken by: plain HBM pointers, a host-authoritative bump allocator over the
 // arena (mirrored into the superblock in page 0) and a root register.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -88,8 +89,11 @@ int dalloc(T** p, uint64_t count) {
   return SHM_OK;
 }
 
+// stream argument of the C-ABI: NULL is the HIP null (default) stream, as for
+// any HIP API; t->stream is used only for create / image transfers.
 hipStream_t pick(shm_tree* t, void* s) {
-  return s ? (hipStream_t)s : t->stream;
+  (void)t;
+  return (hipStream_t)s;
 }
 
 dev::WalkArgs walk_args(shm_tree* t) {
@@ -120,6 +124,30 @@ dev::SegArgs seg_args(shm_tree* t) {
   a.err = t->d_err;
   return a;
 }
+
+// SHM_DEBUG=1: synchronise after every launch and name the failing step
+bool debug_sync_enabled() {
+  static const int on = [] {
+    const char* e = getenv("SHM_DEBUG");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
+int dbg(hipStream_t s, const char* what) {
+  if (!debug_sync_enabled()) return SHM_OK;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) {
+    fprintf(stderr, "sherman_amd[debug]: %s failed: %s\n", what, hipGetErrorString(e));
+    return SHM_EIO;
+  }
+  return SHM_OK;
+}
+#define DBG(s, what)                   \
+  do {                                 \
+    int _r = dbg((s), (what));         \
+    if (_r) return _r;                 \
+  } while (0)
 
 // read `n` device words into pinned host scratch and wait
 int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
@@ -167,11 +195,13 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   w.out_page = t->pages;
   w.target_level = level;
   dev::launch_walk(w, n_ops, 4, true, s);
+  DBG(s, "walk(locate)");
   dev::launch_seg_heads(t->pages, n_ops, t->heads, s);
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
   dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, t->seg_start,
                        t->seg_page, d_ns, s);
+  DBG(s, "seg_fill");
   int rc = readback(t, s, d_ns, sizeof(uint32_t));
   if (rc) return rc;
   return (int64_t)(uint32_t)t->h_pin[0];
@@ -184,6 +214,7 @@ int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
     dev::launch_leaf_plan(a, s);
   else
     dev::launch_int_plan(a, s);
+  DBG(s, "plan");
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
                                  a.num_seg, s));
   // total = pbase[last] + np[last]
@@ -220,6 +251,7 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   a.sep_ptr = t->sep_ptr[out];
   if (is_delete) {
     dev::launch_leaf_delete(a, s);
+    DBG(s, "leaf_delete");
     return 0;
   }
   const bool leaf = level == 0;
@@ -230,10 +262,14 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   a.first_new_page = t->next_page;
   if (leaf) {
     dev::launch_leaf_build(a, (uint32_t)total, s);
+    DBG(s, "leaf_build");
     dev::launch_leaf_update(a, s);
+    DBG(s, "leaf_update");
   } else {
     dev::launch_int_build(a, (uint32_t)total, s);
+    DBG(s, "int_build");
     dev::launch_int_update(a, s);
+    DBG(s, "int_update");
   }
   t->next_page += (uint64_t)total;
   t->splits += (uint64_t)total;
@@ -244,12 +280,14 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
                  const uint64_t* vals, uint64_t n) {
   // 1. stable sort (key, batch index)
   dev::launch_iota(t->ia, n, s);
-  HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, t->ka, t->ia, t->ib, n, 0, s));
+  HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, t->ka, t->ia, t->ib, n, s));
+  DBG(s, "sort(insert)");
   // 2. keep the last writer of each key; split upserts / deletes
   dev::launch_mark_unique(t->ka, t->ib, vals, n, t->flags, t->d_err, s);
   HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, t->flags, t->pos, n, s));
   dev::launch_compact_unique(t->ka, t->ib, vals, t->flags, t->pos, n, t->uk,
                              t->uv, t->dk, t->d_counts, s);
+  DBG(s, "compact");
   HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
   int rc = readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
   if (rc) return rc;
@@ -276,6 +314,7 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
       if (t->next_page + 1 > t->cap_pages) return SHM_ENOMEM;
       const uint64_t off = t->next_page * kPageSize;
       dev::launch_new_root(t->arena, off, t->root, (uint32_t)level, s);
+      DBG(s, "new_root");
       t->next_page += 1;
       t->root = ga_make(t->cfg.node_id, off);
       t->root_level = (uint32_t)level;
@@ -467,7 +506,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
     rc |= dalloc(&t->sep_ptr[i], t->sep_cap);
   }
   if (rc) return fail(SHM_ENOMEM);
-  t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n), dev::scan_temp_bytes(segcap));
+  t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
+                           dev::scan_temp_bytes_max(segcap));
   if (hipMalloc(&t->temp, t->temp_bytes) != hipSuccess) return fail(SHM_ENOMEM);
   if (hipHostMalloc((void**)&t->h_pin, 4096, 0) != hipSuccess) return fail(SHM_ENOMEM);
   hipStream_t s = t->stream;
@@ -510,16 +550,19 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
-      dev::launch_iota(t->ia, m, s);
-      HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys + off, t->ka, t->ia,
-                             t->ib, m, 64u - t->cfg.sort_bits, s));
-      a.keys = t->ka;
+      uint32_t* k32a = reinterpret_cast<uint32_t*>(t->ka);
+      uint32_t* k32b = reinterpret_cast<uint32_t*>(t->kb);
+      dev::launch_top32(keys + off, m, k32a, t->ia, s);
+      HIP_OK(dev::sort_pairs_u32(t->temp, t->temp_bytes, k32a, k32b, t->ia, t->ib, m, s));
+      a.keys = keys + off;
       a.perm = t->ib;
+      DBG(s, "sort(get)");
     } else {
       a.keys = keys + off;
       a.perm = nullptr;
     }
     dev::launch_walk(a, m, kWalkDepth, false, s);
+    DBG(s, "walk(get)");
   }
   HIP_OK(hipGetLastError());
   return SHM_OK;
@@ -674,3 +717,33 @@ int shm_gen_keys(shm_tree* t, uint64_t first, uint64_t n, uint64_t keyspace,
 }
 
 }  // extern "C"
+
+// ---- internal test hooks (not part of include/sherman_amd.h) ----------------
+extern "C" int shm__debug_sort(shm_tree* t, const uint64_t* keys, uint64_t n,
+                               uint64_t* keys_out, uint32_t* perm_out,
+                               unsigned begin_bit, void* stream) {
+  if (!t || n > t->nmax) return SHM_EINVAL;
+  hipStream_t s = pick(t, stream);
+  (void)begin_bit;
+  dev::launch_iota(t->ia, n, s);
+  HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, keys_out, t->ia, perm_out,
+                         n, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return SHM_OK;
+}
+
+extern "C" int shm__debug_walk(shm_tree* t, const uint64_t* keys,
+                               const uint32_t* perm, uint64_t n, uint64_t* vals,
+                               uint8_t* found, int depth, void* stream) {
+  if (!t) return SHM_EINVAL;
+  hipStream_t s = pick(t, stream);
+  dev::WalkArgs a = walk_args(t);
+  a.keys = keys;
+  a.perm = perm;
+  a.n = n;
+  a.out_val = vals;
+  a.out_found = found;
+  dev::launch_walk(a, n, depth, false, s);
+  HIP_OK(hipStreamSynchronize(s));
+  return SHM_OK;
+}

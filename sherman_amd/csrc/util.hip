@@ -21,6 +21,19 @@ void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, grid1(n), dim3(kT), 0, s, idx, n);
 }
 
+__global__ void k_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
+                        uint32_t* idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    out[i] = (uint32_t)(keys[i] >> 32);
+    idx[i] = (uint32_t)i;
+  }
+}
+void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
+                  uint32_t* idx, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_top32, grid1(n), dim3(kT), 0, s, keys, n, out, idx);
+}
+
 // last occurrence of each key in the (stable) sorted batch wins
 // (last writer in batch order); low word counts upserts, high word deletes.
 __global__ void k_mark_unique(const uint64_t* sk, const uint32_t* sidx,

@@ -28,7 +28,9 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   if (wave_base >= n) return;  // wave-uniform
   const uint64_t i = wave_base + (uint64_t)lane;
   const bool active = i < n;
-  const uint64_t k = active ? a.keys[i] : 0;
+  // query i of the walk is input position perm[i] (key read and output)
+  const uint64_t src = active ? (a.perm ? (uint64_t)a.perm[i] : i) : 0;
+  const uint64_t k = active ? a.keys[src] : 0;
   uint64_t ptr = a.root;
   bool done = !active;
   uint64_t val = 0, page_out = 0;
@@ -179,11 +181,10 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   if (err) atomicOr(a.err, err);
   if (active) {
     if (LOCATE) {
-      a.out_page[i] = page_out;
+      a.out_page[src] = page_out;
     } else {
-      const uint64_t o = a.perm ? (uint64_t)a.perm[i] : i;
-      a.out_val[o] = val;
-      if (a.out_found) a.out_found[o] = fnd ? 1 : 0;
+      a.out_val[src] = val;
+      if (a.out_found) a.out_found[src] = fnd ? 1 : 0;
     }
   }
 }

@@ -56,6 +56,14 @@ def lib_ok():
     return True
 
 
+def assert_same(probe, ov, of, gv, gf):
+    bad = np.nonzero((of != gf) | (ov != gv))[0]
+    if bad.size:
+        lines = [f"key={int(probe[i]):#x} oracle=({of[i]},{int(ov[i])}) gpu=({gf[i]},{int(gv[i])})"
+                 for i in bad[:8]]
+        raise AssertionError(f"{bad.size} mismatches:\n" + "\n".join(lines))
+
+
 def compare_contents(tree, orc):
     ok, ov = orc.dump()
     order = np.argsort(ok)
@@ -136,7 +144,7 @@ def test_random_batches_vs_oracle(lib_ok, batch):
     probe = np.concatenate([universe, hashed_keys(30001, 31001)])
     ov, of = orc.search_batch(probe)
     gv, gf = gpu_search(t, probe)
-    assert np.array_equal(of, gf) and np.array_equal(ov, gv)
+    assert_same(probe, ov, of, gv, gf)
     assert orc.check()[0] == 0
     t.close()
 
@@ -170,7 +178,7 @@ def test_image_conformance_oracle_to_gpu(lib_ok):
     probe = np.concatenate([ks, hashed_keys(200001, 210001)])
     ov, of = orc.search_batch(probe)
     gv, gf = gpu_search(t, probe)
-    assert np.array_equal(of, gf) and np.array_equal(ov, gv)
+    assert_same(probe, ov, of, gv, gf)
     # and the GPU can keep inserting into the reference-built tree
     more = hashed_keys(150001, 170001)
     gpu_insert(t, more, more)
@@ -193,7 +201,7 @@ def test_image_conformance_gpu_to_oracle(lib_ok):
     probe = np.concatenate([ks, hashed_keys(900001, 905001)])
     ov, of = orc.search_batch(probe)
     gv, gf = gpu_search(t, probe)
-    assert np.array_equal(of, gf) and np.array_equal(ov, gv)
+    assert_same(probe, ov, of, gv, gf)
     t.close()
 
 
@@ -312,5 +320,5 @@ def test_uniform_get_large_vs_oracle(lib_ok):
     probe = np.array([to_key(int(i)) for i in idx[:200000]], dtype=U64)
     ov, of = orc.search_batch(probe)
     gv, gf = gpu_search(t, probe)
-    assert np.array_equal(of, gf) and np.array_equal(ov, gv)
+    assert_same(probe, ov, of, gv, gf)
     t.close()
