@@ -120,6 +120,18 @@ int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
               uint64_t *n_keys);
 int shm_synchronize(shm_tree *t);
 
+/* per-kernel timing with HIP events recorded on the launch stream around the
+ * get path's phases (order = top-bits sort, walk = the page walk kernel).
+ * Enabled handles pay two event records per phase per call. */
+typedef struct shm_profile_t {
+  uint64_t calls;       /* search_batch calls (chunks) timed */
+  uint64_t queries;     /* queries in those calls */
+  double order_ms;      /* sum of ordering (top32 + radix sort) time */
+  double walk_ms;       /* sum of k_walk kernel time */
+} shm_profile_t;
+int shm_profile_enable(shm_tree *t, int on);
+int shm_profile_read(shm_tree *t, shm_profile_t *out, int reset);
+
 /* multi-GPU routing helpers (range shards: shard s owns
  * [s * 2^64 / P, (s+1) * 2^64 / P)) ------------------------------------------ */
 /* Bucket n keys by owning shard: writes per-shard counts[P], the keys grouped

@@ -71,6 +71,15 @@ class ShermanError(RuntimeError):
         super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
 
 
+class ShmProfile(ctypes.Structure):
+    _fields_ = [
+        ("calls", u64),
+        ("queries", u64),
+        ("order_ms", ctypes.c_double),
+        ("walk_ms", ctypes.c_double),
+    ]
+
+
 _lib = None
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
@@ -89,6 +98,8 @@ _SIGNATURES = [
     ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
     ("shm_check", ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_synchronize", ctypes.c_int, [vp]),
+    ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
+    ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
@@ -267,6 +278,15 @@ class Tree:
         image = np.ascontiguousarray(image, dtype=np.uint8)
         _check(lib().shm_load_image(self.h, image.ctypes.data_as(vp), image.nbytes,
                                     root_ptr), "load_image")
+
+    def profile(self, on=True):
+        _check(lib().shm_profile_enable(self.h, 1 if on else 0), "profile_enable")
+
+    def profile_read(self, reset=True):
+        p = ShmProfile()
+        _check(lib().shm_profile_read(self.h, ctypes.byref(p), 1 if reset else 0),
+               "profile_read")
+        return {f: getattr(p, f) for f, _ in ShmProfile._fields_}
 
     # -- routing / generators ---------------------------------------------------
     def route_bucket(self, keys, num_shards, keys_out, perm_out, counts_out, stream=None):

@@ -65,6 +65,15 @@ struct shm_tree {
   void* temp = nullptr;
   size_t temp_bytes = 0;
   std::mutex mu;
+  // profiling (shm_profile_*)
+  bool prof_on = false;
+  struct ProfRec {
+    hipEvent_t e0, e1, e2;
+    uint64_t n;
+  };
+  std::vector<ProfRec> prof_pending;
+  std::vector<hipEvent_t> event_pool;
+  shm_profile_t prof_acc{};
 };
 
 namespace {
@@ -329,6 +338,36 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
   return SHM_OK;
 }
 
+hipEvent_t take_event(shm_tree* t) {
+  if (!t->event_pool.empty()) {
+    hipEvent_t e = t->event_pool.back();
+    t->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// fold finished event triples into the accumulator
+int drain_profile(shm_tree* t) {
+  for (auto& r : t->prof_pending) {
+    HIP_OK(hipEventSynchronize(r.e2));
+    float a = 0.f, b = 0.f;
+    HIP_OK(hipEventElapsedTime(&a, r.e0, r.e1));
+    HIP_OK(hipEventElapsedTime(&b, r.e1, r.e2));
+    t->prof_acc.calls += 1;
+    t->prof_acc.queries += r.n;
+    t->prof_acc.order_ms += a;
+    t->prof_acc.walk_ms += b;
+    t->event_pool.push_back(r.e0);
+    t->event_pool.push_back(r.e1);
+    t->event_pool.push_back(r.e2);
+  }
+  t->prof_pending.clear();
+  return SHM_OK;
+}
+
 void free_all(shm_tree* t) {
   auto F = [](void* p) {
     if (p) (void)hipFree(p);
@@ -340,6 +379,8 @@ void free_all(shm_tree* t) {
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
   F(t->temp);
+  for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
+  for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
 }
@@ -547,6 +588,14 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     a.out_val = vals_out + off;
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
+    shm_tree::ProfRec pr{nullptr, nullptr, nullptr, m};
+    if (t->prof_on) {
+      pr.e0 = take_event(t);
+      pr.e1 = take_event(t);
+      pr.e2 = take_event(t);
+      if (!pr.e0 || !pr.e1 || !pr.e2) return SHM_EIO;
+      HIP_OK(hipEventRecord(pr.e0, s));
+    }
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
@@ -561,8 +610,13 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.keys = keys + off;
       a.perm = nullptr;
     }
+    if (t->prof_on) HIP_OK(hipEventRecord(pr.e1, s));
     dev::launch_walk(a, m, kWalkDepth, false, s);
     DBG(s, "walk(get)");
+    if (t->prof_on) {
+      HIP_OK(hipEventRecord(pr.e2, s));
+      t->prof_pending.push_back(pr);
+    }
   }
   HIP_OK(hipGetLastError());
   return SHM_OK;
@@ -684,6 +738,23 @@ int shm_check(shm_tree* t, uint64_t* n_leaves, uint64_t* n_internal,
     fprintf(stderr, "sherman_amd: structural check failed (%d)\n", rc);
     return SHM_EIO;
   }
+  return SHM_OK;
+}
+
+int shm_profile_enable(shm_tree* t, int on) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  t->prof_on = on != 0;
+  return SHM_OK;
+}
+
+int shm_profile_read(shm_tree* t, shm_profile_t* out, int reset) {
+  if (!t || !out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  int rc = drain_profile(t);
+  if (rc) return rc;
+  *out = t->prof_acc;
+  if (reset) t->prof_acc = shm_profile_t{};
   return SHM_OK;
 }
 

@@ -221,12 +221,17 @@ def test_range_query_vs_oracle(lib_ok):
     counts, vals = t.range_query_batch(dev(lo), dev(hi))
     counts = counts.cpu().numpy()
     vals = host(vals)
+    # exact order (leaf order, then slot order) is a property of the page
+    # image: check it with the reference scan over the GPU's own pages
+    img, root = t.dump_image()
+    same_pages = OracleTree(image=img, root_ptr=root)
     off = 0
     for i in range(lo.size):
         ref, n = orc.range_query(int(lo[i]), int(hi[i]), cap=60000)
         assert counts[i] == n
         assert np.array_equal(np.sort(vals[off:off + n]), np.sort(ref))
-        assert np.array_equal(vals[off:off + n], ref)  # leaf then slot order
+        ref_img, n_img = same_pages.range_query(int(lo[i]), int(hi[i]), cap=60000)
+        assert n_img == n and np.array_equal(vals[off:off + n], ref_img)
         off += n
     t.close()
 
