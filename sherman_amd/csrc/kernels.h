@@ -13,7 +13,7 @@ struct WalkArgs {
   uint16_t node;
   uint64_t root;
   const uint64_t* keys;
-  const uint32_t* perm;   // walk order: query i is keys[perm[i]] (nullable)
+  const uint32_t* perm;   // output position of walk query i (nullable)
   const uint64_t* n_dev;  // device count (nullable -> use n)
   uint64_t n;
   uint64_t* out_val;      // GET
@@ -69,6 +69,14 @@ void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
 
 // ---- utilities (util.hip) -----------------------------------------------------
 void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);
+// bucket a get batch by its top kPartBits key bits: out_keys in bucket order,
+// out_perm[j] = input position of out_keys[j]
+constexpr int kPartBits = 14;
+constexpr int kPartBuckets = 1 << kPartBits;
+constexpr int kPartTile = 16384;
+void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* gh,
+                      uint32_t* tot, uint64_t* out_keys, uint32_t* out_perm,
+                      hipStream_t s);
 // out[i] = (uint32_t)(keys[i] >> 32), idx[i] = i
 void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
                   uint32_t* idx, hipStream_t s);

@@ -26,8 +26,8 @@ using namespace shm;
 namespace {
 
 constexpr uint64_t kSortMinGets = 8192;   // below this, walk in input order
-constexpr uint32_t kDefaultSortBits = 24; // top key bits that order gets
-constexpr int kWalkDepth = 8;             // pages in flight per wave
+constexpr uint32_t kDefaultSortBits = 14; // top key bits that bucket gets
+constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
 
 }  // namespace
 
@@ -64,6 +64,8 @@ struct shm_tree {
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   void* temp = nullptr;
   size_t temp_bytes = 0;
+  uint32_t* part_hist = nullptr;  // [tiles][kPartBuckets]
+  uint32_t* part_tot = nullptr;   // [kPartBuckets]
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
@@ -378,7 +380,7 @@ void free_all(shm_tree* t) {
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
-  F(t->temp);
+  F(t->temp); F(t->part_hist); F(t->part_tot);
   for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -546,6 +548,9 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);
     rc |= dalloc(&t->sep_ptr[i], t->sep_cap);
   }
+  rc |= dalloc(&t->part_hist, ((n + dev::kPartTile - 1) / dev::kPartTile) *
+                                 (uint64_t)dev::kPartBuckets);
+  rc |= dalloc(&t->part_tot, dev::kPartBuckets);
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
@@ -599,11 +604,9 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
-      uint32_t* k32a = reinterpret_cast<uint32_t*>(t->ka);
-      uint32_t* k32b = reinterpret_cast<uint32_t*>(t->kb);
-      dev::launch_top32(keys + off, m, k32a, t->ia, s);
-      HIP_OK(dev::sort_pairs_u32(t->temp, t->temp_bytes, k32a, k32b, t->ia, t->ib, m, s));
-      a.keys = keys + off;
+      dev::launch_partition(keys + off, m, t->part_hist, t->part_tot, t->ka,
+                            t->ib, s);
+      a.keys = t->ka;
       a.perm = t->ib;
       DBG(s, "sort(get)");
     } else {
