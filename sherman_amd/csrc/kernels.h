@@ -69,14 +69,18 @@ void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
 
 // ---- utilities (util.hip) -----------------------------------------------------
 void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);
-// bucket a get batch by its top kPartBits key bits: out_keys in bucket order,
-// out_perm[j] = input position of out_keys[j]
+// bucket a get batch by its top kPartBits key bits (partition.hip):
+// out_keys in bucket order, pos_of[i] = where input i was placed
 constexpr int kPartBits = 14;
 constexpr int kPartBuckets = 1 << kPartBits;
 constexpr int kPartTile = 16384;
 void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* gh,
-                      uint32_t* tot, uint64_t* out_keys, uint32_t* out_perm,
+                      uint32_t* tot, uint64_t* out_keys, uint32_t* pos_of,
                       hipStream_t s);
+// vals_out[i] = res[pos_of[i]], found_out[i] = res != 0
+void launch_gather_results(const uint64_t* res, const uint32_t* pos_of,
+                           uint64_t n, uint64_t* vals_out, uint8_t* found_out,
+                           hipStream_t s);
 // out[i] = (uint32_t)(keys[i] >> 32), idx[i] = i
 void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
                   uint32_t* idx, hipStream_t s);

@@ -593,6 +593,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     a.out_val = vals_out + off;
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
+    bool gathered = false;
     shm_tree::ProfRec pr{nullptr, nullptr, nullptr, m};
     if (t->prof_on) {
       pr.e0 = take_event(t);
@@ -604,10 +605,15 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
+      // walk results land contiguously in walk order (kb) and are gathered
+      // back to input order afterwards: no scattered 8-byte stores
       dev::launch_partition(keys + off, m, t->part_hist, t->part_tot, t->ka,
                             t->ib, s);
       a.keys = t->ka;
-      a.perm = t->ib;
+      a.perm = nullptr;
+      a.out_val = t->kb;
+      a.out_found = nullptr;
+      gathered = true;
       DBG(s, "sort(get)");
     } else {
       a.keys = keys + off;
@@ -619,6 +625,11 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if (t->prof_on) {
       HIP_OK(hipEventRecord(pr.e2, s));
       t->prof_pending.push_back(pr);
+    }
+    if (gathered) {
+      dev::launch_gather_results(t->kb, t->ib, m, vals_out + off,
+                                 found_out ? found_out + off : nullptr, s);
+      DBG(s, "gather");
     }
   }
   HIP_OK(hipGetLastError());

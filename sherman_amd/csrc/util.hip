@@ -34,92 +34,6 @@ void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
   if (n) hipLaunchKernelGGL(k_top32, grid1(n), dim3(kT), 0, s, keys, n, out, idx);
 }
 
-// ---- get-batch bucketing by the top kPartBits key bits ------------------------
-// (hand-written MSD partition: per-tile LDS histograms, a column scan over
-// tiles, a scan over buckets, then a scatter whose LDS cursors start at each
-// tile's slice of each bucket; order inside a bucket is unspecified)
-__global__ __launch_bounds__(kT) void k_part_hist(const uint64_t* keys, uint64_t n,
-                                                  uint32_t* gh) {
-  __shared__ uint32_t h[kPartBuckets];
-  for (int b = threadIdx.x; b < kPartBuckets; b += kT) h[b] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kPartTile;
-  const uint64_t end = base + kPartTile < n ? base + kPartTile : n;
-  for (uint64_t i = base + threadIdx.x; i < end; i += kT)
-    atomicAdd(&h[keys[i] >> (64 - kPartBits)], 1u);
-  __syncthreads();
-  uint32_t* g = gh + (uint64_t)blockIdx.x * kPartBuckets;
-  for (int b = threadIdx.x; b < kPartBuckets; b += kT) g[b] = h[b];
-}
-__global__ void k_part_colscan(uint32_t* gh, uint32_t tiles, uint32_t* tot) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= (uint32_t)kPartBuckets) return;
-  uint32_t acc = 0;
-  for (uint32_t t = 0; t < tiles; ++t) {
-    const uint64_t o = (uint64_t)t * kPartBuckets + b;
-    const uint32_t v = gh[o];
-    gh[o] = acc;
-    acc += v;
-  }
-  tot[b] = acc;
-}
-// exclusive scan of kPartBuckets totals by one 1024-thread block
-__global__ __launch_bounds__(1024) void k_part_bscan(uint32_t* tot) {
-  constexpr int per = kPartBuckets / 1024;
-  __shared__ uint32_t s[1024];
-  uint32_t v[per];
-  uint32_t sum = 0;
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    v[j] = tot[t * per + j];
-    sum += v[j];
-  }
-  s[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const uint32_t x = t >= off ? s[t - off] : 0;
-    __syncthreads();
-    s[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = s[t] - sum;
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    tot[t * per + j] = run;
-    run += v[j];
-  }
-}
-__global__ __launch_bounds__(kT) void k_part_scatter(const uint64_t* keys, uint64_t n,
-                                                     const uint32_t* gh,
-                                                     const uint32_t* bbase,
-                                                     uint64_t* out_keys,
-                                                     uint32_t* out_perm) {
-  __shared__ uint32_t c[kPartBuckets];
-  const uint32_t* g = gh + (uint64_t)blockIdx.x * kPartBuckets;
-  for (int b = threadIdx.x; b < kPartBuckets; b += kT) c[b] = bbase[b] + g[b];
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kPartTile;
-  const uint64_t end = base + kPartTile < n ? base + kPartTile : n;
-  for (uint64_t i = base + threadIdx.x; i < end; i += kT) {
-    const uint64_t k = keys[i];
-    const uint32_t pos = atomicAdd(&c[k >> (64 - kPartBits)], 1u);
-    out_keys[pos] = k;
-    out_perm[pos] = (uint32_t)i;
-  }
-}
-void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* gh,
-                      uint32_t* tot, uint64_t* out_keys, uint32_t* out_perm,
-                      hipStream_t s) {
-  if (!n) return;
-  const uint32_t tiles = (uint32_t)((n + kPartTile - 1) / kPartTile);
-  hipLaunchKernelGGL(k_part_hist, dim3(tiles), dim3(kT), 0, s, keys, n, gh);
-  hipLaunchKernelGGL(k_part_colscan, dim3(kPartBuckets / kT), dim3(kT), 0, s, gh, tiles, tot);
-  hipLaunchKernelGGL(k_part_bscan, dim3(1), dim3(1024), 0, s, tot);
-  hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(kT), 0, s, keys, n, gh, tot,
-                     out_keys, out_perm);
-}
-
 // last occurrence of each key in the (stable) sorted batch wins
 // (last writer in batch order); low word counts upserts, high word deletes.
 __global__ void k_mark_unique(const uint64_t* sk, const uint32_t* sidx,
