@@ -1,0 +1,21 @@
+"""Average each counter per dispatch for the get-path kernels of a pmc.sh run."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d = sys.argv[1]
+agg = collections.defaultdict(list)
+for p in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
+    for r in csv.DictReader(open(p)):
+        n = r["Kernel_Name"]
+        for tag in ("k_walk<false>", "k_part_hist", "k_part_scatter", "k_gather_results",
+                    "k_part_colscan"):
+            if tag in n:
+                agg[(tag, r["Counter_Name"])].append(float(r["Counter_Value"]))
+out = collections.defaultdict(dict)
+for (k, c), v in sorted(agg.items()):
+    out[k][c] = sum(v) / len(v)
+print(json.dumps(out, indent=1))
