@@ -3,23 +3,24 @@
 //
 // Restates src/Tree.cpp:405-459 (search), 593-663 (page_search),
 // 665-685 (internal_page_search) and 687-697 (leaf_page_search) for a batch.
-// One wave64 owns 64 queries (one per lane).  Each round the wave lists the
-// distinct pages its unfinished queries wait on, streams them through a
-// per-wave ring of kRing 1 KB LDS slots with one global_load_lds_dwordx4 per
-// page (LDS-DMA: the page never occupies VGPRs; kRing pages in flight per
-// wave), and resolves every waiting query against the staged page:
-//   * fences first (k >= highest -> sibling, the B-link "turn right",
-//     Tree.cpp:626-629 / 648-651), page versions (front == rear, else re-read,
-//     Tree.cpp:616-618);
-//   * internal page: child = #keys <= k (Tree.cpp:665-685).  A page shared by
-//     few queries uses the lane-parallel compare + ballot per query; a page
-//     shared by many (the upper levels of a sorted batch) lets every query
-//     lane run a fixed 6-step branchless search over the staged keys, which
-//     costs the same instructions for 64 queries as for one;
-//   * leaf page: lane i holds entry i; slot = ffs(ballot(key_i == k &&
-//     value_i != 0 && f_i == r_i)) (Tree.cpp:687-697), once per distinct key.
-// Queries that share a page (the batch is bucketed by key first) share one
-// page read.
+//
+// One wave64 owns 64 queries.  It first sorts them by key across its lanes
+// (bitonic, in registers), so at every level the queries that wait on the
+// same page occupy a contiguous run of lanes: the pages of a round are the run
+// heads, one ballot away, with no per-page matching loop.  The round's pages
+// stream through a per-wave ring of kRing 1 KB LDS slots, one
+// global_load_lds_dwordx4 per page (LDS-DMA: pages never occupy VGPRs;
+// kRing - 1 pages stay in flight while one is resolved).  Header fields are
+// read with uniform-address LDS loads into (uniform) VGPRs, so fences and
+// versions are checked by each query lane itself:
+//   * k >= highest -> sibling, the B-link "turn right" (Tree.cpp:626-629,
+//     648-651); front != rear -> re-read next round (Tree.cpp:616-618);
+//   * internal page: child = #keys <= k (Tree.cpp:665-685) by a fixed 6-step
+//     branchless search over the staged keys in every waiting lane at once;
+//   * leaf page: lane i holds entry i and one ballot per distinct key gives
+//     slot = ffs(key_i == k && value_i != 0 && f_i == r_i) (Tree.cpp:687-697).
+// The batch arrives bucketed by key (partition.hip), so the queries of a wave
+// share their internal pages and same-leaf queries share one leaf read.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -31,8 +32,7 @@ namespace dev {
 
 namespace {
 
-constexpr int kRing = 4;           // LDS page slots per wave
-constexpr int kBallotQueries = 2;  // <= this many queries: ballot per query
+constexpr int kRing = 4;  // LDS page slots per wave
 
 // One page -> one LDS slot: global_load_lds_dwordx4, lane l's 16 bytes land
 // at slot + 16 l.  Issued from inline asm on purpose: hipcc treats a visible
@@ -56,26 +56,32 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// header (Tree.h:130-160) + versions from a staged page
-__device__ __forceinline__ Hdr lds_hdr(const uint32_t* lp) {
-  const int l = lane_id();
-  const uint32_t v = l < 11 ? lp[l] : (l == 11 ? lp[254] : lp[255]);
-  const uint32_t a2 = rl32(v, 2), a3 = rl32(v, 3);
-  const uint32_t b0 = rl32(v, 4), b1 = rl32(v, 5), b2 = rl32(v, 6), b3 = rl32(v, 7);
-  const uint32_t c0 = rl32(v, 8), c1 = rl32(v, 9), c2 = rl32(v, 10);
-  const uint32_t z2 = rl32(v, 11), z3 = rl32(v, 12);
-  Hdr h;
-  h.fver = a2 & 0xFF;
-  h.leftmost = (uint64_t)((a2 >> 8) | (a3 << 24)) |
-               ((uint64_t)((a3 >> 8) | (b0 << 24)) << 32);
-  h.sibling = (uint64_t)((b0 >> 8) | (b1 << 24)) |
-              ((uint64_t)((b1 >> 8) | (b2 << 24)) << 32);
-  h.level = (b2 >> 8) & 0xFF;
-  h.last_index = (int32_t)(int16_t)(b2 >> 16);
-  h.lowest = (uint64_t)b3 | ((uint64_t)c0 << 32);
-  h.highest = (uint64_t)c1 | ((uint64_t)c2 << 32);
-  h.rver_internal = z3 & 0xFF;
-  h.rver_leaf = z2 & 0xFF;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Header (Tree.h:130-160) + page versions as uniform VGPR values, from three
+// uniform-address 16-byte LDS loads and one 8-byte load.
+struct UHdr {
+  uint64_t leftmost, sibling, lowest, highest;
+  uint32_t level, fver, rver;
+  int32_t cnt;
+};
+__device__ __forceinline__ UHdr uniform_hdr(const uint32_t* lp) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(lp);       // dwords 0..3
+  const u32x4 b = *reinterpret_cast<const u32x4*>(lp + 4);   // dwords 4..7
+  const u32x4 c = *reinterpret_cast<const u32x4*>(lp + 8);   // dwords 8..11
+  const u32x2 z = *reinterpret_cast<const u32x2*>(lp + 254); // 254..255
+  UHdr h;
+  h.fver = a.z & 0xFF;
+  h.leftmost = (uint64_t)((a.z >> 8) | (a.w << 24)) |
+               ((uint64_t)((a.w >> 8) | (b.x << 24)) << 32);
+  h.sibling = (uint64_t)((b.x >> 8) | (b.y << 24)) |
+              ((uint64_t)((b.y >> 8) | (b.z << 24)) << 32);
+  h.level = (b.z >> 8) & 0xFF;
+  h.cnt = (int32_t)(int16_t)(b.z >> 16) + 1;
+  h.lowest = (uint64_t)b.w | ((uint64_t)c.x << 32);
+  h.highest = (uint64_t)c.y | ((uint64_t)c.z << 32);
+  // rear version: byte 1016 (leaf) or 1020 (internal)
+  h.rver = h.leftmost == 0 ? (z.x & 0xFF) : (z.y & 0xFF);
   return h;
 }
 
@@ -98,13 +104,17 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   const uint64_t wave_base =
       ((uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv) * kWave;
   if (wave_base >= n) return;  // wave-uniform
-  const uint64_t i = wave_base + (uint64_t)lane;
-  const bool active = i < n;
-  const uint64_t k = active ? a.keys[i] : 0;
+  const uint32_t nact = (uint32_t)(n - wave_base < (uint64_t)kWave ? n - wave_base : kWave);
+
+  // sort this wave's queries by key; tag = lane the query came from
+  uint64_t k = (uint32_t)lane < nact ? a.keys[wave_base + lane] : kKeyMax;
+  uint32_t tag = (uint32_t)lane;
+  wave_sort64(k, tag);
+  const bool active = tag < nact;
+
   uint64_t ptr = a.root;
   bool done = !active;
   uint64_t val = 0, page_out = 0;
-  bool fnd = false;
   // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
   if (!LOCATE && k == kKeyMax) done = true;
   uint32_t* ring = &s_ring[wv][0][0];
@@ -118,22 +128,22 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
       err |= kErrRounds;
       break;
     }
-    // ---- distinct pages of this round: lane j holds the j-th -------------
-    uint64_t plist = 0;
-    int m = 0;
-    for (uint64_t rem = pend; rem;) {
-      const uint64_t p = rl64(ptr, ctz64(rem));
-      rem &= ~ballot(!done && ptr == p);
-      if (lane == m) plist = p;
-      ++m;
-    }
+    // run heads: first lane of each run of equal page pointers
+    const int pl = lane == 0 ? 0 : lane - 1;
+    const uint64_t prev = shfl64(ptr, pl);
+    const bool prev_pend = ((pend >> pl) & 1) != 0;
+    const bool head = !done && (lane == 0 || !prev_pend || prev != ptr);
+    uint64_t hq = ballot(head);  // heads still to resolve
+    uint64_t hi = hq;            // heads still to load
+    const int m = popc64(hq);
     // invalid pointers load the superblock (always mapped) and are rejected
-    // when processed, so every slot sees exactly one DMA
-    const bool pbad = lane < m && !ptr_ok(plist, a.node, a.arena_bytes);
-    const uint64_t pload = pbad ? 0 : plist;
+    // when resolved, so every slot sees exactly one DMA
+    const uint64_t pload = ptr_ok(ptr, a.node, a.arena_bytes) ? ptr : 0;
     const int pre = m < kRing ? m : kRing;
-    for (int j = 0; j < pre; ++j)
-      glds16(a.arena + ga_offset(rl64(pload, j)), ring + j * kPageDwords);
+    for (int j = 0; j < pre; ++j) {
+      glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))), ring + j * kPageDwords);
+      hi &= hi - 1;
+    }
 
     for (int j = 0; j < m; ++j) {
       if (j + kRing <= m)
@@ -141,140 +151,92 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
       else
         wait_vm<0>();
       const uint32_t* lp = ring + (j % kRing) * kPageDwords;
-      const uint64_t pj = rl64(plist, j);
-      uint64_t qm = ballot(!done && ptr == pj);
+      const int hl = ctz64(hq);
+      hq &= hq - 1;
+      const uint64_t pj = rl64(ptr, hl);
+      const bool mine = !done && ptr == pj;
       if (!ptr_ok(pj, a.node, a.arena_bytes)) {
-        if (ptr == pj) done = true;
+        if (mine) done = true;
         err |= kErrBadPtr;
-      } else if (qm) {
-        const Hdr h = lds_hdr(lp);
+      } else {
+        const UHdr h = uniform_hdr(lp);
         const bool is_leaf = h.leftmost == 0;
-        const uint32_t rv = is_leaf ? h.rver_leaf : h.rver_internal;
-        const bool mine = !done && ptr == pj;
-        if (h.fver != rv) {
-          // torn / in-flight page: the queries re-list it next round
+        if (h.fver != h.rver) {
+          // torn / in-flight page: its queries re-list it next round
           if (++retries > kMaxRetries) {
             if (mine) done = true;
             err |= kErrInconsistent;
           }
+        } else if (mine && k >= h.highest) {
+          ptr = h.sibling;  // turn right
+          if (ptr == 0) done = true;
+        } else if (mine && k < h.lowest) {
+          ptr = a.root;  // stale route: restart (Tree.cpp:652-657)
+          err |= kErrFence;
         } else if (LOCATE && (int)h.level == a.target_level) {
           if (mine) {
-            if (k >= h.highest) {
-              ptr = h.sibling;
-              if (ptr == 0) done = true;
-            } else if (k < h.lowest) {
-              done = true;
-              err |= kErrFence;
-            } else {
-              page_out = pj;
-              done = true;
-            }
+            page_out = pj;
+            done = true;
           }
         } else if (!is_leaf) {
-          const int cnt = h.last_index + 1;
           if (LOCATE && (int)h.level < a.target_level) {
-            if (mine) done = true;
-            err |= kErrFence;
-          } else if (popc64(qm) <= kBallotQueries) {
-            // lane-parallel compare, ballot child select per query
-            const int jr = lane - 3;
-            const bool valid = jr >= 0 && jr < cnt;
-            const uint64_t rk = valid ? lds_ikey(lp, jr) : 0;
-            while (qm) {
-              const int q = ctz64(qm);
-              qm &= qm - 1;
-              const uint64_t kq = rl64(k, q);
-              uint64_t np;
-              bool bad = false;
-              if (kq >= h.highest) {
-                np = h.sibling;
-              } else if (kq < h.lowest) {
-                np = a.root;  // stale route: restart (Tree.cpp:652-657)
-                bad = true;
-              } else {
-                const int c = popc64(ballot(valid && rk <= kq));
-                np = c == 0 ? h.leftmost : lds_iptr(lp, c - 1);
-              }
-              if (lane == q) {
-                ptr = np;
-                if (np == 0) done = true;
-                if (bad) err |= kErrFence;
-              }
+            if (mine) {
+              done = true;
+              err |= kErrFence;
             }
           } else if (mine) {
-            // many queries: each lane runs a branchless 6-step search
-            if (k >= h.highest) {
-              ptr = h.sibling;
-              if (ptr == 0) done = true;
-            } else if (k < h.lowest) {
-              ptr = a.root;
-              err |= kErrFence;
-            } else {
-              int pos = 0;  // number of keys <= k
+            int pos = 0;  // number of keys <= k (keys strictly increase)
 #pragma unroll
-              for (int step = 32; step > 0; step >>= 1) {
-                const int idx = pos + step - 1;
-                if (idx < cnt && lds_ikey(lp, idx) <= k) pos += step;
-              }
-              ptr = pos == 0 ? h.leftmost : lds_iptr(lp, pos - 1);
-              if (ptr == 0) done = true;
+            for (int step = 32; step > 0; step >>= 1) {
+              const int idx = pos + step - 1;
+              if (idx < h.cnt && lds_ikey(lp, idx) <= k) pos += step;
             }
+            ptr = pos == 0 ? h.leftmost : lds_iptr(lp, pos - 1);
+            if (ptr == 0) done = true;
+          }
+        } else if (LOCATE) {
+          if (mine) {  // reached a leaf below the target level
+            done = true;
+            err |= kErrFence;
           }
         } else {
           // leaf (level 0): lane i holds entry i
           const LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
           const bool ok = lane < kLeafCardinality && e.val != kValueNull &&
                           (e.fraw & 0xF) == (e.rraw & 0xF);
+          // waiting queries are a sorted run: one ballot per distinct key
+          uint64_t qm = ballot(mine);
           while (qm) {
             const uint64_t kq = rl64(k, ctz64(qm));
-            const uint64_t same = ballot(!done && ptr == pj && k == kq);
+            const uint64_t same = ballot(mine && k == kq);
             qm &= ~same;
-            const bool me = (same >> lane) & 1;
-            if (kq >= h.highest) {
-              if (me) {
-                ptr = h.sibling;
-                if (ptr == 0) done = true;
-              }
-            } else if (kq < h.lowest) {
-              if (me) {
-                done = true;
-                err |= kErrFence;
-              }
-            } else if (LOCATE) {
-              if (me) {  // reached a leaf below the target level
-                done = true;
-                err |= kErrFence;
-              }
-            } else {
-              const uint64_t mm = ballot(ok && e.key == kq);
-              uint64_t v = 0;
-              if (mm) v = rl64(e.val, ctz64(mm));
-              if (me) {
-                done = true;
-                if (mm) {
-                  val = v;
-                  fnd = true;
-                }
-              }
+            const uint64_t mm = ballot(ok && e.key == kq);
+            const uint64_t v = mm ? rl64(e.val, ctz64(mm)) : 0;
+            if ((same >> lane) & 1) {
+              done = true;
+              val = v;
             }
           }
         }
       }
       // the slot's LDS reads are complete before its next DMA lands
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (j + kRing < m)
-        glds16(a.arena + ga_offset(rl64(pload, j + kRing)),
+      if (hi) {
+        glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))),
                ring + (j % kRing) * kPageDwords);
+        hi &= hi - 1;
+      }
     }
   }
   if (err) atomicOr(a.err, err);
   if (active) {
+    const uint64_t i = wave_base + tag;
     const uint64_t o = a.perm ? (uint64_t)a.perm[i] : i;
     if (LOCATE) {
       a.out_page[o] = page_out;
     } else {
       a.out_val[o] = val;
-      if (a.out_found) a.out_found[o] = fnd ? 1 : 0;
+      if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
     }
   }
 }
