@@ -211,10 +211,8 @@ __device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& tag) {
       const bool up = (l & k) == 0;
       const bool lower = (l & j) == 0;
       const bool take = lower == up ? (pk < key) : (pk > key);
-      if (take) {
-        key = pk;
-        tag = pt;
-      }
+      key = take ? pk : key;
+      tag = take ? pt : tag;
     }
   }
 }

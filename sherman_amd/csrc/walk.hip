@@ -8,15 +8,16 @@
 // (bitonic, in registers), so at every level the queries that wait on the
 // same page occupy a contiguous run of lanes: the pages of a round are the run
 // heads, one ballot away, with no per-page matching loop.  The round's pages
-// stream through a per-wave ring of kRing 1 KB LDS slots, one
-// global_load_lds_dwordx4 per page (LDS-DMA: pages never occupy VGPRs;
-// kRing - 1 pages stay in flight while one is resolved).  Header fields are
-// read with uniform-address LDS loads into (uniform) VGPRs, so fences and
-// versions are checked by each query lane itself:
-//   * k >= highest -> sibling, the B-link "turn right" (Tree.cpp:626-629,
-//     648-651); front != rear -> re-read next round (Tree.cpp:616-618);
+// stream through a per-wave ring of R 1 KB LDS slots, one
+// global_load_lds_dwordx4 per page (LDS-DMA: pages never occupy VGPRs; R - 1
+// pages stay in flight while one is resolved).  Each staged page is resolved
+// with wave-uniform branches on its type (scalar, from readfirstlane of the
+// header) and per-lane selects, no divergent if-blocks:
+//   * fences: k >= highest -> sibling, the B-link "turn right"
+//     (Tree.cpp:626-629, 648-651); front != rear -> re-read next round
+//     (Tree.cpp:616-618);
 //   * internal page: child = #keys <= k (Tree.cpp:665-685) by a fixed 6-step
-//     branchless search over the staged keys in every waiting lane at once;
+//     branchless search over the staged keys in every lane at once;
 //   * leaf page: lane i holds entry i and one ballot per distinct key gives
 //     slot = ffs(key_i == k && value_i != 0 && f_i == r_i) (Tree.cpp:687-697).
 // The batch arrives bucketed by key (partition.hip), so the queries of a wave
@@ -32,22 +33,18 @@ namespace dev {
 
 namespace {
 
-constexpr int kRing = 4;  // LDS page slots per wave
-
 // One page -> one LDS slot: global_load_lds_dwordx4, lane l's 16 bytes land
-// at slot + 16 l.  Issued from inline asm on purpose: hipcc treats a visible
-// LDS-DMA as a pending LDS write and puts s_waitcnt vmcnt(0) in front of every
-// later ds_read, which would drain the whole ring; the ring's waits are
-// counted by hand instead (wait_vm below).
-__device__ __forceinline__ void glds16(const uint8_t* gsrc, uint32_t* lds) {
-  const uint64_t ga = (uint64_t)(gsrc + 16 * lane_id());
-  const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane(
-      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+// at lds_addr + 16 l.  Issued from inline asm on purpose: hipcc treats a
+// visible LDS-DMA as a pending LDS write and puts s_waitcnt vmcnt(0) in front
+// of every later ds_read, which would drain the whole ring; the ring's waits
+// are counted by hand instead (wait_vm below).
+__device__ __forceinline__ void glds16(const uint8_t* page, uint32_t lds_addr) {
+  const uint64_t ga = (uint64_t)(page + 16 * lane_id());
   asm volatile(
       "s_mov_b32 m0, %1\n\t"
       "global_load_lds_dwordx4 %0, off"
       :
-      : "v"(ga), "s"(la)
+      : "v"(ga), "s"(lds_addr)
       : "memory", "m0");
 }
 
@@ -56,36 +53,13 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// Header (Tree.h:130-160) + page versions as uniform VGPR values, from three
-// uniform-address 16-byte LDS loads and one 8-byte load.
-struct UHdr {
-  uint64_t leftmost, sibling, lowest, highest;
-  uint32_t level, fver, rver;
-  int32_t cnt;
-};
-__device__ __forceinline__ UHdr uniform_hdr(const uint32_t* lp) {
-  const u32x4 a = *reinterpret_cast<const u32x4*>(lp);       // dwords 0..3
-  const u32x4 b = *reinterpret_cast<const u32x4*>(lp + 4);   // dwords 4..7
-  const u32x4 c = *reinterpret_cast<const u32x4*>(lp + 8);   // dwords 8..11
-  const u32x2 z = *reinterpret_cast<const u32x2*>(lp + 254); // 254..255
-  UHdr h;
-  h.fver = a.z & 0xFF;
-  h.leftmost = (uint64_t)((a.z >> 8) | (a.w << 24)) |
-               ((uint64_t)((a.w >> 8) | (b.x << 24)) << 32);
-  h.sibling = (uint64_t)((b.x >> 8) | (b.y << 24)) |
-              ((uint64_t)((b.y >> 8) | (b.z << 24)) << 32);
-  h.level = (b.z >> 8) & 0xFF;
-  h.cnt = (int32_t)(int16_t)(b.z >> 16) + 1;
-  h.lowest = (uint64_t)b.w | ((uint64_t)c.x << 32);
-  h.highest = (uint64_t)c.y | ((uint64_t)c.z << 32);
-  // rear version: byte 1016 (leaf) or 1020 (internal)
-  h.rver = h.leftmost == 0 ? (z.x & 0xFF) : (z.y & 0xFF);
-  return h;
+__device__ __forceinline__ uint32_t rfl(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-// internal record j (key at byte 44+16j = dword 11+4j)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// internal record j (key at byte 44+16j = dword 11+4j), j <= 60
 __device__ __forceinline__ uint64_t lds_ikey(const uint32_t* lp, int j) {
   return (uint64_t)lp[11 + 4 * j] | ((uint64_t)lp[12 + 4 * j] << 32);
 }
@@ -95,9 +69,9 @@ __device__ __forceinline__ uint64_t lds_iptr(const uint32_t* lp, int j) {
 
 }  // namespace
 
-template <bool LOCATE>
+template <bool LOCATE, int R>
 __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[kWavesPerBlock][kRing][kPageDwords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[kWavesPerBlock][R][kPageDwords];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t n = a.n_dev ? *a.n_dev : a.n;
@@ -105,6 +79,8 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
       ((uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv) * kWave;
   if (wave_base >= n) return;  // wave-uniform
   const uint32_t nact = (uint32_t)(n - wave_base < (uint64_t)kWave ? n - wave_base : kWave);
+  const uint32_t ring_lds = rfl((uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint32_t*)&s_ring[wv][0][0]));
 
   // sort this wave's queries by key; tag = lane the query came from
   uint64_t k = (uint32_t)lane < nact ? a.keys[wave_base + lane] : kKeyMax;
@@ -117,7 +93,6 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   uint64_t val = 0, page_out = 0;
   // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
   if (!LOCATE && k == kKeyMax) done = true;
-  uint32_t* ring = &s_ring[wv][0][0];
   uint32_t err = 0;
   int rounds = 0, retries = 0;
 
@@ -138,94 +113,104 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
     const int m = popc64(hq);
     // invalid pointers load the superblock (always mapped) and are rejected
     // when resolved, so every slot sees exactly one DMA
-    const uint64_t pload = ptr_ok(ptr, a.node, a.arena_bytes) ? ptr : 0;
-    const int pre = m < kRing ? m : kRing;
-    for (int j = 0; j < pre; ++j) {
-      glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))), ring + j * kPageDwords);
-      hi &= hi - 1;
+    const bool pok = ptr_ok(ptr, a.node, a.arena_bytes);
+    const uint64_t badm = ballot(!pok);
+    const uint64_t pload = pok ? ptr : 0;
+#pragma unroll
+    for (int j = 0; j < R - 1; ++j) {
+      if (hi) {
+        glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))), ring_lds + j * kPageSize);
+        hi &= hi - 1;
+      }
     }
 
     for (int j = 0; j < m; ++j) {
-      if (j + kRing <= m)
-        wait_vm<kRing - 1>();
-      else
+      // refill the slot resolved last iteration, then wait for page j
+      const bool refill = hi != 0;
+      if (refill) {
+        glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))),
+               ring_lds + ((j + R - 1) % R) * kPageSize);
+        hi &= hi - 1;
+        wait_vm<R - 1>();
+      } else {
         wait_vm<0>();
-      const uint32_t* lp = ring + (j % kRing) * kPageDwords;
+      }
+      const uint32_t* lp = &s_ring[wv][j % R][0];
       const int hl = ctz64(hq);
       hq &= hq - 1;
       const uint64_t pj = rl64(ptr, hl);
       const bool mine = !done && ptr == pj;
-      if (!ptr_ok(pj, a.node, a.arena_bytes)) {
+      if ((badm >> hl) & 1) {
         if (mine) done = true;
         err |= kErrBadPtr;
       } else {
-        const UHdr h = uniform_hdr(lp);
-        const bool is_leaf = h.leftmost == 0;
-        if (h.fver != h.rver) {
+        // header: uniform-address loads (one LDS broadcast each)
+        const u32x4 A = *reinterpret_cast<const u32x4*>(lp);      // dwords 0..3
+        const u32x4 B = *reinterpret_cast<const u32x4*>(lp + 4);  // dwords 4..7
+        const u32x4 C = *reinterpret_cast<const u32x4*>(lp + 8);  // dwords 8..11
+        const u32x2 Z = *reinterpret_cast<const u32x2*>(lp + 254);
+        // leaf entries, read speculatively (cheap for internal pages too)
+        const LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
+        const uint32_t az = rfl(A.z), aw = rfl(A.w), bx = rfl(B.x), bz = rfl(B.z);
+        const bool is_leaf = ((az >> 8) | aw | (bx & 0xFF)) == 0;  // leftmost == 0
+        const uint32_t rver = rfl(is_leaf ? Z.x : Z.y) & 0xFF;
+        const uint64_t leftmost = (uint64_t)((az >> 8) | (aw << 24)) |
+                                  ((uint64_t)((aw >> 8) | (bx << 24)) << 32);
+        const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
+                                 ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
+        const uint64_t lowest = (uint64_t)B.w | ((uint64_t)C.x << 32);
+        const uint64_t highest = (uint64_t)C.y | ((uint64_t)C.z << 32);
+        const int level = (int)((bz >> 8) & 0xFF);
+        const int cnt = (int)(int16_t)(bz >> 16) + 1;
+        if ((az & 0xFF) != rver) {
           // torn / in-flight page: its queries re-list it next round
           if (++retries > kMaxRetries) {
             if (mine) done = true;
             err |= kErrInconsistent;
           }
-        } else if (mine && k >= h.highest) {
-          ptr = h.sibling;  // turn right
-          if (ptr == 0) done = true;
-        } else if (mine && k < h.lowest) {
-          ptr = a.root;  // stale route: restart (Tree.cpp:652-657)
-          err |= kErrFence;
-        } else if (LOCATE && (int)h.level == a.target_level) {
-          if (mine) {
-            page_out = pj;
-            done = true;
-          }
-        } else if (!is_leaf) {
-          if (LOCATE && (int)h.level < a.target_level) {
-            if (mine) {
-              done = true;
-              err |= kErrFence;
-            }
-          } else if (mine) {
+        } else {
+          const bool right = mine && k >= highest;  // turn right
+          const bool low = mine && k < lowest;      // mis-routed
+          const bool here = mine && !right && !low;
+          if (ballot(low)) err |= kErrFence;
+          if (LOCATE && level == a.target_level) {
+            page_out = here ? pj : page_out;
+          } else if (LOCATE && level < a.target_level) {
+            if (ballot(here)) err |= kErrFence;  // below the target level
+          } else if (!is_leaf) {
+            // every lane runs the branchless search; `here` lanes commit
             int pos = 0;  // number of keys <= k (keys strictly increase)
 #pragma unroll
             for (int step = 32; step > 0; step >>= 1) {
               const int idx = pos + step - 1;
-              if (idx < h.cnt && lds_ikey(lp, idx) <= k) pos += step;
+              const int ci = idx < 60 ? idx : 60;
+              if (idx < cnt && lds_ikey(lp, ci) <= k) pos += step;
             }
-            ptr = pos == 0 ? h.leftmost : lds_iptr(lp, pos - 1);
-            if (ptr == 0) done = true;
-          }
-        } else if (LOCATE) {
-          if (mine) {  // reached a leaf below the target level
-            done = true;
-            err |= kErrFence;
-          }
-        } else {
-          // leaf (level 0): lane i holds entry i
-          const LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
-          const bool ok = lane < kLeafCardinality && e.val != kValueNull &&
-                          (e.fraw & 0xF) == (e.rraw & 0xF);
-          // waiting queries are a sorted run: one ballot per distinct key
-          uint64_t qm = ballot(mine);
-          while (qm) {
-            const uint64_t kq = rl64(k, ctz64(qm));
-            const uint64_t same = ballot(mine && k == kq);
-            qm &= ~same;
-            const uint64_t mm = ballot(ok && e.key == kq);
-            const uint64_t v = mm ? rl64(e.val, ctz64(mm)) : 0;
-            if ((same >> lane) & 1) {
-              done = true;
-              val = v;
+            const uint64_t child = pos == 0 ? leftmost : lds_iptr(lp, pos - 1);
+            ptr = here ? child : ptr;
+          } else if (!LOCATE) {
+            // leaf (level 0): lane i holds entry i
+            const bool ok = lane < kLeafCardinality && e.val != kValueNull &&
+                            (e.fraw & 0xF) == (e.rraw & 0xF);
+            uint64_t qm = ballot(here);
+            while (qm) {  // one ballot per distinct key of the sorted run
+              const uint64_t kq = rl64(k, ctz64(qm));
+              const bool same = here && k == kq;
+              qm &= ~ballot(same);
+              const uint64_t mm = ballot(ok && e.key == kq);
+              const uint64_t v = mm ? rl64(e.val, ctz64(mm)) : 0;
+              val = same ? v : val;
             }
           }
+          ptr = right ? sibling : ptr;
+          const bool finished =
+              (LOCATE && level <= a.target_level) || (!LOCATE && is_leaf);
+          done = done || low || (right && sibling == 0) ||
+                 (here && (finished || ptr == 0));
         }
       }
       // the slot's LDS reads are complete before its next DMA lands
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (hi) {
-        glds16(a.arena + ga_offset(rl64(pload, ctz64(hi))),
-               ring + (j % kRing) * kPageDwords);
-        hi &= hi - 1;
-      }
     }
   }
   if (err) atomicOr(a.err, err);
@@ -241,16 +226,31 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   }
 }
 
+static int ring_depth() {
+  static const int r = [] {
+    const char* e = getenv("SHM_WALK_RING");
+    const int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 4 || v == 6 || v == 8) ? v : 4;
+  }();
+  return r;
+}
+
 void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
                  hipStream_t s) {
   (void)depth;
   if (n_upper == 0) return;
   const uint64_t waves = (n_upper + kWave - 1) / kWave;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  if (locate)
-    hipLaunchKernelGGL((k_walk<true>), grid, dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_walk<false>), grid, dim3(kBlock), 0, s, a);
+  if (locate) {
+    hipLaunchKernelGGL((k_walk<true, 4>), grid, dim3(kBlock), 0, s, a);
+    return;
+  }
+  switch (ring_depth()) {
+    case 2: hipLaunchKernelGGL((k_walk<false, 2>), grid, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((k_walk<false, 6>), grid, dim3(kBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_walk<false, 8>), grid, dim3(kBlock), 0, s, a); break;
+    default: hipLaunchKernelGGL((k_walk<false, 4>), grid, dim3(kBlock), 0, s, a); break;
+  }
 }
 
 }  // namespace dev

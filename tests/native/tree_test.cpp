@@ -1,0 +1,52 @@
+// tree_test.cpp — the reference's known-answer test (test/tree_test.cpp:31-68)
+// through the host C++ facade (sherman_amd/csrc/Tree.hpp) on one MI355X.
+// Single-node: the reference's node-1 spin (tree_test.cpp:25-28) has no
+// counterpart.  The delete phase, which the reference only prints, is
+// asserted here.  Exit code 0 = pass.
+#include <cstdio>
+#include <cstdlib>
+
+#include "../../sherman_amd/csrc/Tree.hpp"
+
+#define CHECK(c)                                                   \
+  do {                                                             \
+    if (!(c)) {                                                    \
+      std::fprintf(stderr, "FAIL %s (%s:%d)\n", #c, __FILE__, __LINE__); \
+      std::exit(1);                                                \
+    }                                                              \
+  } while (0)
+
+int main() {
+  shm_config cfg = shm::Tree::default_config();
+  cfg.arena_bytes = 64ull << 20;
+  cfg.max_batch = 1 << 14;
+  shm::Tree tree(cfg);
+  shm::Value v;
+  const uint64_t N = 10240;
+  for (uint64_t i = 1; i < N; ++i) tree.insert(i, i * 2);
+  for (uint64_t i = N - 1; i >= 1; --i) tree.insert(i, i * 3);
+  for (uint64_t i = 1; i < N; ++i) {
+    bool res = tree.search(i, v);
+    CHECK(res && v == i * 3);
+  }
+  for (uint64_t i = 1; i < N; ++i) tree.del(i);
+  for (uint64_t i = 1; i < N; ++i) CHECK(!tree.search(i, v));
+  for (uint64_t i = N - 1; i >= 1; --i) tree.insert(i, i * 3);
+  for (uint64_t i = 1; i < N; ++i) {
+    bool res = tree.search(i, v);
+    CHECK(res && v == i * 3);
+  }
+  // range_query over [100, 199]: 100 values, leaf order then slot order
+  std::vector<shm::Value> buf(N);
+  CHECK(tree.range_query(100, 199, buf.data()) == 100);
+  uint64_t sum = 0;
+  for (int i = 0; i < 100; ++i) sum += buf[i];
+  CHECK(sum == 3 * (100 + 199) * 100 / 2);
+  uint64_t leaves = 0, internal = 0, keys = 0;
+  tree.check_tree(&leaves, &internal, &keys);
+  CHECK(keys == N - 1);
+  std::printf("tree_test ok: %lu keys, %lu leaves, %lu internal pages, height %u\n",
+              (unsigned long)keys, (unsigned long)leaves, (unsigned long)internal,
+              tree.stats().height);
+  return 0;
+}
