@@ -61,7 +61,7 @@ typedef struct shm_config {
   uint64_t arena_bytes;  /* HBM page arena (1 KB pages) */
   uint64_t max_batch;    /* largest n accepted by a batch call */
   uint32_t num_locks;    /* HBM lock table words (reference: 16384) */
-  uint32_t sort_bits;    /* top key bits used to order gets (0 = default) */
+  uint32_t sort_bits;    /* top key bits that order gets: 0 or 16 */
 } shm_config;
 
 typedef struct shm_stats_t {

@@ -157,7 +157,7 @@ class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
-                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=14):
+                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=16):
         L = lib()
         cfg = ShmConfig()
         _check(L.shm_config_init(ctypes.byref(cfg)), "config")

@@ -69,18 +69,24 @@ void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
 
 // ---- utilities (util.hip) -----------------------------------------------------
 void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);
-// bucket a get batch by its top kPartBits key bits (partition.hip):
-// out_keys in bucket order, pos_of[i] = where input i was placed
-constexpr int kPartBits = 14;
-constexpr int kPartBuckets = 1 << kPartBits;
-constexpr int kPartTile = 16384;
-void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* gh,
-                      uint32_t* tot, uint64_t* out_keys, uint32_t* pos_of,
-                      hipStream_t s);
-// vals_out[i] = res[pos_of[i]], found_out[i] = res != 0
-void launch_gather_results(const uint64_t* res, const uint32_t* pos_of,
-                           uint64_t n, uint64_t* vals_out, uint8_t* found_out,
-                           hipStream_t s);
+// order a get batch by its top 16 key bits (partition.hip): keys_out is the
+// walk order, src[p] = keys1 slot of walk slot p, pos1[i] = keys1 slot of
+// input i.  M = [kMaxTiles][kCoarse] tile counts, S = group sums (all zero
+// between calls; zero it once at creation), chunks = 2 x
+// partition_chunk_slots(n) words.
+constexpr int kCoarse = 256;
+constexpr int kFine = 256;
+constexpr int kMaxTiles = 256;
+constexpr int kFineCap = 8192;
+constexpr int kPartHistWords = kMaxTiles * kCoarse;
+constexpr int kPartGroupWords = 16 * kCoarse;
+uint32_t partition_chunk_slots(uint64_t n);
+void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* M, uint32_t* S,
+                      uint32_t* chunks, uint64_t* keys1, uint32_t* pos1,
+                      uint64_t* keys_out, uint32_t* src, hipStream_t s);
+// out[i] = vals1[pos1[i]], found[i] = out[i] != 0
+void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
+                        uint64_t* out, uint8_t* found, hipStream_t s);
 // out[i] = (uint32_t)(keys[i] >> 32), idx[i] = i
 void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
                   uint32_t* idx, hipStream_t s);

@@ -26,7 +26,9 @@ using namespace shm;
 namespace {
 
 constexpr uint64_t kSortMinGets = 8192;   // below this, walk in input order
-constexpr uint32_t kDefaultSortBits = 14; // top key bits that bucket gets
+
+
+constexpr uint32_t kDefaultSortBits = 16; // top key bits that order gets (8 + 8)
 constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
 
 }  // namespace
@@ -64,8 +66,9 @@ struct shm_tree {
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   void* temp = nullptr;
   size_t temp_bytes = 0;
-  uint32_t* part_hist = nullptr;  // [tiles][kPartBuckets]
-  uint32_t* part_tot = nullptr;   // [kPartBuckets]
+  uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
+  uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
+  uint32_t* part_chunks = nullptr;  // fine-pass chunk table
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
@@ -380,7 +383,7 @@ void free_all(shm_tree* t) {
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
-  F(t->temp); F(t->part_hist); F(t->part_tot);
+  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks);
   for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -500,7 +503,8 @@ int shm_config_init(shm_config* c) {
 int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (!cfg || !out || cfg->struct_size != sizeof(shm_config)) return SHM_EINVAL;
   if (cfg->arena_bytes < 4 * kPageSize || cfg->max_batch == 0 ||
-      cfg->max_batch > (1ull << 31) || cfg->num_locks == 0)
+      cfg->max_batch > (1ull << 31) || cfg->num_locks == 0 ||
+      (cfg->sort_bits != 0 && cfg->sort_bits != kDefaultSortBits))
     return SHM_EINVAL;
   shm_tree* t = new shm_tree();
   t->cfg = *cfg;
@@ -548,9 +552,9 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);
     rc |= dalloc(&t->sep_ptr[i], t->sep_cap);
   }
-  rc |= dalloc(&t->part_hist, ((n + dev::kPartTile - 1) / dev::kPartTile) *
-                                 (uint64_t)dev::kPartBuckets);
-  rc |= dalloc(&t->part_tot, dev::kPartBuckets);
+  rc |= dalloc(&t->part_hist, dev::kPartHistWords);
+  rc |= dalloc(&t->part_S, dev::kPartGroupWords);
+  rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
@@ -559,6 +563,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   hipStream_t s = t->stream;
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
+      hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->arena, 0, kPageSize, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
@@ -605,12 +610,13 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
-      // walk results land contiguously in walk order (kb) and are gathered
-      // back to input order afterwards: no scattered 8-byte stores
-      dev::launch_partition(keys + off, m, t->part_hist, t->part_tot, t->ka,
-                            t->ib, s);
+      // (keys1 = kb, pos1 = ia, walk order = ka, src = ib); the walk stores
+      // result p at vals1[src[p]] (kb, inside p's chunk), unpartition gathers
+      dev::launch_partition(keys + off, m, t->part_hist, t->part_S, t->part_chunks,
+                            t->kb, t->ia,
+                            t->ka, t->ib, s);
       a.keys = t->ka;
-      a.perm = nullptr;
+      a.perm = t->ib;
       a.out_val = t->kb;
       a.out_found = nullptr;
       gathered = true;
@@ -627,8 +633,8 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       t->prof_pending.push_back(pr);
     }
     if (gathered) {
-      dev::launch_gather_results(t->kb, t->ib, m, vals_out + off,
-                                 found_out ? found_out + off : nullptr, s);
+      dev::launch_unpartition(t->kb, t->ia, m, vals_out + off,
+                              found_out ? found_out + off : nullptr, s);
       DBG(s, "gather");
     }
   }

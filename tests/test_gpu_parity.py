@@ -327,3 +327,25 @@ def test_uniform_get_large_vs_oracle(lib_ok):
     gv, gf = gpu_search(t, probe)
     assert_same(probe, ov, of, gv, gf)
     t.close()
+
+
+def test_sorted_get_skewed_and_ragged(lib_ok):
+    """Sorted-get partition under skew: one 16-bit bucket far larger than a
+    fine-pass chunk, next to uniform keys, with a ragged batch length."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 18)
+    orc = OracleTree(256 << 20)
+    dense = np.arange(1, 60001, dtype=U64) * U64(3)           # all in bucket 0
+    spread = hashed_keys(1, 40001)
+    keys = np.concatenate([dense, spread])
+    vals = np.arange(1, keys.size + 1, dtype=U64) * U64(5)
+    gpu_insert(t, keys, vals)
+    orc.apply_batch(keys, vals)
+    rng = np.random.default_rng(5)
+    probe = np.concatenate([dense[rng.integers(0, dense.size, 70001)],
+                            spread[rng.integers(0, spread.size, 30000)],
+                            rng.integers(1, 1 << 63, 1234, dtype=np.int64).astype(U64)])
+    rng.shuffle(probe)
+    ov, of = orc.search_batch(probe)
+    gv, gf = gpu_search(t, probe)
+    assert_same(probe, ov, of, gv, gf)
+    t.close()
