@@ -54,6 +54,7 @@ def main():
     import torch
 
     import sherman_amd as shm
+    from sherman_amd.shard import ShardRouter, owner_of
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,7 +126,7 @@ def main():
 
     route = None
     if world > 1:
-        route = Router(tree, world, batch, dev, dist)
+        route = ShardRouter(tree, world, dist)
 
     def step(i):
         q = qs[i % n_batches]
@@ -230,13 +231,6 @@ def main():
     tree.close()
 
 
-def owner_of(k, world):
-    """floor(k * world / 2^64) for u64 keys held as int64 (== __umul64hi)."""
-    hi = (k >> 32) & 0xFFFFFFFF
-    lo = k & 0xFFFFFFFF
-    return (hi * world + ((lo * world) >> 32)) >> 32
-
-
 def hash_ids(tree, ids, dev):
     """key(i) = CityHash64(i) + 1 for an arbitrary id tensor (device)."""
     import torch
@@ -272,44 +266,6 @@ def cityhash64_torch(x):
     g = (d ^ h) * mul
     g = g ^ lsr(g, 47)
     return g * mul
-
-
-class Router:
-    """Range-shard routing with RCCL all-to-all (replaces DSM chunk
-    round-robin, include/DSM.h:198-224): bucket by owner, exchange counts,
-    exchange keys, search locally, send values back, un-permute."""
-
-    def __init__(self, tree, world, batch, dev, dist):
-        import torch
-        self.tree, self.world, self.dist = tree, world, dist
-        self.kbuf = torch.empty(batch, dtype=torch.int64, device=dev)
-        self.perm = torch.empty(batch, dtype=torch.int32, device=dev)
-        self.cnt = torch.empty(world, dtype=torch.int64, device=dev)
-        self.rcnt = torch.empty(world, dtype=torch.int64, device=dev)
-        self.recv = torch.empty(batch * 2, dtype=torch.int64, device=dev)
-        self.rvals = torch.empty(batch * 2, dtype=torch.int64, device=dev)
-        self.rfound = torch.empty(batch * 2, dtype=torch.uint8, device=dev)
-        self.back = torch.empty(batch, dtype=torch.int64, device=dev)
-
-    def search(self, q, vals, found):
-        import torch
-        t, dist = self.tree, self.dist
-        t.route_bucket(q, self.world, self.kbuf, self.perm, self.cnt)
-        dist.all_to_all_single(self.rcnt, self.cnt)
-        cnt = self.cnt.tolist()
-        rcnt = self.rcnt.tolist()
-        nrecv = sum(rcnt)
-        if nrecv > self.recv.numel():
-            self.recv = torch.empty(nrecv, dtype=torch.int64, device=q.device)
-            self.rvals = torch.empty(nrecv, dtype=torch.int64, device=q.device)
-            self.rfound = torch.empty(nrecv, dtype=torch.uint8, device=q.device)
-        recv = self.recv[:nrecv]
-        dist.all_to_all_single(recv, self.kbuf[:q.numel()], rcnt, cnt)
-        rv = self.rvals[:nrecv]
-        t.search_batch(recv, rv, self.rfound[:nrecv])
-        dist.all_to_all_single(self.back[:q.numel()], rv, cnt, rcnt)
-        t.route_unpermute(self.back[:q.numel()], self.perm, vals)
-        found.copy_((vals != 0).to(torch.uint8))
 
 
 def cpu_baseline(tree, qs, vals, found, args, step):

@@ -134,11 +134,17 @@ int shm_profile_read(shm_tree *t, shm_profile_t *out, int reset);
 
 /* multi-GPU routing helpers (range shards: shard s owns
  * [s * 2^64 / P, (s+1) * 2^64 / P)) ------------------------------------------ */
-/* Bucket n keys by owning shard: writes per-shard counts[P], the keys grouped
- * by shard into keys_out, and perm[i] = source position of keys_out[i]. */
+/* Bucket n <= max_batch keys by owning shard (1 <= P <= 64): writes
+ * per-shard counts[P], the keys grouped by shard into keys_out, and perm[i] =
+ * source position of keys_out[i].  Stable: inside a shard, keys keep their
+ * input order (routed insert batches keep last-writer-in-batch-order). */
 int shm_route_bucket(shm_tree *t, const uint64_t *keys, uint64_t n,
                      uint32_t num_shards, uint64_t *counts_out,
                      uint64_t *keys_out, uint32_t *perm_out, void *stream);
+/* out[i] = in[perm[i]] (carry a companion array, e.g. insert values, along
+ * with the bucketed keys). */
+int shm_route_permute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
+                      uint64_t n, uint64_t *out, void *stream);
 /* out[perm[i]] = in[i] (reverse of the bucket permutation). */
 int shm_route_unpermute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
                         uint64_t n, uint64_t *out, void *stream);

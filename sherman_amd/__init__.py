@@ -101,6 +101,7 @@ _SIGNATURES = [
     ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
+    ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
 ]
@@ -293,6 +294,10 @@ class Tree:
         _check(lib().shm_route_bucket(self.h, _ptr(keys), keys.numel(), num_shards,
                                       _ptr(counts_out), _ptr(keys_out), _ptr(perm_out),
                                       _stream_ptr(stream)), "route_bucket")
+
+    def route_permute(self, vals_in, perm, out, stream=None):
+        _check(lib().shm_route_permute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
+                                       _ptr(out), _stream_ptr(stream)), "permute")
 
     def route_unpermute(self, vals_in, perm, out, stream=None):
         _check(lib().shm_route_unpermute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),

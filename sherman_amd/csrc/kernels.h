@@ -106,9 +106,14 @@ void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
+// stable bucketing by owning shard; cm = route_scratch_words(n) words
+uint64_t route_scratch_words(uint64_t n_max);
 void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
                          uint64_t* counts, uint64_t* keys_out, uint32_t* perm,
-                         uint32_t* cursor, hipStream_t s);
+                         uint32_t* cm, hipStream_t s);
+// out[i] = in[perm[i]]
+void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64_t* out,
+                    hipStream_t s);
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
                       uint64_t* out, hipStream_t s);
 void launch_range_count(const uint8_t* arena, uint64_t arena_bytes,

@@ -528,7 +528,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->locks, cfg->num_locks);
   rc |= dalloc(&t->d_err, 4);
   rc |= dalloc(&t->d_counts, 16);
-  rc |= dalloc(&t->route_scratch, 256);
+  rc |= dalloc(&t->route_scratch, dev::route_scratch_words(n));
   rc |= dalloc(&t->ka, n);
   rc |= dalloc(&t->kb, n);
   rc |= dalloc(&t->ia, n);
@@ -783,10 +783,18 @@ int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
                      uint64_t* keys_out, uint32_t* perm_out, void* stream) {
   if (!t || num_shards == 0 || num_shards > 64 || !counts_out) return SHM_EINVAL;
   if (n && (!keys || !keys_out || !perm_out)) return SHM_EINVAL;
-  if (n > 0xFFFFFFFFull) return SHM_E2BIG;
+  if (n > t->nmax) return SHM_E2BIG;
   hipStream_t s = pick(t, stream);
   dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out,
                            t->route_scratch, s);
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_route_permute(shm_tree* t, const uint64_t* in, const uint32_t* perm,
+                      uint64_t n, uint64_t* out, void* stream) {
+  if (!t || (n && (!in || !perm || !out))) return SHM_EINVAL;
+  dev::launch_permute(in, perm, n, out, pick(t, stream));
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }

@@ -134,70 +134,148 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t k, uint32_t shards) {
 }
 constexpr int kRouteMaxShards = 64;
 constexpr int kRoutePer = 4;  // keys per thread
+constexpr int kRouteTile = kT * kRoutePer;
 
-__global__ void k_route_count(const uint64_t* keys, uint64_t n, uint32_t shards,
-                              uint32_t* cnt) {
+// Stable bucketing by owner (keys_out keeps input order inside each shard,
+// which insert routing needs for last-writer-in-batch-order semantics):
+//   count   : per-tile shard counts            -> cm[tile][shard]
+//   scan    : per shard, exclusive over tiles  -> cm = tile bases, counts_out
+//   scatter : per tile, ranks in index order from wave ballots
+__global__ __launch_bounds__(kT) void k_route_count(const uint64_t* __restrict__ keys,
+                                                    uint64_t n, uint32_t shards,
+                                                    uint32_t* __restrict__ cm) {
   __shared__ uint32_t c[kRouteMaxShards];
   if (threadIdx.x < kRouteMaxShards) c[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kT * kRoutePer;
+  const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+#pragma unroll
   for (int r = 0; r < kRoutePer; ++r) {
     const uint64_t i = base + (uint64_t)r * kT + threadIdx.x;
     if (i < n) atomicAdd(&c[owner_of(keys[i], shards)], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < shards && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
+  if (threadIdx.x < shards) cm[(uint64_t)blockIdx.x * shards + threadIdx.x] = c[threadIdx.x];
 }
-// cursor[s] = exclusive prefix of cnt; counts_out[s] = cnt[s]
-__global__ void k_route_scan(const uint32_t* cnt, uint32_t shards,
-                             uint32_t* cursor, uint64_t* counts_out) {
-  if (threadIdx.x != 0) return;
-  uint32_t acc = 0;
-  for (uint32_t s = 0; s < shards; ++s) {
-    cursor[s] = acc;
-    counts_out[s] = cnt[s];
-    acc += cnt[s];
-  }
-}
-__global__ void k_route_scatter(const uint64_t* keys, uint64_t n,
-                                uint32_t shards, uint32_t* cursor,
-                                uint64_t* keys_out, uint32_t* perm) {
-  __shared__ uint32_t c[kRouteMaxShards];
-  __shared__ uint32_t b[kRouteMaxShards];
-  if (threadIdx.x < kRouteMaxShards) c[threadIdx.x] = 0;
+
+__global__ __launch_bounds__(1024) void k_route_scan(uint32_t* __restrict__ cm, uint32_t tiles,
+                                                     uint32_t shards,
+                                                     uint64_t* __restrict__ counts_out) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t off[kRouteMaxShards];
+  const uint32_t t = threadIdx.x;
+  const uint32_t Q = 1024 / shards;  // tile slices
+  const uint32_t q = t / shards, sh = t % shards;
+  const bool live = q < Q;
+  const uint32_t b0 = live ? (uint32_t)(((uint64_t)tiles * q) / Q) : 0;
+  const uint32_t b1 = live ? (uint32_t)(((uint64_t)tiles * (q + 1)) / Q) : 0;
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) sum += cm[(uint64_t)b * shards + sh];
+  if (live) part[q * shards + sh] = sum;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kT * kRoutePer;
-  uint32_t own[kRoutePer], rank[kRoutePer];
-  uint64_t kk[kRoutePer];
-  for (int r = 0; r < kRoutePer; ++r) {
-    const uint64_t i = base + (uint64_t)r * kT + threadIdx.x;
-    own[r] = ~0u;
-    if (i < n) {
-      kk[r] = keys[i];
-      own[r] = owner_of(kk[r], shards);
-      rank[r] = atomicAdd(&c[own[r]], 1u);
+  if (t < shards) {
+    uint32_t acc = 0;
+    for (uint32_t x = 0; x < Q; ++x) {
+      const uint32_t v = part[x * shards + t];
+      part[x * shards + t] = acc;
+      acc += v;
+    }
+    off[t] = acc;  // shard total for now
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (uint32_t x = 0; x < shards; ++x) {
+      const uint32_t v = off[x];
+      counts_out[x] = v;
+      off[x] = acc;
+      acc += v;
     }
   }
   __syncthreads();
-  if (threadIdx.x < shards) b[threadIdx.x] = c[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], c[threadIdx.x]) : 0;
-  __syncthreads();
-  for (int r = 0; r < kRoutePer; ++r) {
-    if (own[r] == ~0u) continue;
-    const uint64_t i = base + (uint64_t)r * kT + threadIdx.x;
-    const uint32_t o = b[own[r]] + rank[r];
-    keys_out[o] = kk[r];
-    perm[o] = (uint32_t)i;
+  if (live) {
+    uint32_t run = off[sh] + part[q * shards + sh];
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint64_t o = (uint64_t)b * shards + sh;
+      const uint32_t v = cm[o];
+      cm[o] = run;
+      run += v;
+    }
   }
 }
+
+__global__ __launch_bounds__(kT) void k_route_scatter(const uint64_t* __restrict__ keys,
+                                                      uint64_t n, uint32_t shards,
+                                                      const uint32_t* __restrict__ cm,
+                                                      uint64_t* __restrict__ keys_out,
+                                                      uint32_t* __restrict__ perm) {
+  constexpr int kW = kT / kWave;
+  __shared__ uint32_t wc[kRoutePer][kW][kRouteMaxShards];
+  const int t = threadIdx.x, w = t >> 6, lane = lane_id();
+  for (int j = t; j < kRoutePer * kW * kRouteMaxShards; j += kT) (&wc[0][0][0])[j] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+  uint64_t kk[kRoutePer];
+  uint32_t own[kRoutePer], rank[kRoutePer];
+#pragma unroll
+  for (int r = 0; r < kRoutePer; ++r) {
+    const uint64_t i = base + (uint64_t)r * kT + t;
+    const bool valid = i < n;
+    kk[r] = valid ? keys[i] : 0;
+    own[r] = valid ? owner_of(kk[r], shards) : ~0u;
+    rank[r] = 0;
+    uint64_t pending = ballot(valid);
+    while (pending) {  // one pass per distinct owner in this wave
+      const uint32_t o = rl32(own[r], ctz64(pending));
+      const uint64_t m = ballot(own[r] == o);
+      if (own[r] == o) rank[r] = popc64(m & lanemask_lt());
+      if (lane == 0) wc[r][w][o] = popc64(m);
+      pending &= ~m;
+    }
+  }
+  __syncthreads();
+  if ((uint32_t)t < shards) {  // index order = (round, wave, lane)
+    uint32_t run = cm[(uint64_t)blockIdx.x * shards + t];
+    for (int r = 0; r < kRoutePer; ++r)
+      for (int x = 0; x < kW; ++x) {
+        const uint32_t v = wc[r][x][t];
+        wc[r][x][t] = run;
+        run += v;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRoutePer; ++r) {
+    if (own[r] == ~0u) continue;
+    const uint32_t o = wc[r][w][own[r]] + rank[r];
+    keys_out[o] = kk[r];
+    perm[o] = (uint32_t)(base + (uint64_t)r * kT + t);
+  }
+}
+
+uint64_t route_scratch_words(uint64_t n_max) {
+  return ((n_max + kRouteTile - 1) / kRouteTile) * kRouteMaxShards;
+}
+
 void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
                          uint64_t* counts, uint64_t* keys_out, uint32_t* perm,
-                         uint32_t* cursor, hipStream_t s) {
-  // cursor: 2 * kRouteMaxShards scratch words (cnt, cursor)
-  (void)hipMemsetAsync(cursor, 0, sizeof(uint32_t) * 2 * kRouteMaxShards, s);
-  const dim3 g = grid1(n, kT * kRoutePer);
-  if (n) hipLaunchKernelGGL(k_route_count, g, dim3(kT), 0, s, keys, n, shards, cursor);
-  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(64), 0, s, cursor, shards, cursor + kRouteMaxShards, counts);
-  if (n) hipLaunchKernelGGL(k_route_scatter, g, dim3(kT), 0, s, keys, n, shards, cursor + kRouteMaxShards, keys_out, perm);
+                         uint32_t* cm, hipStream_t s) {
+  const uint32_t tiles = (uint32_t)((n + kRouteTile - 1) / kRouteTile);
+  if (n) hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kT), 0, s, keys, n, shards, cm);
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, s, cm, tiles, shards, counts);
+  if (n)
+    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kT), 0, s, keys, n, shards,
+                       (const uint32_t*)cm, keys_out, perm);
+}
+
+// out[i] = in[perm[i]] (apply the bucket permutation to a companion array)
+__global__ void k_permute(const uint64_t* in, const uint32_t* perm, uint64_t n,
+                          uint64_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[perm[i]];
+}
+void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64_t* out,
+                    hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_permute, grid1(n), dim3(kT), 0, s, in, perm, n, out);
 }
 
 __global__ void k_unpermute(const uint64_t* in, const uint32_t* perm,

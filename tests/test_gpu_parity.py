@@ -282,7 +282,9 @@ def test_device_cityhash_matches_oracle(lib_ok):
 
 
 def test_route_bucket_roundtrip(lib_ok):
-    t = shm.Tree(arena_bytes=8 << 20, max_batch=1024)
+    """Stable bucketing by owner (the permutation equals a stable argsort of
+    the owners), companion permute, and the reverse permutation."""
+    t = shm.Tree(arena_bytes=8 << 20, max_batch=1 << 17)
     rng = np.random.default_rng(3)
     keys = rng.integers(0, 1 << 63, 100000, dtype=np.uint64) * U64(2) + U64(1)
     for shards in (1, 2, 3, 8):
@@ -300,6 +302,14 @@ def test_route_bucket_roundtrip(lib_ok):
         for s in range(shards):
             seg = kh[off[s]:off[s + 1]]
             assert np.array_equal(np.sort(seg), np.sort(keys[owner == s]))
+        order = np.argsort(owner, kind="stable")
+        assert np.array_equal(perm.cpu().numpy().astype(np.int64), order)
+        assert np.array_equal(kh, keys[order])
+        vals = dev(np.arange(keys.size, dtype=U64) * U64(3))
+        vo = torch.empty_like(vals)
+        t.route_permute(vals, perm, vo)
+        t.synchronize()
+        assert np.array_equal(host(vo), order.astype(U64) * U64(3))
         back = torch.empty_like(k)
         t.route_unpermute(ko, perm, back)
         t.synchronize()
