@@ -126,7 +126,7 @@ int shm_synchronize(shm_tree *t);
 typedef struct shm_profile_t {
   uint64_t calls;       /* search_batch calls (chunks) timed */
   uint64_t queries;     /* queries in those calls */
-  double order_ms;      /* sum of ordering (top32 + radix sort) time */
+  double order_ms;      /* sum of get-ordering (partition) time */
   double walk_ms;       /* sum of k_walk kernel time */
 } shm_profile_t;
 int shm_profile_enable(shm_tree *t, int on);
