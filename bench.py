@@ -1,19 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: batched get on the MI355X-native Sherman B+tree.
+"""Benchmark: batched get (and mixed get/insert) on the MI355X-native Sherman
+B+tree.
 
-Workload (BASELINE.json configs[1], "C2"): 2^26 keys per GPU,
-key(i) = CityHash64(i) + 1 (test/benchmark.cpp:43-46 without the modulus),
-value(i) = 2i, inserted through the batched insert path in 1 Mi batches;
-then uniform 100 % get batches of 1 Mi queries resident in HBM.  A "step" is
-one batched get of 1 Mi queries (per GPU).
+Default workload, C2 (BASELINE.json configs[1]) — the headline line:
+  * 2^26 keys per GPU, key(i) = CityHash64(i) + 1 (test/benchmark.cpp:43-46
+    without the modulus), value(i) = 2i.
+  * The keys go in through the batched insert path in 1 Mi batches (untimed).
+  * Then uniform 100 % get batches of 1 Mi queries, resident in HBM.
+  * A "step" is one batched get of 1 Mi queries per GPU.
 
-N > 1 (python -m torch.distributed.run ... bench.py --gpus N): the key space
-is range-partitioned one shard per GPU (shard s owns [s*2^64/N, (s+1)*2^64/N)),
-each rank holds 2^26 keys of a 2^26*N global key set and issues 1 Mi uniform
-queries over the whole set per step; queries and replies are routed with
-RCCL all-to-all (weak scaling).
+--workload c3 (BASELINE.json configs[2], N = 1):
+  * The C2 tree, then batches of 1 Mi ops.
+  * Key = to_key(1 + zipf(0.99) over 2^26).
+  * An op is a get with probability 50 %, otherwise an insert of value
+    (global op index + 1).
+  * A step is one batch: its gets see the previous batch's state, then its
+    inserts apply in batch order.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+N > 1 (python -m torch.distributed.run ... bench.py --gpus N, C2):
+  * The key space is range-partitioned, one shard per GPU: shard s owns
+    [s*2^64/N, (s+1)*2^64/N).
+  * Each rank holds 2^26 keys of a 2^26*N global key set.
+  * Each rank issues 1 Mi uniform queries over the whole set per step.
+  * Queries and replies are routed with RCCL all-to-all (sherman_amd.shard),
+    i.e. weak scaling.
+
+Prints ONE JSON line on rank 0 (DESIGN.md §Measurement explains every field).
 """
 import argparse
 import json
@@ -25,8 +37,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ALG_BYTES_PER_GET = 1040  # 1024 B leaf + 8 B key + 8 B value
-HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+ALG_BYTES_PER_GET = 1040     # 1024 B leaf + 8 B key + 8 B value
+ALG_BYTES_PER_INSERT = 1074  # 1024 B leaf + 18 B entry + 16 B k/v + 16 B lock
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
+N_BATCHES = 8                # distinct resident batches the steps cycle over
 
 
 def parse():
@@ -34,8 +48,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", choices=("c2", "c3"), default="c2")
     p.add_argument("--keys-log2", type=int, default=26, help="keys per GPU = 2^k")
-    p.add_argument("--batch-log2", type=int, default=20, help="queries per step per GPU")
+    p.add_argument("--batch-log2", type=int, default=20, help="ops per step per GPU")
+    p.add_argument("--theta", type=float, default=0.99, help="c3 zipf skew")
+    p.add_argument("--read-ratio", type=int, default=50, help="c3 get percentage")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--no-sort", action="store_true", help="walk gets in input order")
@@ -48,18 +65,55 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def build_shard(tree, n_keys, world, rank, dev):
+    """Insert this rank's share of key(1..n_keys*world) (untimed)."""
+    import torch
+    from sherman_amd.shard import owner_of
+
+    total = n_keys * world
+    chunk = 1 << 22
+    inserted = 0
+    parts = []
+    for first in range(1, total + 1, chunk):
+        m = min(chunk, total + 1 - first)
+        k = torch.empty(m, dtype=torch.int64, device=dev)
+        tree.gen_keys(first, m, k)
+        ids = torch.arange(first, first + m, dtype=torch.int64, device=dev)
+        if world > 1:
+            mine = owner_of(k, world) == rank
+            k, ids = k[mine], ids[mine]
+        parts.append(k)
+        for c in range(0, k.numel(), 1 << 20):
+            kk = k[c:c + (1 << 20)]
+            tree.insert_batch(kk, ids[c:c + (1 << 20)] * 2)
+            inserted += kk.numel()
+    torch.cuda.synchronize()
+    return torch.cat(parts), inserted
+
+
 def main():
     args = parse()
-    import numpy as np
     import torch
 
     import sherman_amd as shm
-    from sherman_amd.shard import ShardRouter, owner_of
+    from sherman_amd.shard import ShardRouter
+    from sherman_amd.workload import Zipf, op_is_get
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    assert args.workload == "c2" or world == 1, "c3 is a single-GPU config"
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -71,70 +125,73 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    n_keys = 1 << args.keys_log2          # per GPU
-    batch = 1 << args.batch_log2          # queries per GPU per step
-    total_keys = n_keys * world
+    n_keys = 1 << args.keys_log2
+    batch = 1 << args.batch_log2
     dev = torch.device(f"cuda:{local}")
     arena = max(2 << 30, n_keys * 48)
     tree = shm.Tree(arena_bytes=arena, max_batch=1 << 20, device=local,
                     node_id=rank, sort_gets=not args.no_sort)
 
-    # ---- build the shard through the batched insert path (untimed) --------
     t0 = time.time()
-    chunk = 1 << 22
-    inserted = 0
-    all_keys = []
-    for first in range(1, total_keys + 1, chunk):
-        m = min(chunk, total_keys + 1 - first)
-        k = torch.empty(m, dtype=torch.int64, device=dev)
-        tree.gen_keys(first, m, k)
-        ids = torch.arange(first, first + m, dtype=torch.int64, device=dev)
-        if world > 1:
-            # owner = floor(key * world / 2^64), on unsigned bits
-            mine = owner_of(k, world) == rank
-            k, ids = k[mine], ids[mine]
-        all_keys.append(k)
-        for c in range(0, k.numel(), 1 << 20):
-            kk = k[c:c + (1 << 20)]
-            tree.insert_batch(kk, ids[c:c + (1 << 20)] * 2)
-            inserted += kk.numel()
-    torch.cuda.synchronize()
+    keys_local, inserted = build_shard(tree, n_keys, world, rank, dev)
     build_s = time.time() - t0
-    keys_local = torch.cat(all_keys)
-    del all_keys
     st = tree.stats()
     log(f"[rank {rank}] built {inserted} keys in {build_s:.1f}s "
         f"({inserted / build_s / 1e6:.2f} M inserts/s), height {st['height']}, "
         f"pages {st['pages_used']}")
 
-    # ---- query batches (uniform over the global key set), resident in HBM --
+    # ---- resident op batches ----------------------------------------------
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED0000 + rank)
-    n_batches = 8
-    if world == 1:
-        qs = [keys_local[torch.randint(0, n_keys, (batch,), device=dev, generator=g)]
-              for _ in range(n_batches)]
-    else:
-        qs = []
-        for _ in range(n_batches):
-            # uniform i over the GLOBAL key set, key(i) hashed on device with
-            # the same CityHash64 as the build; owners are spread uniformly
-            ids = torch.randint(1, total_keys + 1, (batch,), device=dev, generator=g)
-            qs.append(hash_ids(tree, ids, dev))
     vals = torch.empty(batch, dtype=torch.int64, device=dev)
     found = torch.empty(batch, dtype=torch.uint8, device=dev)
-
-    route = None
-    if world > 1:
-        route = ShardRouter(tree, world, dist)
-
-    def step(i):
-        q = qs[i % n_batches]
-        if route is None:
-            tree.search_batch(q, vals, found)
+    if args.workload == "c2":
+        if world == 1:
+            qs = [keys_local[torch.randint(0, n_keys, (batch,), device=dev, generator=g)]
+                  for _ in range(N_BATCHES)]
         else:
-            route.search(q, vals, found)
+            qs = []
+            for _ in range(N_BATCHES):
+                # uniform i over the GLOBAL key set, hashed on device
+                ids = torch.randint(1, n_keys * world + 1, (batch,), device=dev, generator=g)
+                k = torch.empty_like(ids)
+                tree.hash_keys(ids, k)
+                qs.append(k)
+        route = ShardRouter(tree, world, dist) if world > 1 else None
 
+        def step(i):
+            q = qs[i % N_BATCHES]
+            if route is None:
+                tree.search_batch(q, vals, found)
+            else:
+                route.search(q, vals, found)
+    else:
+        zipf = Zipf(n_keys, args.theta, dev)
+        mixed = []
+        for b in range(N_BATCHES):
+            ids = zipf.sample(batch, g) + 1  # key(1 + zipf_next())
+            k = torch.empty_like(ids)
+            tree.hash_keys(ids, k)
+            is_get = op_is_get(batch, args.read_ratio, dev, g)
+            op_idx = torch.arange(b * batch, (b + 1) * batch, dtype=torch.int64, device=dev)
+            mixed.append((k[is_get].contiguous(), k[~is_get].contiguous(),
+                          (op_idx[~is_get] + 1).contiguous()))
+        del keys_local
+
+        def step(i):
+            gk, pk, pv = mixed[i % N_BATCHES]
+            tree.search_batch(gk, vals[:gk.numel()], found[:gk.numel()])
+            tree.insert_batch(pk, pv)
+
+    # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
+    cpu = parity = None
+    if world == 1 and not args.no_cpu_baseline:
+        if args.workload == "c2":
+            cpu, parity = cpu_baseline_get(tree, qs, vals, found, args, step)
+        else:
+            cpu, parity = cpu_baseline_mixed(tree, mixed, vals, found, args, step)
+
+    # ---- timed steps --------------------------------------------------------
     for i in range(args.warmup):
         step(i)
     barrier()
@@ -147,12 +204,14 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    total_q = batch * args.steps * world
-    mops = total_q / elapsed / 1e6
-
-    # correctness on the last batch: every query hits (keys all present)
+    total_ops = batch * args.steps * world
+    mops = total_ops / elapsed / 1e6
     torch.cuda.synchronize()
-    hit_rate = float(found.float().mean().item())
+    if args.workload == "c2":
+        hit_rate = float(found.float().mean().item())
+    else:
+        n_get = mixed[(args.steps - 1) % N_BATCHES][0].numel()
+        hit_rate = float(found[:n_get].float().mean().item())
 
     # ---- roofline: k_walk timed with HIP events on its launch stream -------
     tree.profile(True)
@@ -167,23 +226,32 @@ def main():
     achieved = q_per_launch * ALG_BYTES_PER_GET / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_walk.json")
-    if os.path.exists(pmc_path):
+    if args.workload == "c2" and os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("batch") == batch and pmc.get("keys_log2") == args.keys_log2:
                 traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
 
-    # ---- CPU baseline (rank 0, N=1 only): reference algorithm on host cores
-    cpu = None
-    parity = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(tree, qs, vals, found, args, step)
-
     if rank == 0:
+        if args.workload == "c2":
+            metric = "batched get Mops/s (64M uint64 keys)"
+            workload = ("C2: batched get, 2^%d uint64 keys/GPU, uniform 100%% read, "
+                        "2^%d-query batches%s" % (args.keys_log2, args.batch_log2,
+                                                    "" if world == 1 else
+                                                    ", range shards + RCCL all-to-all"))
+            data = "synthetic: key(i)=CityHash64(i)+1, value=2i; uniform queries"
+        else:
+            metric = "mixed get/insert Mops/s (64M uint64 keys, zipf %.2f, %d%% get)" % (
+                args.theta, args.read_ratio)
+            workload = ("C3: 2^%d uint64 keys, 2^%d-op batches, key=to_key(1+zipf(%.2f)), "
+                        "%d%% get / %d%% insert (value = op index + 1)" % (
+                            args.keys_log2, args.batch_log2, args.theta, args.read_ratio,
+                            100 - args.read_ratio))
+            data = "synthetic: key(i)=CityHash64(i)+1 preload, zipf op stream"
         out = {
-            "metric": "batched get Mops/s (64M uint64 keys)",
+            "metric": metric,
             "value": round(mops, 2),
             "unit": "Mops/s",
             "n_gpus": world,
@@ -194,12 +262,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic: key(i)=CityHash64(i)+1, value=2i; uniform queries",
+            "data": data,
             "config": {
-                "workload": "C2: batched get, 2^%d uint64 keys/GPU, uniform 100%% read, "
-                            "2^%d-query batches%s" % (args.keys_log2, args.batch_log2,
-                                                        "" if world == 1 else
-                                                        ", range shards + RCCL all-to-all"),
+                "workload": workload,
                 "keys_per_gpu": n_keys,
                 "batch_per_gpu": batch,
                 "tree_height": st["height"],
@@ -224,6 +289,12 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if args.workload == "c3":
+            # whole-step algorithmic rate (gets 1040 B, inserts 1074 B per op)
+            step_s = elapsed / args.steps
+            b0 = mixed[0]
+            alg = (b0[0].numel() * ALG_BYTES_PER_GET + b0[1].numel() * ALG_BYTES_PER_INSERT)
+            out["roofline"]["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
@@ -231,65 +302,34 @@ def main():
     tree.close()
 
 
-def hash_ids(tree, ids, dev):
-    """key(i) = CityHash64(i) + 1 for an arbitrary id tensor (device)."""
-    import torch
-    # gen_keys hashes a contiguous range; hash ids chunk-wise via a sort-free
-    # route: compute on device with torch integer ops (same arithmetic as
-    # layout.h cityhash64_u64, 64-bit wrap-around).
-    return cityhash64_torch(ids) + 1
+def _oracle_on_gpu_image(tree):
+    from oracle.pyoracle import OracleTree
+    img, root = tree.dump_image()
+    orc = OracleTree(image=img, root_ptr=root, node_id=tree.node_id)
+    del img
+    return orc
 
 
-def cityhash64_torch(x):
-    import torch
-    M = (1 << 64) - 1
-
-    def c(v):  # signed int64 constant with the same bits
-        v &= M
-        return v - (1 << 64) if v >= (1 << 63) else v
-
-    k2 = c(0x9ae16a3b2f90404f)
-    mul = c(0x9ae16a3b2f90404f + 16)
-
-    def rot(v, s):
-        return ((v >> s) & ((1 << (64 - s)) - 1)) | (v << (64 - s))
-
-    def lsr(v, s):
-        return (v >> s) & ((1 << (64 - s)) - 1)
-
-    a = x + k2
-    b = x
-    cc = rot(b, 37) * mul + a
-    d = (rot(a, 25) + b) * mul
-    h = (cc ^ d) * mul
-    h = h ^ lsr(h, 47)
-    g = (d ^ h) * mul
-    g = g ^ lsr(g, 47)
-    return g * mul
+def _threads():
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return max(1, min(16, ncpu))
 
 
-def cpu_baseline(tree, qs, vals, found, args, step):
+def cpu_baseline_get(tree, qs, vals, found, args, step):
     """Reference Tree::search restated in C (oracle/, "port"), run on this
     host's cores over the GPU's own page image (identical tree), on a bounded
     sample: repeated 1 Mi-query batches for ~args.cpu_seconds."""
     import numpy as np
     import torch
 
-    from oracle.pyoracle import OracleTree
-
-    img, root = tree.dump_image()
-    orc = OracleTree(image=img, root_ptr=root, node_id=tree.node_id)
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(16, ncpu))
+    orc = _oracle_on_gpu_image(tree)
+    threads = _threads()
     q0 = qs[0].cpu().numpy().view(np.uint64)
-    # parity on one full batch: same queries through the GPU path
-    step(0)
+    step(0)  # parity on one full batch: same queries through the GPU path
     torch.cuda.synchronize()
     gv = vals.cpu().numpy().view(np.uint64)
     gf = found.cpu().numpy()
-    done = 0
-    secs = 0.0
-    parity = None
+    done, secs, parity = 0, 0.0, None
     while secs < args.cpu_seconds or done == 0:
         ov, of, s = orc.search_batch_mt(q0, threads)
         if parity is None:
@@ -297,7 +337,6 @@ def cpu_baseline(tree, qs, vals, found, args, step):
         secs += s
         done += q0.size
     orc.close()
-    del img
     cpu = {
         "value": round(done / secs / 1e6, 3),
         "unit": "Mops/s",
@@ -305,7 +344,51 @@ def cpu_baseline(tree, qs, vals, found, args, step):
         "kind": "port",
         "sample": f"{done} uniform gets ({done // q0.size} x 1 Mi batch) over the "
                   f"GPU-built tree image, oracle Tree::search restatement, "
-                  f"{threads} pinned threads on {platform.processor() or platform.machine()}",
+                  f"{threads} pinned threads on {cpu_name()}",
+    }
+    return cpu, parity
+
+
+def cpu_baseline_mixed(tree, mixed, vals, found, args, step):
+    """Mixed batches on the oracle over the GPU's image: gets on `threads`
+    pinned threads, then the batch's inserts (the restated Tree::insert is
+    single-threaded), for ~args.cpu_seconds.  Parity: the first two batches'
+    get results (the second sees the first's inserts) equal the GPU's."""
+    import numpy as np
+    import torch
+
+    orc = _oracle_on_gpu_image(tree)
+    threads = _threads()
+    parity = True
+    done, secs, b = 0, 0.0, 0
+    while secs < args.cpu_seconds or b < 2:
+        gk, pk, pv = mixed[b % N_BATCHES]
+        if b < 2:
+            step(b)
+            torch.cuda.synchronize()
+            gv = vals[:gk.numel()].cpu().numpy().view(np.uint64)
+            gf = found[:gk.numel()].cpu().numpy()
+        gkh = gk.cpu().numpy().view(np.uint64)
+        pkh = pk.cpu().numpy().view(np.uint64)
+        pvh = pv.cpu().numpy().view(np.uint64)
+        ov, of, s = orc.search_batch_mt(gkh, threads)
+        t0 = time.perf_counter()
+        orc.apply_batch(pkh, pvh)
+        s += time.perf_counter() - t0
+        if b < 2:
+            parity = parity and bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
+        secs += s
+        done += gkh.size + pkh.size
+        b += 1
+    orc.close()
+    cpu = {
+        "value": round(done / secs / 1e6, 3),
+        "unit": "Mops/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{b} mixed 1 Mi-op batches ({done} ops) over the GPU-built tree "
+                  f"image: gets on {threads} pinned threads, inserts on 1 thread "
+                  f"(oracle Tree::search / Tree::insert restatement) on {cpu_name()}",
     }
     return cpu, parity
 

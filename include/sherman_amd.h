@@ -153,6 +153,10 @@ int shm_route_unpermute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
 /* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */
 int shm_gen_keys(shm_tree *t, uint64_t first, uint64_t n, uint64_t keyspace,
                  uint64_t *keys_out, void *stream);
+/* keys[j] = CityHash64(ids[j]) + 1 (mod keyspace if keyspace != 0): to_key
+ * over an id array, e.g. a zipf stream (test/benchmark.cpp:43-46, 172-173) */
+int shm_hash_keys(shm_tree *t, const uint64_t *ids, uint64_t n, uint64_t keyspace,
+                  uint64_t *keys_out, void *stream);
 
 #ifdef __cplusplus
 }

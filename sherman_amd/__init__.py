@@ -104,6 +104,7 @@ _SIGNATURES = [
     ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
+    ("shm_hash_keys", ctypes.c_int, [vp, vp, u64, u64, vp, vp]),
 ]
 
 
@@ -302,6 +303,10 @@ class Tree:
     def route_unpermute(self, vals_in, perm, out, stream=None):
         _check(lib().shm_route_unpermute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
                                          _ptr(out), _stream_ptr(stream)), "unpermute")
+
+    def hash_keys(self, ids, out, keyspace=0, stream=None):
+        _check(lib().shm_hash_keys(self.h, _ptr(ids), ids.numel(), keyspace, _ptr(out),
+                                   _stream_ptr(stream)), "hash_keys")
 
     def gen_keys(self, first, n, out, keyspace=0, stream=None):
         _check(lib().shm_gen_keys(self.h, first, n, keyspace, _ptr(out),

@@ -106,6 +106,8 @@ void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
+void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_t* out,
+                     hipStream_t s);
 // stable bucketing by owning shard; cm = route_scratch_words(n) words
 uint64_t route_scratch_words(uint64_t n_max);
 void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,

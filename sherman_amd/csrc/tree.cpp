@@ -815,6 +815,14 @@ int shm_gen_keys(shm_tree* t, uint64_t first, uint64_t n, uint64_t keyspace,
   return SHM_OK;
 }
 
+int shm_hash_keys(shm_tree* t, const uint64_t* ids, uint64_t n, uint64_t keyspace,
+                  uint64_t* keys_out, void* stream) {
+  if (!t || (n && (!ids || !keys_out))) return SHM_EINVAL;
+  dev::launch_hash_ids(ids, n, keyspace, keys_out, pick(t, stream));
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
 }  // extern "C"
 
 // ---- internal test hooks (not part of include/sherman_amd.h) ----------------

@@ -128,6 +128,19 @@ void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
   if (n) hipLaunchKernelGGL(k_gen_keys, grid1(n), dim3(kT), 0, s, first, n, keyspace, out);
 }
 
+// keys[i] = to_key(ids[i]) for an arbitrary id array (zipf streams)
+__global__ void k_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace,
+                           uint64_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = cityhash64_u64(ids[i]) + 1;
+  out[i] = keyspace ? h % keyspace : h;
+}
+void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_t* out,
+                     hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_hash_ids, grid1(n), dim3(kT), 0, s, ids, n, keyspace, out);
+}
+
 // ---- multi-GPU routing: shard s owns [s*2^64/P, (s+1)*2^64/P) -------------
 __device__ __forceinline__ uint32_t owner_of(uint64_t k, uint32_t shards) {
   return (uint32_t)__umul64hi(k, (uint64_t)shards);

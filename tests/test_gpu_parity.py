@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 import sherman_amd as shm  # noqa: E402
-from oracle.pyoracle import OracleTree, to_key  # noqa: E402
+from oracle.pyoracle import OracleTree, op_mix, to_key, zipf_fill  # noqa: E402
 
 U64 = np.uint64
 
@@ -358,4 +358,32 @@ def test_sorted_get_skewed_and_ragged(lib_ok):
     ov, of = orc.search_batch(probe)
     gv, gf = gpu_search(t, probe)
     assert_same(probe, ov, of, gv, gf)
+    t.close()
+
+
+def test_mixed_zipf_batches_vs_oracle(lib_ok):
+    """Config C3 at small scale: zipf(0.99) key stream, 50 % get / 50 % insert
+    (oracle generators = the reference's zipf.h / rand_r restatement), batch
+    semantics of SURVEY §8a: each batch's gets see the previous batch's state,
+    then its inserts apply in batch order.  Every get result and the final
+    contents must equal the oracle's."""
+    n_items, batch = 1 << 16, 1 << 14
+    t = shm.Tree(arena_bytes=128 << 20, max_batch=1 << 15)
+    orc = OracleTree(128 << 20)
+    pre = hashed_keys(1, n_items + 1)
+    pv = np.arange(1, n_items + 1, dtype=U64) * U64(2)
+    gpu_insert(t, pre, pv)
+    orc.apply_batch(pre, pv)
+    for b in range(4):
+        ids = zipf_fill(n_items, 0.99, 0x5EED0000 + b, batch) + U64(1)
+        keys = np.array([to_key(int(i)) for i in ids], dtype=U64)
+        is_get = op_mix(b + 1, 50, batch).astype(bool)
+        op_val = np.arange(b * batch, (b + 1) * batch, dtype=U64) + U64(1)
+        gk, pk, pval = keys[is_get], keys[~is_get], op_val[~is_get]
+        ov, of = orc.search_batch(gk)
+        gv, gf = gpu_search(t, gk)
+        assert_same(gk, ov, of, gv, gf)
+        gpu_insert(t, pk, pval)
+        orc.apply_batch(pk, pval)
+    compare_contents(t, orc)
     t.close()
