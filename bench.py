@@ -129,7 +129,7 @@ def main():
     batch = 1 << args.batch_log2
     dev = torch.device(f"cuda:{local}")
     arena = max(2 << 30, n_keys * 48)
-    tree = shm.Tree(arena_bytes=arena, max_batch=1 << 20, device=local,
+    tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch), device=local,
                     node_id=rank, sort_gets=not args.no_sort)
 
     t0 = time.time()

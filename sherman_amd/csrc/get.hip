@@ -1,0 +1,342 @@
+// get.hip — batched Tree::search walk with grouped page resolution.
+//
+// Restates src/Tree.cpp:405-459 (search), 593-663 (page_search),
+// 665-685 (internal_page_search) and 687-697 (leaf_page_search) for a batch.
+//
+// One wave64 owns 64 queries, sorted by key across its lanes (bitonic, in
+// registers), so the queries waiting on one page form a run of lanes.  Each
+// round, the run heads' pages are fetched G at a time: one
+// global_load_lds_dwordx4 (1 KB LDS-DMA) per page into one of two G-page LDS
+// buffers, so group g + 1 is in flight while group g is resolved.  A group is
+// resolved by the whole wave at once, not page by page:
+//   * query side (lane = query): every lane reads the header of its own
+//     page's slot (per-lane LDS address; G distinct pages), checks versions
+//     (Tree.cpp:616-618) and fences (k >= highest -> sibling, 626-629), and
+//     for an internal page runs a 6-step branchless search over its page's
+//     keys (child = #keys <= k, 665-685);
+//   * entry side (lane = entries): the 64 lanes split into G groups of
+//     L = 64 / G lanes, group q holding slot q's 54 leaf entries, E = 54 / L
+//     consecutive entries per lane (one 18E-byte chunk).  Per step t, group q
+//     compares its entries with the key of query (head_q + t) of its run and
+//     the wave ballots the hits; the query lane takes the value of the first
+//     valid slot (key == k && value != 0 && f == r, Tree.cpp:687-697) with one
+//     lane permute.
+// The per-page scalar work (waits, header broadcasts, per-key ballots) of a
+// page-at-a-time walk is paid once per G pages.
+#include "device_common.h"
+#include "kernels.h"
+#include "lds_dma.h"
+
+namespace shm {
+namespace dev {
+
+namespace {
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* lp, int d) {
+  return (uint64_t)lp[d] | ((uint64_t)lp[d + 1] << 32);
+}
+
+// dword-pair funnel: the 4 bytes starting at byte offset o (compile time) of
+// a dword array
+template <int O, int N>
+__device__ __forceinline__ uint32_t bytes4(const uint32_t (&D)[N]) {
+  static_assert((O >> 2) + 1 < N || (O & 3) == 0, "chunk bound");
+  if constexpr ((O & 3) == 0) {
+    return D[O >> 2];
+  } else {
+    return __builtin_amdgcn_alignbyte(D[(O >> 2) + 1], D[O >> 2], O & 3);
+  }
+}
+template <int O, int N>
+__device__ __forceinline__ uint32_t byte1(const uint32_t (&D)[N]) {
+  return (D[O >> 2] >> (8 * (O & 3))) & 0xFF;
+}
+
+template <int J, int N>
+__device__ __forceinline__ void entry_at(const uint32_t (&D)[N], uint64_t& key, uint64_t& val,
+                                         bool& vok) {
+  constexpr int O = kLeafEntry * J;  // f @0, key @1, value @9, r @17
+  key = (uint64_t)bytes4<O + 1>(D) | ((uint64_t)bytes4<O + 5>(D) << 32);
+  val = (uint64_t)bytes4<O + 9>(D) | ((uint64_t)bytes4<O + 13>(D) << 32);
+  vok = ((byte1<O>(D) ^ byte1<O + 17>(D)) & 0xF) == 0;
+}
+
+}  // namespace
+
+template <int G, int NB, int WPB>
+__global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
+  constexpr int L = kWave / G;                               // lanes per page
+  constexpr int E = (kLeafCardinality + L - 1) / L;          // entries per lane
+  constexpr int CD = kLeafEntry * E / 4;                     // dwords per lane chunk
+  static_assert(kLeafEntry * E % 4 == 0, "lane chunks must be dword multiples");
+  static_assert(G * L == kWave, "G must divide 64");
+  static_assert(NB >= 1 && NB <= 4, "1..4 group buffers");
+  constexpr int kWaveRing = NB * G * kPageDwords;
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[WPB * kWaveRing];
+
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t n = a.n;
+  const uint64_t wave_base = ((uint64_t)blockIdx.x * WPB + (uint64_t)wv) * kWave;
+  if (wave_base >= n) return;  // wave-uniform
+  const uint32_t nact = (uint32_t)(n - wave_base < (uint64_t)kWave ? n - wave_base : kWave);
+  const uint64_t t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint32_t* ring = &s_ring[wv * kWaveRing];
+  const uint32_t ring_lds = lds_addr_of(ring);
+
+  // sort this wave's queries by key; tag = lane the query came from
+  uint64_t k = (uint32_t)lane < nact ? a.keys[wave_base + lane] : kKeyMax;
+  uint32_t tag = (uint32_t)lane;
+  wave_sort64(k, tag);
+  const bool active = tag < nact;
+
+  uint64_t ptr = a.start ? a.start[k >> a.start_shift] : a.root;
+  // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
+  bool done = !active || k == kKeyMax;
+  uint64_t val = 0;
+  uint32_t err = 0;
+  int rounds = 0, retries = 0;
+
+  // entry side: this lane holds entries [E*li, E*li + E) of slot q
+  const int q = lane / L;
+  const int li = lane % L;
+  // chunks stay inside the page: the last lane's chunk is shifted down to end
+  // at entry 53 and masks the entries its left neighbour owns; lanes past
+  // 54 / E mask everything
+  const int ebase = E * li < kLeafCardinality - E ? E * li : kLeafCardinality - E;
+  const int chunk_dw = (kOffRecords + kLeafEntry * ebase) / 4;
+  static_assert((kLeafCardinality - E) % 2 == 0, "chunk starts must be dword aligned");
+  const uint64_t lanemask_le = ~0ull >> (63 - lane);
+
+  for (;;) {
+    const uint64_t pend = ballot(!done);
+    if (pend == 0) break;
+    if (++rounds > kMaxRounds) {
+      err |= kErrRounds;
+      break;
+    }
+    // run heads: first lane of each run of equal page pointers
+    const int pl = lane == 0 ? 0 : lane - 1;
+    const uint64_t prev = shfl64(ptr, pl);
+    const bool prev_pend = ((pend >> pl) & 1) != 0;
+    const bool head = !done && (lane == 0 || !prev_pend || prev != ptr);
+    const uint64_t H = ballot(head);
+    const uint64_t Hle = H & lanemask_le;
+    const int run = popc64(Hle) - 1;          // run index of this (pending) lane
+    const int myhead = 63 - __builtin_clzll(Hle | 1ull);
+    const int ng = (popc64(H) + G - 1) / G;
+    // invalid pointers load the superblock (always mapped) and are rejected
+    // when resolved; padding slots of a short group load it too, so every
+    // group is exactly G DMAs and the waits below are constants
+    const bool pok = ptr_ok(ptr, a.node, a.arena_bytes);
+    const uint64_t pload = pok ? ptr : 0;
+    uint64_t hi = H;  // heads still to load
+    uint64_t hr = H;  // heads still to resolve
+
+    auto issue = [&](int b) {
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        uint64_t off = 0;
+        if (hi) {
+          off = ga_offset(rl64(pload, ctz64(hi)));
+          hi &= hi - 1;
+        }
+        glds16(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+      }
+    };
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (b < ng) issue(b);
+
+    for (int g = 0; g < ng; ++g) {
+      // groups issued after g: min(NB - 1, ng - 1 - g), G DMAs each
+      const int later = ng - 1 - g < NB - 1 ? ng - 1 - g : NB - 1;
+      if (later >= 3)
+        wait_vm<3 * G>();
+      else if (later == 2)
+        wait_vm<2 * G>();
+      else if (later == 1)
+        wait_vm<G>();
+      else
+        wait_vm<0>();
+      const int b = g % NB;
+      // head lane of each slot of this group (64 = padding)
+      int hq[G];
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        hq[s] = hr ? ctz64(hr) : 64;
+        hr &= hr - 1;
+      }
+      const uint32_t* buf = ring + b * G * kPageDwords;
+
+      // ---- one LDS trip: my page's header (query side), my entry chunk of
+      // slot q (entry side) and the key of slot q's first query --------------
+      const int slot = run - g * G;
+      const bool inq = !done && slot >= 0 && slot < G;
+      const uint32_t* lp = buf + (inq ? slot : 0) * kPageDwords;
+      const u32x4 A = *reinterpret_cast<const u32x4*>(lp);      // dwords 0..3
+      const u32x4 B = *reinterpret_cast<const u32x4*>(lp + 4);  // dwords 4..7
+      const u32x2 C = *reinterpret_cast<const u32x2*>(lp + 8);  // dwords 8..9
+      const uint32_t C2 = lp[10];
+      const u32x2 Z = *reinterpret_cast<const u32x2*>(lp + 254);
+      uint32_t D[CD];
+      {
+        const uint32_t* ep = buf + q * kPageDwords + chunk_dw;
+#pragma unroll
+        for (int i = 0; i < CD; ++i) D[i] = ep[i];
+      }
+      int hsrc = hq[0];
+#pragma unroll
+      for (int s = 1; s < G; ++s) hsrc = q == s ? hq[s] : hsrc;
+      uint64_t kq = shfl64(k, hsrc < 63 ? hsrc : 63);
+
+      const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
+                                ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
+      const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
+                               ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
+      const uint64_t lowest = (uint64_t)B.w | ((uint64_t)C.x << 32);
+      const uint64_t highest = (uint64_t)C.y | ((uint64_t)C2 << 32);
+      const int cnt = (int)(int16_t)(B.z >> 16) + 1;
+      const bool is_leaf = leftmost == 0;
+      const uint32_t rver = (is_leaf ? Z.x : Z.y) & 0xFF;
+      const bool vok = (A.z & 0xFF) == rver;
+      const bool live = inq && pok && vok;
+      const bool right = live && k >= highest;  // turn right
+      const bool low = live && k < lowest;      // mis-routed
+      const bool here = live && !right && !low;
+      const bool qint = here && !is_leaf;
+      const bool qleaf = here && is_leaf;
+      const uint64_t any_int = ballot(qint);
+      // the buffer is no longer needed once no internal page is searched in
+      // it: refill it now so the next group's pages land during the compute
+      bool refilled = false;
+      if (!any_int && g + NB < ng) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(b);
+        refilled = true;
+      }
+      if (ballot(inq && !pok)) err |= kErrBadPtr;
+      if (ballot(inq && pok && !vok)) {
+        // torn / in-flight page: its queries re-list it next round
+        if (++retries > kMaxRetries) err |= kErrInconsistent;
+      }
+      if (ballot(low)) err |= kErrFence;
+
+      // ---- internal pages: branchless search, lane = query ----------------
+      if (any_int) {
+        int pos = 0;  // number of keys <= k (keys strictly increase)
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+          const int idx = pos + step - 1;
+          const int ci = idx < 60 ? idx : 60;
+          const uint64_t kk = lds_u64(lp, 11 + 4 * ci);
+          pos += (idx < cnt && kk <= k) ? step : 0;
+        }
+        const uint64_t child = lds_u64(lp, 13 + 4 * (pos > 0 ? pos - 1 : 0));
+        ptr = qint ? (pos == 0 ? leftmost : child) : ptr;
+      }
+
+      // ---- leaf pages: lane groups hold the entries -----------------------
+      uint64_t lq = ballot(qleaf);
+      if (lq) {
+        uint64_t ekey[E], evalue[E];
+        bool eok[E];
+        entry_at<0>(D, ekey[0], evalue[0], eok[0]);
+        entry_at<1>(D, ekey[1], evalue[1], eok[1]);
+        if constexpr (E > 2) {
+          entry_at<2>(D, ekey[2], evalue[2], eok[2]);
+          entry_at<3>(D, ekey[3], evalue[3], eok[3]);
+        }
+        static_assert(E == 2 || E == 4, "entry unpack covers E = 2 and 4");
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+          eok[j] = eok[j] && evalue[j] != kValueNull && ebase + j >= li * E;
+        const int tl = lane - myhead;  // my position in my run
+        const int sl = slot & (G - 1);
+        for (int t = 0;; ++t) {
+          bool hit = false;
+          uint64_t hv = 0;
+#pragma unroll
+          for (int j = E - 1; j >= 0; --j) {  // lowest slot wins
+            const bool h = eok[j] && ekey[j] == kq;
+            hit = hit || h;
+            hv = h ? evalue[j] : hv;
+          }
+          const uint64_t M = ballot(hit);
+          const bool mine = qleaf && tl == t;
+          const uint64_t mq = (M >> (sl * L)) & (L == 64 ? ~0ull : ((1ull << (L & 63)) - 1));
+          const uint64_t v = shfl64(hv, sl * L + (mq ? ctz64(mq) : 0));
+          val = mine ? (mq ? v : 0) : val;
+          lq &= ~ballot(mine);
+          if (!lq) break;
+          const int src = hsrc + t + 1;
+          kq = shfl64(k, src < 63 ? src : 63);
+        }
+      }
+
+      ptr = right ? sibling : ptr;
+      done = done || (inq && !pok) || low || (right && sibling == 0) || qleaf ||
+             (qint && ptr == 0);
+      if (!refilled && g + NB < ng) {
+        // the buffer's LDS reads are complete before its next DMA lands
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(b);
+      }
+    }
+    if (retries > kMaxRetries) break;
+  }
+  if (err) atomicOr(a.err, err);
+  if (a.stamps && lane < 2) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    a.stamps[2 * (wave_base / kWave) + lane] = lane == 0 ? t_start : t_end;
+  }
+  if (active) {
+    const uint64_t i = wave_base + tag;
+    const uint64_t o = a.perm ? (uint64_t)a.perm[i] : i;
+    a.out_val[o] = val;
+    if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
+  }
+}
+
+// SHM_GET_CFG="G,NB,WPB" picks pages per group, group buffers per wave and
+// waves per block (measurement knob; default 4,1,4)
+static int get_cfg() {
+  static const int c = [] {
+    const char* e = getenv("SHM_GET_CFG");
+    int g = 4, nb = 1, w = 4;
+    if (e) sscanf(e, "%d,%d,%d", &g, &nb, &w);
+    return g * 100 + nb * 10 + w;
+  }();
+  return c;
+}
+
+template <int G, int NB, int WPB>
+static void launch_cfg(const WalkArgs& a, uint64_t waves, hipStream_t s) {
+  const dim3 grid((unsigned)((waves + WPB - 1) / WPB));
+  hipLaunchKernelGGL((k_get<G, NB, WPB>), grid, dim3(WPB * kWave), 0, s, a);
+}
+
+void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s) {
+  if (n == 0) return;
+  const uint64_t waves = (n + kWave - 1) / kWave;
+  switch (get_cfg()) {
+    case 414: launch_cfg<4, 1, 4>(a, waves, s); break;
+    case 411: launch_cfg<4, 1, 1>(a, waves, s); break;
+    case 214: launch_cfg<2, 1, 4>(a, waves, s); break;
+    case 221: launch_cfg<2, 2, 1>(a, waves, s); break;
+    case 224: launch_cfg<2, 2, 4>(a, waves, s); break;
+    case 231: launch_cfg<2, 3, 1>(a, waves, s); break;
+    case 241: launch_cfg<2, 4, 1>(a, waves, s); break;
+    case 244: launch_cfg<2, 4, 4>(a, waves, s); break;
+    case 421: launch_cfg<4, 2, 1>(a, waves, s); break;
+    case 431: launch_cfg<4, 3, 1>(a, waves, s); break;
+    case 422: launch_cfg<4, 2, 2>(a, waves, s); break;
+    case 424: launch_cfg<4, 2, 4>(a, waves, s); break;
+    default: launch_cfg<4, 1, 4>(a, waves, s); break;
+  }
+}
+
+}  // namespace dev
+}  // namespace shm

@@ -21,10 +21,25 @@ struct WalkArgs {
   uint64_t* out_page;     // LOCATE
   int target_level;       // LOCATE
   uint32_t* err;
+  // GET: per-key-prefix start pages (nullable -> every query starts at root)
+  const uint64_t* start;
+  uint32_t start_shift;   // prefix = key >> start_shift
+  // diagnostics (nullable): per wave {start, end} s_memrealtime stamps
+  uint64_t* stamps;
 };
 
 void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
                  hipStream_t s);
+// batched get walk with grouped page resolution (get.hip)
+void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
+// start[p] = the deepest page whose fences cover every key with prefix p
+// (key >> (64 - bits) == p), found by walking from root.  A page's lowest
+// fence never changes (a split keeps the left half in place), so a start page
+// stays a valid B-link entry point for its prefix after later splits: keys
+// past its highest fence move right (Tree.cpp:626-629).
+void launch_start_table(const uint8_t* arena, uint64_t arena_bytes, uint16_t node,
+                        uint64_t root, uint32_t bits, uint64_t* table, uint32_t* err,
+                        hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 struct SegArgs {

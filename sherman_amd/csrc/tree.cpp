@@ -29,6 +29,7 @@ constexpr uint64_t kSortMinGets = 8192;   // below this, walk in input order
 
 
 constexpr uint32_t kDefaultSortBits = 16; // top key bits that order gets (8 + 8)
+constexpr uint32_t kStartBits = 16;       // get start table: 2^16 prefixes
 constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
 
 }  // namespace
@@ -69,6 +70,10 @@ struct shm_tree {
   uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
   uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
+  // get start pages per key prefix (dev::launch_start_table); rebuilt before a
+  // search when pages were added or the root moved since it was built
+  uint64_t* start = nullptr;
+  uint64_t start_np = ~0ull, start_root = ~0ull;
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
@@ -109,6 +114,45 @@ hipStream_t pick(shm_tree* t, void* s) {
   (void)t;
   return (hipStream_t)s;
 }
+
+// SHM_GET_KERNEL=walk selects the page-at-a-time walk (k_walk) for gets
+// instead of the grouped one (k_get): an A/B switch for measurements.
+bool get_kernel_v4() {
+  static const bool v4 = [] {
+    const char* e = getenv("SHM_GET_KERNEL");
+    return e && strcmp(e, "walk") == 0;
+  }();
+  return v4;
+}
+
+// SHM_GET_STAMPS=<file>: append the per-wave {start, end} s_memrealtime
+// stamps (100 MHz) of every get walk launch to <file> (diagnostics only;
+// synchronises the stream after each launch).
+struct StampDump {
+  uint64_t* d = nullptr;
+  uint64_t n = 0;
+  hipStream_t s;
+  StampDump(dev::WalkArgs& a, uint64_t m, hipStream_t st) : s(st) {
+    static const char* path = getenv("SHM_GET_STAMPS");
+    if (!path) return;
+    n = 2 * ((m + 63) / 64);
+    if (hipMalloc((void**)&d, n * 8) != hipSuccess) d = nullptr;
+    a.stamps = d;
+  }
+  ~StampDump() {
+    if (!d) return;
+    std::vector<uint64_t> h(n);
+    if (hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+      if (FILE* f = fopen(getenv("SHM_GET_STAMPS"), "ab")) {
+        fwrite(&n, 8, 1, f);
+        fwrite(h.data(), 8, n, f);
+        fclose(f);
+      }
+    }
+    (void)hipFree(d);
+  }
+};
 
 dev::WalkArgs walk_args(shm_tree* t) {
   dev::WalkArgs a{};
@@ -383,7 +427,7 @@ void free_all(shm_tree* t) {
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
-  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks);
+  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start);
   for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -555,6 +599,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_hist, dev::kPartHistWords);
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
+  rc |= dalloc(&t->start, 1ull << kStartBits);
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
@@ -592,6 +637,13 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   if (!t || (n && (!keys || !vals_out))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
+  const bool use_start = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
+  if (use_start && (t->start_np != t->next_page || t->start_root != t->root)) {
+    dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, kStartBits,
+                            t->start, t->d_err, s);
+    t->start_np = t->next_page;
+    t->start_root = t->root;
+  }
   for (uint64_t off = 0; off < n; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
     dev::WalkArgs a = walk_args(t);
@@ -619,6 +671,8 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.perm = t->ib;
       a.out_val = t->kb;
       a.out_found = nullptr;
+      a.start = t->start;
+      a.start_shift = 64 - kStartBits;
       gathered = true;
       DBG(s, "sort(get)");
     } else {
@@ -626,7 +680,12 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.perm = nullptr;
     }
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e1, s));
-    dev::launch_walk(a, m, kWalkDepth, false, s);
+    if (get_kernel_v4()) {
+      dev::launch_walk(a, m, kWalkDepth, false, s);
+    } else {
+      StampDump sd(a, m, s);
+      dev::launch_get(a, m, s);
+    }
     DBG(s, "walk(get)");
     if (t->prof_on) {
       HIP_OK(hipEventRecord(pr.e2, s));
@@ -741,6 +800,7 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   t->root = root_ptr;
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;
+  t->start_np = ~0ull;  // contents changed: rebuild the get start table
   return write_superblock(t, t->stream);
 }
 

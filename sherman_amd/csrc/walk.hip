@@ -24,38 +24,12 @@
 // share their internal pages and same-leaf queries share one leaf read.
 #include "device_common.h"
 #include "kernels.h"
-
-// m0 is set by the LDS-DMA asm below; nothing else in these kernels uses it
-#pragma clang diagnostic ignored "-Winline-asm"
+#include "lds_dma.h"
 
 namespace shm {
 namespace dev {
 
 namespace {
-
-// One page -> one LDS slot: global_load_lds_dwordx4, lane l's 16 bytes land
-// at lds_addr + 16 l.  Issued from inline asm on purpose: hipcc treats a
-// visible LDS-DMA as a pending LDS write and puts s_waitcnt vmcnt(0) in front
-// of every later ds_read, which would drain the whole ring; the ring's waits
-// are counted by hand instead (wait_vm below).
-__device__ __forceinline__ void glds16(const uint8_t* page, uint32_t lds_addr) {
-  const uint64_t ga = (uint64_t)(page + 16 * lane_id());
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "global_load_lds_dwordx4 %0, off"
-      :
-      : "v"(ga), "s"(lds_addr)
-      : "memory", "m0");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ uint32_t rfl(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -88,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
   wave_sort64(k, tag);
   const bool active = tag < nact;
 
-  uint64_t ptr = a.root;
+  uint64_t ptr = (!LOCATE && a.start) ? a.start[k >> a.start_shift] : a.root;
   bool done = !active;
   uint64_t val = 0, page_out = 0;
   // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
@@ -224,6 +198,74 @@ __global__ __launch_bounds__(kBlock) void k_walk(WalkArgs a) {
       if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
     }
   }
+}
+
+namespace {
+// 4-byte aligned u64 at byte offset o of a page
+__device__ __forceinline__ uint64_t pg_u64(const uint8_t* pg, int o) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(pg + o);
+  return (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+}
+// u64 at byte offset 4d+1 (leftmost @9, sibling @17)
+__device__ __forceinline__ uint64_t pg_u64_b1(const uint8_t* pg, int d) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(pg) + d;
+  return (uint64_t)((w[0] >> 8) | (w[1] << 24)) | ((uint64_t)((w[1] >> 8) | (w[2] << 24)) << 32);
+}
+// internal_page_search (Tree.cpp:665-685): index of the child covering x,
+// 0 = leftmost, j + 1 = records[j]
+__device__ __forceinline__ int child_index(const uint8_t* pg, int cnt, uint64_t x) {
+  int lo = 0, hi = cnt;  // number of keys <= x
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (pg_u64(pg, kOffRecords + kInternalEntry * mid) <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_start_table(const uint8_t* __restrict__ arena,
+                                                     uint64_t arena_bytes, uint16_t node,
+                                                     uint64_t root, uint32_t bits,
+                                                     uint64_t* __restrict__ table,
+                                                     uint32_t* err) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >> bits) return;
+  const uint64_t lo = p << (64 - bits);
+  const uint64_t hi = lo | (~0ull >> bits);
+  uint64_t ptr = root;
+  for (int it = 0; it < 256; ++it) {
+    if (!ptr_ok(ptr, node, arena_bytes)) {
+      atomicOr(err, kErrBadPtr);
+      ptr = root;
+      break;
+    }
+    const uint8_t* pg = arena + ga_offset(ptr);
+    const uint64_t leftmost = pg_u64_b1(pg, 2);
+    const uint64_t sibling = pg_u64_b1(pg, 4);
+    const uint64_t highest = pg_u64(pg, kOffHighest);
+    if (lo >= highest) {  // B-link turn right (Tree.cpp:626-629)
+      if (sibling == 0) break;
+      ptr = sibling;
+      continue;
+    }
+    if (leftmost == 0 || hi >= highest) break;  // leaf, or prefix leaves this page
+    const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
+    const int c = child_index(pg, cnt, lo);
+    if (child_index(pg, cnt, hi) != c) break;  // prefix spans two children
+    ptr = c == 0 ? leftmost : pg_u64(pg, kOffRecords + kInternalEntry * (c - 1) + 8);
+  }
+  table[p] = ptr;
+}
+
+void launch_start_table(const uint8_t* arena, uint64_t arena_bytes, uint16_t node,
+                        uint64_t root, uint32_t bits, uint64_t* table, uint32_t* err,
+                        hipStream_t s) {
+  const uint64_t n = 1ull << bits;
+  hipLaunchKernelGGL(k_start_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     arena, arena_bytes, node, root, bits, table, err);
 }
 
 static int ring_depth() {

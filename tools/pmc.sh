@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/p$i -o run \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_get|k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/p$i -o run \
     -- python3 $R/bench.py --steps 3 --warmup 1 --profile-steps 0 --no-cpu-baseline \
     > $OUT/p$i.json 2> $OUT/p$i.err || exit $?
 done

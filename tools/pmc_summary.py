@@ -11,8 +11,8 @@ agg = collections.defaultdict(list)
 for p in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
         n = r["Kernel_Name"]
-        for tag in ("k_walk<false", "k_part_hist", "k_part_scatter", "k_gather_results",
-                    "k_part_colscan"):
+        for tag in ("k_get<", "k_walk<false", "k_part_coarse_hist", "k_part_coarse_scatter",
+                    "k_part_fine", "k_unpartition"):
             if tag in n:
                 agg[(tag, r["Counter_Name"])].append(float(r["Counter_Value"]))
 out = collections.defaultdict(dict)

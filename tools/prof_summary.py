@@ -9,7 +9,7 @@ import os
 import sys
 
 
-def main(d, match=("k_walk", "k_part", "k_unpart", "k_gather")):
+def main(d, match=("k_get", "k_walk", "k_part", "k_unpart", "k_gather")):
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     out = {"kernels": {}, "pmc": {}}
     for r in stats:

@@ -11,8 +11,8 @@ cd /tmp && export TMPDIR=/tmp
 ARGS="--no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run \
   -- python3 $R/bench.py --steps 20 --warmup 5 $ARGS > $OUT/trace_bench.json 2> $OUT/trace_bench.err || exit $?
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/pmc_fetch -o run \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_get|k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/pmc_fetch -o run \
   -- python3 $R/bench.py --steps 5 --warmup 1 --profile-steps 0 $ARGS > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/pmc_write -o run \
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_get|k_walk|k_part|k_unpart|k_gather" --output-format csv -d $OUT/pmc_write -o run \
   -- python3 $R/bench.py --steps 5 --warmup 1 --profile-steps 0 $ARGS > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit $?
 find $OUT -name "*.csv" | head -50
