@@ -280,7 +280,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_walk<false>",
+                "kernel": "k_get<4,1,4>",
                 "alg_bytes_per_get": ALG_BYTES_PER_GET,
                 "walk_ms_per_launch": round(walk_ms, 4),
                 "order_ms_per_launch": round(order_ms, 4),

@@ -199,18 +199,22 @@ __device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,
          off >= kPageSize && off + kPageSize <= arena_bytes;
 }
 
-// in-wave ascending bitonic sort of (key, tag) over 64 lanes
+// in-wave ascending bitonic sort of (key, tag) over 64 lanes; branch-free
+// compare-exchange (xor shuffles with constant masks)
 __device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& tag) {
   const int l = lane_id();
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint64_t pk = shfl64(key, l ^ j);
-      const uint32_t pt = shfl32(tag, l ^ j);
-      const bool up = (l & k) == 0;
-      const bool lower = (l & j) == 0;
-      const bool take = lower == up ? (pk < key) : (pk > key);
+      const uint64_t pk = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)key, j) |
+                          ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), j) << 32);
+      const uint32_t pt = (uint32_t)__shfl_xor((int)tag, j);
+      // keep the smaller key iff this lane is the lower one of an ascending
+      // pair or the upper one of a descending pair
+      const uint32_t want_min = (uint32_t)(((l & k) == 0) == ((l & j) == 0));
+      const uint32_t take = (want_min & (uint32_t)(pk < key)) |
+                            ((want_min ^ 1u) & (uint32_t)(pk > key));
       key = take ? pk : key;
       tag = take ? pt : tag;
     }

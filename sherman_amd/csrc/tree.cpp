@@ -29,7 +29,15 @@ constexpr uint64_t kSortMinGets = 8192;   // below this, walk in input order
 
 
 constexpr uint32_t kDefaultSortBits = 16; // top key bits that order gets (8 + 8)
-constexpr uint32_t kStartBits = 16;       // get start table: 2^16 prefixes
+// get start table: 2^bits key prefixes (SHM_START_BITS, 8..22, default 16)
+uint32_t start_bits() {
+  static const uint32_t b = [] {
+    const char* e = getenv("SHM_START_BITS");
+    const int v = e ? atoi(e) : 16;
+    return (uint32_t)(v < 8 ? 8 : v > 22 ? 22 : v);
+  }();
+  return b;
+}
 constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
 
 }  // namespace
@@ -599,7 +607,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_hist, dev::kPartHistWords);
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
-  rc |= dalloc(&t->start, 1ull << kStartBits);
+  rc |= dalloc(&t->start, 1ull << start_bits());
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
@@ -639,7 +647,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   hipStream_t s = pick(t, stream);
   const bool use_start = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
   if (use_start && (t->start_np != t->next_page || t->start_root != t->root)) {
-    dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, kStartBits,
+    dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, start_bits(),
                             t->start, t->d_err, s);
     t->start_np = t->next_page;
     t->start_root = t->root;
@@ -672,7 +680,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.out_val = t->kb;
       a.out_found = nullptr;
       a.start = t->start;
-      a.start_shift = 64 - kStartBits;
+      a.start_shift = 64 - start_bits();
       gathered = true;
       DBG(s, "sort(get)");
     } else {
