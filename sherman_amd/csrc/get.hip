@@ -79,7 +79,17 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t n = a.n;
-  const uint64_t wave_base = ((uint64_t)blockIdx.x * WPB + (uint64_t)wv) * kWave;
+  // XCD-aware chunk order: blocks are dealt to the 8 XCDs round-robin
+  // (block b -> XCD b % 8; placement only affects speed), so give each XCD a
+  // contiguous run of chunks.  Neighbouring chunks share internal pages and
+  // write their results into one fine-partition range, and both then stay in
+  // one XCD's L2 instead of being fetched / partially written back by eight.
+  const uint32_t nb = gridDim.x, bx = blockIdx.x;
+  const uint32_t xcd = a.xcd_remap ? bx & 7u : 0u, per = nb >> 3, rem = nb & 7u;
+  const uint32_t lblock = a.xcd_remap
+                              ? xcd * per + (xcd < rem ? xcd : rem) + (bx >> 3)
+                              : bx;
+  const uint64_t wave_base = ((uint64_t)lblock * WPB + (uint64_t)wv) * kWave;
   if (wave_base >= n) return;  // wave-uniform
   const uint32_t nact = (uint32_t)(n - wave_base < (uint64_t)kWave ? n - wave_base : kWave);
   const uint64_t t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -92,7 +102,26 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   wave_sort64(k, tag);
   const bool active = tag < nact;
 
-  uint64_t ptr = a.start ? a.start[k >> a.start_shift] : a.root;
+  uint64_t ptr = a.root;
+  if (a.dir) {
+    // leaf directory: start at the leaf (or the covering internal page)
+    const uint64_t p = (k - a.dir_lo) >> a.dir_shift;
+    if (k >= a.dir_lo && p < a.dir_n && k != kKeyMax) {
+      const u32x4* e = reinterpret_cast<const u32x4*>(a.dir + 8 * p);
+      const u32x4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+      const uint64_t sep1 = (uint64_t)e2.x | ((uint64_t)e2.y << 32);
+      const uint64_t sep2 = (uint64_t)e2.z | ((uint64_t)e2.w << 32);
+      const uint64_t sep3 = (uint64_t)e3.x | ((uint64_t)e3.y << 32);
+      const uint32_t cnt = e3.z;
+      const uint32_t i = (uint32_t)(cnt > 1 && k >= sep1) + (uint32_t)(cnt > 2 && k >= sep2) +
+                         (uint32_t)(cnt > 3 && k >= sep3);
+      const uint32_t lo32 = i == 0 ? e0.x : i == 1 ? e0.z : i == 2 ? e1.x : e1.z;
+      const uint32_t hi32 = i == 0 ? e0.y : i == 1 ? e0.w : i == 2 ? e1.y : e1.w;
+      ptr = (uint64_t)lo32 | ((uint64_t)hi32 << 32);
+    }
+  } else if (a.start) {
+    ptr = a.start[k >> a.start_shift];
+  }
   // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
   bool done = !active || k == kKeyMax;
   uint64_t val = 0;

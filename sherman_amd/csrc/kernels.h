@@ -24,6 +24,14 @@ struct WalkArgs {
   // GET: per-key-prefix start pages (nullable -> every query starts at root)
   const uint64_t* start;
   uint32_t start_shift;   // prefix = key >> start_shift
+  // GET: leaf directory (leafdir.hip; nullable): 8 u64 per entry, entry p
+  // covers keys [dir_lo + (p << dir_shift), ... + 2^dir_shift)
+  const uint64_t* dir;
+  uint64_t dir_lo;
+  uint64_t dir_n;
+  uint32_t dir_shift;
+  // GET: map blocks to chunks XCD-contiguously (see get.hip)
+  int xcd_remap;
   // diagnostics (nullable): per wave {start, end} s_memrealtime stamps
   uint64_t* stamps;
 };
@@ -40,6 +48,11 @@ void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
 void launch_start_table(const uint8_t* arena, uint64_t arena_bytes, uint16_t node,
                         uint64_t root, uint32_t bits, uint64_t* table, uint32_t* err,
                         hipStream_t s);
+// leaf directory (leafdir.hip): n_ent entries of 8 u64 from dir_lo, 2^shift
+// keys each
+void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                     uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
+                     uint32_t* err, hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 struct SegArgs {

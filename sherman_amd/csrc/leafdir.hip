@@ -1,0 +1,126 @@
+// leafdir.hip — the leaf directory: a flat index from key prefixes to leaves.
+//
+// Plays the role of Sherman's index cache (src/IndexCache.h, include/
+// CacheEntry.h: cached level-1 pages let a search jump straight to its leaf;
+// dead in the reference fork, Directory.cpp:8/77-79) for the batched get.
+// Entry p covers keys [lo_p, lo_p + 2^shift), lo_p = dir_lo + (p << shift),
+// and lists the up to four leaves that cover that range, in key order:
+//   u64[8] = {ptr0, ptr1, ptr2, ptr3, sep1, sep2, sep3, n}
+// with sep_i = lowest fence of ptr_i; a query k starts at ptr_i for the
+// largest i < n with sep_i <= k.  n == 0 marks a prefix spanning more than
+// four leaves: ptr0 is then the deepest internal page whose fences cover the
+// whole prefix.
+//
+// Stale entries stay correct: a page's lowest fence never changes (a split
+// keeps the left half in place, Tree.cpp:926-945), so ptr_i remains a valid
+// B-link entry point for keys >= sep_i and keys past its current highest
+// fence move right along the sibling chain (Tree.cpp:626-629).  The host
+// rebuilds the directory when the tree has grown enough to make the extra
+// hops matter.
+#include "device_common.h"
+#include "kernels.h"
+
+namespace shm {
+namespace dev {
+
+namespace {
+__device__ __forceinline__ uint64_t pg64(const uint8_t* pg, int o) {  // 4-aligned
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(pg + o);
+  return (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+}
+__device__ __forceinline__ uint64_t pg64_b1(const uint8_t* pg, int d) {  // byte 4d+1
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(pg) + d;
+  return (uint64_t)((w[0] >> 8) | (w[1] << 24)) | ((uint64_t)((w[1] >> 8) | (w[2] << 24)) << 32);
+}
+// internal_page_search (Tree.cpp:665-685): number of keys <= x
+__device__ __forceinline__ int keys_le(const uint8_t* pg, int cnt, uint64_t x) {
+  int lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (pg64(pg, kOffRecords + kInternalEntry * mid) <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ arena,
+                                                  uint64_t arena_bytes, uint16_t node,
+                                                  uint64_t root, uint64_t dir_lo,
+                                                  uint32_t shift, uint64_t n_ent,
+                                                  uint64_t* __restrict__ dir, uint32_t* err) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_ent) return;
+  const uint64_t lo = dir_lo + (p << shift);
+  const uint64_t span = (1ull << shift) - 1;
+  const uint64_t hi = lo > ~0ull - span ? ~0ull : lo + span;
+  uint64_t ptr = root, cover = root;
+  uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool ok = false;
+  for (int it = 0; it < 4096; ++it) {
+    if (!ptr_ok(ptr, node, arena_bytes)) break;
+    const uint8_t* pg = arena + ga_offset(ptr);
+    const uint64_t leftmost = pg64_b1(pg, 2);
+    const uint64_t sibling = pg64_b1(pg, 4);
+    const uint64_t highest = pg64(pg, kOffHighest);
+    if (lo >= highest) {  // turn right (Tree.cpp:626-629)
+      if (sibling == 0) break;
+      ptr = sibling;
+      continue;
+    }
+    if (leftmost != 0) {  // internal: descend towards lo
+      const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
+      const int c = keys_le(pg, cnt, lo);
+      if (hi < highest && keys_le(pg, cnt, hi) == c) cover = ptr;  // whole prefix below
+      ptr = c == 0 ? leftmost : pg64(pg, kOffRecords + kInternalEntry * (c - 1) + 8);
+      continue;
+    }
+    // leaf containing lo; collect the leaves that cover [lo, hi]
+    out[0] = ptr;
+    uint64_t h = highest, sib = sibling;
+    int n = 1;
+    while (h <= hi && sib != 0 && n <= 4) {
+      if (n == 4 || !ptr_ok(sib, node, arena_bytes)) {
+        n = 5;  // too many leaves: fall back to the covering internal page
+        break;
+      }
+      const uint8_t* sp = arena + ga_offset(sib);
+      out[n] = sib;
+      out[3 + n] = pg64(sp, kOffLowest);  // sep_n = lowest of ptr_n
+      h = pg64(sp, kOffHighest);
+      sib = pg64_b1(sp, 4);
+      ++n;
+    }
+    if (n <= 4) {
+      out[7] = (uint64_t)n;
+    } else {
+      for (int i = 0; i < 8; ++i) out[i] = 0;
+      out[0] = cover;
+    }
+    ok = true;
+    break;
+  }
+  if (!ok) {
+    atomicOr(err, kErrBadPtr);
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    out[0] = root;
+  }
+  u32x4* e = reinterpret_cast<u32x4*>(dir + 8 * p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    e[i] = u32x4{(uint32_t)out[2 * i], (uint32_t)(out[2 * i] >> 32), (uint32_t)out[2 * i + 1],
+                 (uint32_t)(out[2 * i + 1] >> 32)};
+}
+
+void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                     uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
+                     uint32_t* err, hipStream_t s) {
+  if (!n_ent) return;
+  hipLaunchKernelGGL(k_leaf_dir, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s, arena,
+                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, err);
+}
+
+}  // namespace dev
+}  // namespace shm

@@ -82,6 +82,13 @@ struct shm_tree {
   // search when pages were added or the root moved since it was built
   uint64_t* start = nullptr;
   uint64_t start_np = ~0ull, start_root = ~0ull;
+  // leaf directory (leafdir.hip): 2^dir_bits entries of 64 B over the whole
+  // key space, rebuilt before a search once the tree grew by 1/32 since the
+  // last build (stale entries only cost B-link right moves)
+  uint64_t* dir = nullptr;
+  uint32_t dir_bits = 0;
+  uint64_t dir_np = 0;
+  bool dir_valid = false;
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
@@ -170,6 +177,38 @@ dev::WalkArgs walk_args(shm_tree* t) {
   a.root = t->root;
   a.err = t->d_err;
   return a;
+}
+
+// SHM_LEAF_DIR=0 starts gets from the prefix start table instead of the
+// leaf directory (A/B switch)
+bool use_leaf_dir() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_LEAF_DIR");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+// (re)build the leaf directory when missing or the tree grew by > 1/32;
+// 2^bits entries with bits = ceil(log2(pages)) (~1 entry per leaf)
+int refresh_dir(shm_tree* t, hipStream_t s) {
+  if (t->dir_valid && t->next_page <= t->dir_np + t->dir_np / 32) return SHM_OK;
+  uint32_t bits = 10;
+  while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
+  if (!t->dir || bits != t->dir_bits) {
+    if (t->dir) {
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipFree(t->dir));
+      t->dir = nullptr;
+    }
+    if (dalloc(&t->dir, 8ull << bits)) return SHM_ENOMEM;
+    t->dir_bits = bits;
+  }
+  dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, 0, 64 - bits,
+                       1ull << bits, t->dir, t->d_err, s);
+  t->dir_np = t->next_page;
+  t->dir_valid = true;
+  return SHM_OK;
 }
 
 dev::SegArgs seg_args(shm_tree* t) {
@@ -435,7 +474,7 @@ void free_all(shm_tree* t) {
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
-  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start);
+  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir);
   for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -646,7 +685,10 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
   const bool use_start = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
-  if (use_start && (t->start_np != t->next_page || t->start_root != t->root)) {
+  if (use_start && use_leaf_dir()) {
+    const int rc = refresh_dir(t, s);
+    if (rc) return rc;
+  } else if (use_start && (t->start_np != t->next_page || t->start_root != t->root)) {
     dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, start_bits(),
                             t->start, t->d_err, s);
     t->start_np = t->next_page;
@@ -679,8 +721,16 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.perm = t->ib;
       a.out_val = t->kb;
       a.out_found = nullptr;
-      a.start = t->start;
-      a.start_shift = 64 - start_bits();
+      a.xcd_remap = getenv("SHM_XCD_REMAP") ? atoi(getenv("SHM_XCD_REMAP")) : 1;
+      if (use_leaf_dir()) {
+        a.dir = t->dir;
+        a.dir_lo = 0;
+        a.dir_shift = 64 - t->dir_bits;
+        a.dir_n = 1ull << t->dir_bits;
+      } else {
+        a.start = t->start;
+        a.start_shift = 64 - start_bits();
+      }
       gathered = true;
       DBG(s, "sort(get)");
     } else {
@@ -809,6 +859,7 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;
   t->start_np = ~0ull;  // contents changed: rebuild the get start table
+  t->dir_valid = false;  // and the leaf directory
   return write_superblock(t, t->stream);
 }
 
