@@ -387,3 +387,40 @@ def test_mixed_zipf_batches_vs_oracle(lib_ok):
         orc.apply_batch(pk, pval)
     compare_contents(t, orc)
     t.close()
+
+
+def test_leaf_dir_stale_after_splits(lib_ok):
+    """The get path starts from the leaf directory (leafdir.hip), built at the
+    first search and rebuilt only after the tree grew by 1/32.  Inserts that
+    split leaves in between leave entries pointing at pages whose high fence
+    moved left; those gets must still be exact (B-link right moves)."""
+    n0 = 1 << 18
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18)
+    orc = OracleTree(512 << 20)
+    base = hashed_keys(1, n0 + 1)
+    bv = np.arange(1, n0 + 1, dtype=U64) * U64(2)
+    gpu_insert(t, base, bv)
+    orc.apply_batch(base, bv)
+    rng = np.random.default_rng(17)
+    probe = base[rng.integers(0, n0, 1 << 16)]
+    assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))  # builds the directory
+    pages0 = t.stats()["pages_used"]
+    nxt = n0 + 1
+    for step in range(3):
+        # 30 new keys right after each of 60 existing keys: those leaves
+        # overflow and split (~1-2 % more pages, below the rebuild threshold
+        # at least for the first step)
+        anchors = base[rng.integers(0, n0, 60)]
+        add = np.unique((anchors[:, None] + np.arange(1, 31, dtype=U64)[None, :]).ravel())
+        add = add[~np.isin(add, base)]
+        av = np.arange(nxt, nxt + add.size, dtype=U64) * U64(7)
+        nxt += add.size
+        gpu_insert(t, add, av)
+        orc.apply_batch(add, av)
+        probe = np.concatenate([add, add + U64(1 << 20), base[rng.integers(0, n0, 30000)]])
+        assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))
+        if step == 0:
+            assert pages0 < t.stats()["pages_used"] <= pages0 + pages0 // 32
+    assert t.stats()["pages_used"] > pages0
+    compare_contents(t, orc)
+    t.close()
