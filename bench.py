@@ -57,6 +57,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--no-sort", action="store_true", help="walk gets in input order")
     p.add_argument("--profile-steps", type=int, default=10)
+    p.add_argument("--sim-world", type=int, default=1,
+                   help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
+                        "range partition (the per-GPU work of an N-GPU run, no exchange)")
+    p.add_argument("--sim-rank", type=int, default=0)
+    p.add_argument("--no-range-hint", action="store_true",
+                   help="do not pass the shard key range to the tree (A/B)")
     return p.parse_args()
 
 
@@ -129,11 +135,16 @@ def main():
     batch = 1 << args.batch_log2
     dev = torch.device(f"cuda:{local}")
     arena = max(2 << 30, n_keys * 48)
+    from sherman_amd.shard import shard_range
+    sim = world == 1 and args.sim_world > 1
+    s_rank, s_world = (args.sim_rank, args.sim_world) if sim else (rank, world)
+    key_lo, key_bits = (0, 64) if args.no_range_hint else shard_range(s_rank, s_world)
     tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch), device=local,
-                    node_id=rank, sort_gets=not args.no_sort)
+                    node_id=rank, sort_gets=not args.no_sort, key_lo=key_lo, key_bits=key_bits)
 
     t0 = time.time()
-    keys_local, inserted = build_shard(tree, n_keys, world, rank, dev)
+    keys_local, inserted = build_shard(tree, n_keys, s_world, s_rank, dev)
+    n_keys = inserted if sim else n_keys
     build_s = time.time() - t0
     st = tree.stats()
     log(f"[rank {rank}] built {inserted} keys in {build_s:.1f}s "
@@ -241,6 +252,8 @@ def main():
                         "2^%d-query batches%s" % (args.keys_log2, args.batch_log2,
                                                     "" if world == 1 else
                                                     ", range shards + RCCL all-to-all"))
+            if sim:
+                workload += ", shard %d of %d (no exchange)" % (s_rank, s_world)
             data = "synthetic: key(i)=CityHash64(i)+1, value=2i; uniform queries"
         else:
             metric = "mixed get/insert Mops/s (64M uint64 keys, zipf %.2f, %d%% get)" % (

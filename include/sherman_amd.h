@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 1
+#define SHM_ABI_VERSION 2
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -62,6 +62,13 @@ typedef struct shm_config {
   uint64_t max_batch;    /* largest n accepted by a batch call */
   uint32_t num_locks;    /* HBM lock table words (reference: 16384) */
   uint32_t sort_bits;    /* top key bits that order gets: 0 or 16 */
+  /* key range hint: this shard's keys lie in [key_lo, key_lo + 2^key_bits)
+   * (a range shard of a multi-GPU tree; key_bits = 64: the whole key space).
+   * It only steers the get ordering and the leaf directory; keys outside it
+   * are still stored and found exactly. */
+  uint64_t key_lo;
+  uint32_t key_bits;     /* 1..64 (0 is read as 64) */
+  uint32_t reserved1;
 } shm_config;
 
 typedef struct shm_stats_t {

@@ -46,6 +46,9 @@ class ShmConfig(ctypes.Structure):
         ("max_batch", u64),
         ("num_locks", u32),
         ("sort_bits", u32),
+        ("key_lo", u64),
+        ("key_bits", u32),
+        ("reserved1", u32),
     ]
 
 
@@ -159,7 +162,8 @@ class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
-                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=16):
+                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=16,
+                 key_lo=0, key_bits=64):
         L = lib()
         cfg = ShmConfig()
         _check(L.shm_config_init(ctypes.byref(cfg)), "config")
@@ -169,6 +173,8 @@ class Tree:
         cfg.max_batch = max_batch
         cfg.num_locks = num_locks
         cfg.sort_bits = sort_bits
+        cfg.key_lo = key_lo
+        cfg.key_bits = key_bits
         cfg.flags = SHM_FLAG_SORT_GETS if sort_gets else 0
         h = vp()
         _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")

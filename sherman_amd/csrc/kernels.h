@@ -109,9 +109,11 @@ constexpr int kFineCap = 8192;
 constexpr int kPartHistWords = kMaxTiles * kCoarse;
 constexpr int kPartGroupWords = 16 * kCoarse;
 uint32_t partition_chunk_slots(uint64_t n);
-void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* M, uint32_t* S,
-                      uint32_t* chunks, uint64_t* keys1, uint32_t* pos1,
-                      uint64_t* keys_out, uint32_t* src, hipStream_t s);
+// get ordering by the top 16 bits of the key's offset in the shard's range
+// [key_lo, key_lo + 2^key_bits) (keys outside clamp to the first/last bucket)
+void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
+                      uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
+                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);

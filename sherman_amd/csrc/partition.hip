@@ -39,8 +39,24 @@ static_assert(kGroups * kCoarse == kPartGroupWords, "S layout");
 static_assert(kFinePer * kPT == kFineCap, "fine cap");
 static_assert(kCoarse == 256 && kFine == 256, "bin code assumes 256 bins");
 
-__device__ __forceinline__ uint32_t coarse_of(uint64_t k) { return (uint32_t)(k >> 56); }
-__device__ __forceinline__ uint32_t fine_of(uint64_t k) { return (uint32_t)(k >> 48) & 0xFF; }
+// a key's offset in the shard range [lo, lo + 2^bits), scaled to 64 bits
+// (clamped outside the range): the ordering key of both passes
+struct KeyRange {
+  uint64_t lo;
+  uint32_t bits;
+};
+__device__ __forceinline__ uint64_t rel_key(uint64_t k, KeyRange r) {
+  if (r.bits >= 64) return k;
+  if (k < r.lo) return 0;
+  const uint64_t d = k - r.lo;
+  return (d >> r.bits) ? ~0ull : d << (64 - r.bits);
+}
+__device__ __forceinline__ uint32_t coarse_of(uint64_t k, KeyRange r) {
+  return (uint32_t)(rel_key(k, r) >> 56);
+}
+__device__ __forceinline__ uint32_t fine_of(uint64_t k, KeyRange r) {
+  return (uint32_t)(rel_key(k, r) >> 48) & 0xFF;
+}
 
 // Exclusive scan of v over threads 0..255 of the block (others pass 0 and get
 // garbage).  Every thread of the block calls it; it ends with a barrier, so
@@ -64,7 +80,8 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum) {
 }  // namespace
 
 __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __restrict__ keys,
-                                                          uint64_t n, uint32_t groups,
+                                                          uint64_t n, KeyRange kr,
+                                                          uint32_t groups,
                                                           uint32_t* __restrict__ M,
                                                           uint32_t* __restrict__ S) {
   __shared__ uint32_t h[kCoarse];
@@ -77,7 +94,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __rest
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = base + (uint64_t)g * kGrpKeys + (uint64_t)r * kPT + t;
-      d[r] = i < n ? coarse_of(keys[i]) : ~0u;
+      d[r] = i < n ? coarse_of(keys[i], kr) : ~0u;
     }
 #pragma unroll
     for (int r = 0; r < kGrp; ++r)
@@ -92,7 +109,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __rest
 }
 
 __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
-    const uint64_t* __restrict__ keys, uint64_t n, uint32_t groups, uint32_t tiles,
+    const uint64_t* __restrict__ keys, uint64_t n, KeyRange kr, uint32_t groups, uint32_t tiles,
     const uint32_t* __restrict__ M, const uint32_t* __restrict__ S,
     uint64_t* __restrict__ keys1, uint32_t* __restrict__ pos1,
     uint32_t* __restrict__ chunks, uint32_t nchunk_slots) {
@@ -168,7 +185,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = gb + (uint64_t)r * kPT + t;
-      rank[r] = i < n ? atomicAdd(&cnt[coarse_of(k[r])], 1u) : 0;
+      rank[r] = i < n ? atomicAdd(&cnt[coarse_of(k[r], kr)], 1u) : 0;
     }
     __syncthreads();
     const uint32_t c = t < kCoarse ? cnt[t] : 0;
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = gb + (uint64_t)r * kPT + t;
       if (i < n) {
-        const uint32_t b = coarse_of(k[r]);
+        const uint32_t b = coarse_of(k[r], kr);
         stage[lex[b] + rank[r]] = k[r];
         pos1[i] = gbase[b] + rank[r];  // coalesced in i
       }
@@ -192,7 +209,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
       const uint32_t j = (uint32_t)(r * kPT + t);
       if (j < valid) {
         const uint64_t key = stage[j];
-        const uint32_t b = coarse_of(key);
+        const uint32_t b = coarse_of(key, kr);
         keys1[gbase[b] + (j - lex[b])] = key;
       }
     }
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
   }
 }
 
-__global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ keys1,
+__global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ keys1, KeyRange kr,
                                                    const uint32_t* __restrict__ chunks,
                                                    uint32_t* __restrict__ S,
                                                    uint64_t* __restrict__ keys_out,
@@ -232,7 +249,7 @@ __global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ 
   uint32_t rank[kFinePer];
 #pragma unroll
   for (int r = 0; r < kFinePer; ++r)
-    rank[r] = (uint32_t)(r * kPT + t) < ch.len ? atomicAdd(&h[fine_of(k[r])], 1u) : 0;
+    rank[r] = (uint32_t)(r * kPT + t) < ch.len ? atomicAdd(&h[fine_of(k[r], kr)], 1u) : 0;
   __syncthreads();
   const uint32_t ex = scan256(t < kFine ? h[t] : 0, wsum);
   if (t < kFine) h[t] = ex;
@@ -241,7 +258,7 @@ __global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ 
   for (int r = 0; r < kFinePer; ++r) {
     const uint32_t o = (uint32_t)(r * kPT + t);
     if (o < ch.len) {
-      const uint32_t lp = h[fine_of(k[r])] + rank[r];
+      const uint32_t lp = h[fine_of(k[r], kr)] + rank[r];
       stage[lp] = k[r];
       sq[lp] = (uint32_t)ch.start + o;
     }
@@ -288,20 +305,21 @@ uint32_t partition_chunk_slots(uint64_t n) {
   return (uint32_t)((n + kFineCap - 1) / kFineCap + kCoarse);
 }
 
-void launch_partition(const uint64_t* keys, uint64_t n, uint32_t* M, uint32_t* S,
-                      uint32_t* chunks, uint64_t* keys1, uint32_t* pos1,
-                      uint64_t* keys_out, uint32_t* src, hipStream_t s) {
+void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
+                      uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
+                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s) {
   if (!n) return;
+  const KeyRange kr{key_lo, key_bits};
   const uint64_t all_groups = (n + kGrpKeys - 1) / kGrpKeys;
   const uint32_t groups = (uint32_t)((all_groups + kMaxTiles - 1) / kMaxTiles);
   const uint32_t tiles = (uint32_t)((all_groups + groups - 1) / groups);
   const uint32_t slots = partition_chunk_slots(n);
-  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, groups, M,
+  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, groups, M,
                      S);
-  hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, groups,
+  hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, groups,
                      tiles, (const uint32_t*)M, (const uint32_t*)S, keys1, pos1, chunks,
                      slots);
-  hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1,
+  hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1, kr,
                      (const uint32_t*)chunks, S, keys_out, src);
 }
 

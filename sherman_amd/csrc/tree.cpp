@@ -195,6 +195,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   if (t->dir_valid && t->next_page <= t->dir_np + t->dir_np / 32) return SHM_OK;
   uint32_t bits = 10;
   while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
+  if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
   if (!t->dir || bits != t->dir_bits) {
     if (t->dir) {
       HIP_OK(hipStreamSynchronize(s));
@@ -204,8 +205,8 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
     if (dalloc(&t->dir, 8ull << bits)) return SHM_ENOMEM;
     t->dir_bits = bits;
   }
-  dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, 0, 64 - bits,
-                       1ull << bits, t->dir, t->d_err, s);
+  dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
+                       t->cfg.key_bits - bits, 1ull << bits, t->dir, t->d_err, s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
   return SHM_OK;
@@ -588,6 +589,8 @@ int shm_config_init(shm_config* c) {
   c->max_batch = 1ull << 20;
   c->num_locks = 1u << 16;
   c->sort_bits = kDefaultSortBits;
+  c->key_lo = 0;
+  c->key_bits = 64;
   return SHM_OK;
 }
 
@@ -595,11 +598,13 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (!cfg || !out || cfg->struct_size != sizeof(shm_config)) return SHM_EINVAL;
   if (cfg->arena_bytes < 4 * kPageSize || cfg->max_batch == 0 ||
       cfg->max_batch > (1ull << 31) || cfg->num_locks == 0 ||
-      (cfg->sort_bits != 0 && cfg->sort_bits != kDefaultSortBits))
+      (cfg->sort_bits != 0 && cfg->sort_bits != kDefaultSortBits) || cfg->key_bits > 64)
     return SHM_EINVAL;
   shm_tree* t = new shm_tree();
   t->cfg = *cfg;
   if (!t->cfg.sort_bits || t->cfg.sort_bits > 64) t->cfg.sort_bits = kDefaultSortBits;
+  if (t->cfg.key_bits == 0) t->cfg.key_bits = 64;
+  if (t->cfg.key_bits == 64) t->cfg.key_lo = 0;
   auto fail = [&](int rc) {
     free_all(t);
     delete t;
@@ -714,7 +719,8 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       // walked by the same wave (one page read per group, not per query)
       // (keys1 = kb, pos1 = ia, walk order = ka, src = ib); the walk stores
       // result p at vals1[src[p]] (kb, inside p's chunk), unpartition gathers
-      dev::launch_partition(keys + off, m, t->part_hist, t->part_S, t->part_chunks,
+      dev::launch_partition(keys + off, m, t->cfg.key_lo, t->cfg.key_bits, t->part_hist,
+                            t->part_S, t->part_chunks,
                             t->kb, t->ia,
                             t->ka, t->ib, s);
       a.keys = t->ka;
@@ -724,8 +730,8 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.xcd_remap = getenv("SHM_XCD_REMAP") ? atoi(getenv("SHM_XCD_REMAP")) : 1;
       if (use_leaf_dir()) {
         a.dir = t->dir;
-        a.dir_lo = 0;
-        a.dir_shift = 64 - t->dir_bits;
+        a.dir_lo = t->cfg.key_lo;
+        a.dir_shift = t->cfg.key_bits - t->dir_bits;
         a.dir_n = 1ull << t->dir_bits;
       } else {
         a.start = t->start;

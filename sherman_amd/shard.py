@@ -31,6 +31,14 @@ def owner_of(keys, world):
     return (hi * world + ((lo * world) >> 32)) >> 32
 
 
+def shard_range(rank, world):
+    """(key_lo, key_bits) hint for shard `rank` of `world`: its keys lie in
+    [ceil(rank * 2^64 / P), ...) within 2^key_bits of key_lo (shm_config)."""
+    lo = (rank * (1 << 64) + world - 1) // world
+    bits = 64 - (world.bit_length() - 1)  # 2^bits >= 2^64 / P
+    return lo, bits
+
+
 class ShardRouter:
     def __init__(self, local, world, dist, group=None):
         self.local, self.world, self.dist, self.group = local, world, dist, group

@@ -40,13 +40,14 @@ def test_exported_symbols_are_c_abi():
 
 
 def test_config_layout_and_defaults():
-    assert ctypes.sizeof(shm.ShmConfig) == 40
+    assert ctypes.sizeof(shm.ShmConfig) == 56
     cfg = shm.ShmConfig()
     assert shm.lib().shm_config_init(ctypes.byref(cfg)) == 0
-    assert cfg.struct_size == 40
+    assert cfg.struct_size == 56
+    assert cfg.key_lo == 0 and cfg.key_bits == 64
     assert cfg.flags & shm.SHM_FLAG_SORT_GETS
     assert cfg.max_batch == 1 << 20 and cfg.num_locks == 1 << 16
-    assert shm.lib().shm_abi_version() == 1
+    assert shm.lib().shm_abi_version() == 2
     assert shm.lib().shm_strerror(shm.SHM_EINVAL).startswith(b"invalid")
 
 
@@ -59,6 +60,9 @@ def test_create_rejects_bad_config_without_touching_gpu():
     assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
     L.shm_config_init(ctypes.byref(cfg))
     cfg.max_batch = 0
+    assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
+    L.shm_config_init(ctypes.byref(cfg))
+    cfg.key_bits = 65
     assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
     assert L.shm_tree_destroy(None) == shm.SHM_EINVAL
 

@@ -424,3 +424,29 @@ def test_leaf_dir_stale_after_splits(lib_ok):
     assert t.stats()["pages_used"] > pages0
     compare_contents(t, orc)
     t.close()
+
+
+def test_shard_key_range_hint(lib_ok):
+    """A range shard (shm_config key_lo / key_bits, here shard 5 of 8) orders
+    gets and builds its leaf directory over its own slice; keys outside the
+    slice are still stored and found exactly."""
+    from sherman_amd.shard import owner_of, shard_range
+    lo, bits = shard_range(5, 8)
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18, key_lo=lo, key_bits=bits)
+    orc = OracleTree(512 << 20)
+    allk = hashed_keys(1, 1 << 20)
+    own = owner_of(torch.from_numpy(allk.view(np.int64)), 8).numpy()
+    mine = allk[own == 5]                                   # ~131 K keys in the slice
+    stray = allk[own != 5][:3000]                           # outside the hint
+    keys = np.concatenate([mine, stray])
+    vals = np.arange(1, keys.size + 1, dtype=U64) * U64(3)
+    for c in range(0, keys.size, 1 << 17):
+        gpu_insert(t, keys[c:c + (1 << 17)], vals[c:c + (1 << 17)])
+        orc.apply_batch(keys[c:c + (1 << 17)], vals[c:c + (1 << 17)])
+    rng = np.random.default_rng(23)
+    probe = np.concatenate([mine[rng.integers(0, mine.size, 1 << 17)], stray,
+                            allk[own != 5][3000:6000]])      # strays and misses
+    rng.shuffle(probe)
+    assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))
+    compare_contents(t, orc)
+    t.close()
