@@ -139,7 +139,8 @@ def main():
     sim = world == 1 and args.sim_world > 1
     s_rank, s_world = (args.sim_rank, args.sim_world) if sim else (rank, world)
     key_lo, key_bits = (0, 64) if args.no_range_hint else shard_range(s_rank, s_world)
-    tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch), device=local,
+    # N > 1: a rank receives ~batch routed keys (+ a few %), keep one chunk
+    tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch + (batch >> 2 if world > 1 else 0)), device=local,
                     node_id=rank, sort_gets=not args.no_sort, key_lo=key_lo, key_bits=key_bits)
 
     t0 = time.time()
