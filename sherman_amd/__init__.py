@@ -162,7 +162,7 @@ class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
-                 node_id=0, sort_gets=True, num_locks=1 << 16, sort_bits=16,
+                 node_id=0, sort_gets=True, num_locks=None, sort_bits=16,
                  key_lo=0, key_bits=64):
         L = lib()
         cfg = ShmConfig()
@@ -171,7 +171,8 @@ class Tree:
         cfg.node_id = node_id
         cfg.arena_bytes = arena_bytes
         cfg.max_batch = max_batch
-        cfg.num_locks = num_locks
+        if num_locks is not None:
+            cfg.num_locks = num_locks
         cfg.sort_bits = sort_bits
         cfg.key_lo = key_lo
         cfg.key_bits = key_bits

@@ -26,6 +26,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "lds_dma.h"
+#include "leaf_chunk.h"
 
 namespace shm {
 namespace dev {
@@ -38,34 +39,11 @@ __device__ __forceinline__ uint64_t lds_u64(const uint32_t* lp, int d) {
   return (uint64_t)lp[d] | ((uint64_t)lp[d + 1] << 32);
 }
 
-// dword-pair funnel: the 4 bytes starting at byte offset o (compile time) of
-// a dword array
-template <int O, int N>
-__device__ __forceinline__ uint32_t bytes4(const uint32_t (&D)[N]) {
-  static_assert((O >> 2) + 1 < N || (O & 3) == 0, "chunk bound");
-  if constexpr ((O & 3) == 0) {
-    return D[O >> 2];
-  } else {
-    return __builtin_amdgcn_alignbyte(D[(O >> 2) + 1], D[O >> 2], O & 3);
-  }
-}
-template <int O, int N>
-__device__ __forceinline__ uint32_t byte1(const uint32_t (&D)[N]) {
-  return (D[O >> 2] >> (8 * (O & 3))) & 0xFF;
-}
-
-template <int J, int N>
-__device__ __forceinline__ void entry_at(const uint32_t (&D)[N], uint64_t& key, uint64_t& val,
-                                         bool& vok) {
-  constexpr int O = kLeafEntry * J;  // f @0, key @1, value @9, r @17
-  key = (uint64_t)bytes4<O + 1>(D) | ((uint64_t)bytes4<O + 5>(D) << 32);
-  val = (uint64_t)bytes4<O + 9>(D) | ((uint64_t)bytes4<O + 13>(D) << 32);
-  vok = ((byte1<O>(D) ^ byte1<O + 17>(D)) & 0xF) == 0;
-}
-
 }  // namespace
 
-template <int G, int NB, int WPB>
+// LOC = the leaf-locate walk of the insert path (Tree::insert's descent to
+// level 0, Tree.cpp:353-403): out_page[i] = the leaf whose fences hold key i.
+template <int G, int NB, int WPB, bool LOC = false>
 __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   constexpr int L = kWave / G;                               // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;          // entries per lane
@@ -134,9 +112,8 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   // chunks stay inside the page: the last lane's chunk is shifted down to end
   // at entry 53 and masks the entries its left neighbour owns; lanes past
   // 54 / E mask everything
-  const int ebase = E * li < kLeafCardinality - E ? E * li : kLeafCardinality - E;
+  const int ebase = chunk_base<E>(li);
   const int chunk_dw = (kOffRecords + kLeafEntry * ebase) / 4;
-  static_assert((kLeafCardinality - E) % 2 == 0, "chunk starts must be dword aligned");
   const uint64_t lanemask_le = ~0ull >> (63 - lane);
 
   for (;;) {
@@ -211,15 +188,16 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
       const uint32_t C2 = lp[10];
       const u32x2 Z = *reinterpret_cast<const u32x2*>(lp + 254);
       uint32_t D[CD];
-      {
+      int hsrc = hq[0];
+      uint64_t kq = 0;
+      if constexpr (!LOC) {
         const uint32_t* ep = buf + q * kPageDwords + chunk_dw;
 #pragma unroll
         for (int i = 0; i < CD; ++i) D[i] = ep[i];
-      }
-      int hsrc = hq[0];
 #pragma unroll
-      for (int s = 1; s < G; ++s) hsrc = q == s ? hq[s] : hsrc;
-      uint64_t kq = shfl64(k, hsrc < 63 ? hsrc : 63);
+        for (int s = 1; s < G; ++s) hsrc = q == s ? hq[s] : hsrc;
+        kq = shfl64(k, hsrc < 63 ? hsrc : 63);
+      }
 
       const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
                                 ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
@@ -269,19 +247,17 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 
       // ---- leaf pages: lane groups hold the entries -----------------------
       uint64_t lq = ballot(qleaf);
-      if (lq) {
+      if constexpr (LOC) {
+        val = qleaf ? ptr : val;  // the leaf holding the key
+      } else if (lq) {
         uint64_t ekey[E], evalue[E];
+        uint32_t efr[E], erv[E];
+        chunk_entries<E>(D, ekey, evalue, efr, erv);
         bool eok[E];
-        entry_at<0>(D, ekey[0], evalue[0], eok[0]);
-        entry_at<1>(D, ekey[1], evalue[1], eok[1]);
-        if constexpr (E > 2) {
-          entry_at<2>(D, ekey[2], evalue[2], eok[2]);
-          entry_at<3>(D, ekey[3], evalue[3], eok[3]);
-        }
-        static_assert(E == 2 || E == 4, "entry unpack covers E = 2 and 4");
 #pragma unroll
         for (int j = 0; j < E; ++j)
-          eok[j] = eok[j] && evalue[j] != kValueNull && ebase + j >= li * E;
+          eok[j] = evalue[j] != kValueNull && ((efr[j] ^ erv[j]) & 0xF) == 0 &&
+                   ebase + j >= li * E;
         const int tl = lane - myhead;  // my position in my run
         const int sl = slot & (G - 1);
         for (int t = 0;; ++t) {
@@ -324,8 +300,12 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   if (active) {
     const uint64_t i = wave_base + tag;
     const uint64_t o = a.perm ? (uint64_t)a.perm[i] : i;
-    a.out_val[o] = val;
-    if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
+    if constexpr (LOC) {
+      a.out_page[o] = val;
+    } else {
+      a.out_val[o] = val;
+      if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
+    }
   }
 }
 
@@ -345,6 +325,13 @@ template <int G, int NB, int WPB>
 static void launch_cfg(const WalkArgs& a, uint64_t waves, hipStream_t s) {
   const dim3 grid((unsigned)((waves + WPB - 1) / WPB));
   hipLaunchKernelGGL((k_get<G, NB, WPB>), grid, dim3(WPB * kWave), 0, s, a);
+}
+
+void launch_locate_leaf(const WalkArgs& a, uint64_t n, hipStream_t s) {
+  if (n == 0) return;
+  const uint64_t waves = (n + kWave - 1) / kWave;
+  hipLaunchKernelGGL((k_get<4, 1, 4, true>), dim3((unsigned)((waves + 3) / 4)), dim3(4 * kWave),
+                     0, s, a);
 }
 
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s) {

@@ -319,6 +319,8 @@ __global__ __launch_bounds__(kBlock) void k_leaf_update(SegArgs a) {
   WaveLds& L = s_l[threadIdx.x >> 6];
   const uint64_t page = a.seg_page[g];
   if (!ptr_ok(page, a.node, a.arena_bytes)) return;
+  // after k_leaf_upsert only the segments it flagged for a split remain
+  if (a.split_only && a.seg_P[g] == 1) return;
   const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
   if (!lock_page(a, page, a.tag_base + g + 1)) {
     if (lane == 0) atomicOr(a.err, kErrLock);

@@ -40,6 +40,8 @@ void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
                  hipStream_t s);
 // batched get walk with grouped page resolution (get.hip)
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
+// the same walk as a leaf locate (insert path): out_page[i] = leaf of keys[i]
+void launch_locate_leaf(const WalkArgs& a, uint64_t n, hipStream_t s);
 // start[p] = the deepest page whose fences cover every key with prefix p
 // (key >> (64 - bits) == p), found by walking from root.  A page's lowest
 // fence never changes (a split keeps the left half in place), so a start page
@@ -81,12 +83,15 @@ struct SegArgs {
   uint64_t tag_base;
   int level;
   int is_delete;
+  int split_only;             // k_leaf_update: skip segments with P == 1
   uint32_t* err;
 };
 
 void launch_leaf_plan(const SegArgs& a, hipStream_t s);
 void launch_leaf_build(const SegArgs& a, uint32_t total_new, hipStream_t s);
 void launch_leaf_update(const SegArgs& a, hipStream_t s);
+// in-place upserts, 4 segments per wave (upsert.hip); flags P > 1 segments
+void launch_leaf_upsert(const SegArgs& a, hipStream_t s);
 void launch_leaf_delete(const SegArgs& a, hipStream_t s);
 void launch_int_plan(const SegArgs& a, hipStream_t s);
 void launch_int_build(const SegArgs& a, uint32_t total_new, hipStream_t s);

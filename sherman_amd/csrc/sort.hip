@@ -13,20 +13,23 @@ namespace dev {
 
 size_t scan_temp_bytes(uint64_t n);
 
+// Onesweep for every size above one block: rocPRIM's default switches to a
+// block-sort + merge-sort cascade below 2^20 items, which took ~175 us (24
+// launches) on a 0.5 Mi-pair insert batch.
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                           rocprim::default_config, 0>;
+
 static size_t sort_bytes_at(uint64_t n, unsigned begin_bit) {
   size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint64_t*)nullptr,
+  (void)rocprim::radix_sort_pairs<SortCfg>(nullptr, bytes, (const uint64_t*)nullptr,
                                   (uint64_t*)nullptr, (const uint32_t*)nullptr,
                                   (uint32_t*)nullptr, (size_t)n, begin_bit, 64u);
   return bytes;
 }
 
-// rocPRIM picks block sort / merge sort / onesweep by size, each with its own
-// temporary-storage need, so the workspace is the max over every size up to
-// n (not just the need at n).
 static size_t sort32_bytes_at(uint64_t n) {
   size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr,
+  (void)rocprim::radix_sort_pairs<SortCfg>(nullptr, bytes, (const uint32_t*)nullptr,
                                   (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                   (uint32_t*)nullptr, (size_t)n, 0u, 32u);
   return bytes;
@@ -48,16 +51,16 @@ hipError_t sort_pairs(void* temp, size_t bytes, const uint64_t* kin,
                       uint64_t* kout, const uint32_t* vin, uint32_t* vout,
                       uint64_t n, hipStream_t s) {
   if (sort_bytes_at(n, 0) > bytes) return hipErrorInvalidValue;
-  return rocprim::radix_sort_pairs(temp, bytes, kin, kout, vin, vout, (size_t)n,
-                                   0u, 64u, s);
+  return rocprim::radix_sort_pairs<SortCfg>(temp, bytes, kin, kout, vin, vout, (size_t)n,
+                                            0u, 64u, s);
 }
 
 hipError_t sort_pairs_u32(void* temp, size_t bytes, const uint32_t* kin,
                           uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                           uint64_t n, hipStream_t s) {
   if (sort32_bytes_at(n) > bytes) return hipErrorInvalidValue;
-  return rocprim::radix_sort_pairs(temp, bytes, kin, kout, vin, vout, (size_t)n,
-                                   0u, 32u, s);
+  return rocprim::radix_sort_pairs<SortCfg>(temp, bytes, kin, kout, vin, vout, (size_t)n,
+                                            0u, 32u, s);
 }
 
 size_t scan_temp_bytes_max(uint64_t n) {

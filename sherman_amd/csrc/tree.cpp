@@ -179,6 +179,16 @@ dev::WalkArgs walk_args(shm_tree* t) {
   return a;
 }
 
+// SHM_FAST_INSERT=0 selects the page-at-a-time locate walk and the
+// plan / update leaf kernels instead of the grouped locate + k_leaf_upsert
+bool use_fast_insert() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_FAST_INSERT");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // SHM_LEAF_DIR=0 starts gets from the prefix start table instead of the
 // leaf directory (A/B switch)
 bool use_leaf_dir() {
@@ -300,7 +310,20 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   w.n = n_ops;
   w.out_page = t->pages;
   w.target_level = level;
-  dev::launch_walk(w, n_ops, 4, true, s);
+  if (level == 0 && use_fast_insert()) {
+    // the grouped get walk as a leaf locate, started from the leaf directory
+    if (use_leaf_dir()) {
+      const int rc = refresh_dir(t, s);
+      if (rc) return rc;
+      w.dir = t->dir;
+      w.dir_lo = t->cfg.key_lo;
+      w.dir_shift = t->cfg.key_bits - t->dir_bits;
+      w.dir_n = 1ull << t->dir_bits;
+    }
+    dev::launch_locate_leaf(w, n_ops, s);
+  } else {
+    dev::launch_walk(w, n_ops, 4, true, s);
+  }
   DBG(s, "walk(locate)");
   dev::launch_seg_heads(t->pages, n_ops, t->heads, s);
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
@@ -314,6 +337,8 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
 }
 
 // plan + scan + capacity check; returns new page count (or negative status)
+int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t reserve);
+
 int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
                    uint64_t reserve) {
   if (leaf)
@@ -321,6 +346,11 @@ int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
   else
     dev::launch_int_plan(a, s);
   DBG(s, "plan");
+  return new_page_total(t, s, a, reserve);
+}
+
+// scan seg_newpages into seg_pbase and read back the level's new-page total
+int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t reserve) {
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
                                  a.num_seg, s));
   // total = pbase[last] + np[last]
@@ -363,7 +393,17 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   const bool leaf = level == 0;
   // head-room for the parent levels a split of this level can trigger
   const uint64_t reserve = 2 * (uint64_t)kMaxLevelOfTree;
-  const int64_t total = plan_level(t, s, a, leaf, reserve);
+  int64_t total;
+  if (leaf && use_fast_insert()) {
+    // in-place segments are applied here; the rest go the k-way split path
+    dev::launch_leaf_upsert(a, s);
+    DBG(s, "leaf_upsert");
+    total = new_page_total(t, s, a, reserve);
+    if (total <= 0) return total;
+    a.split_only = 1;
+  } else {
+    total = plan_level(t, s, a, leaf, reserve);
+  }
   if (total < 0) return total;
   a.first_new_page = t->next_page;
   if (leaf) {
@@ -587,7 +627,7 @@ int shm_config_init(shm_config* c) {
   c->flags = SHM_FLAG_SORT_GETS;
   c->arena_bytes = 1ull << 30;
   c->max_batch = 1ull << 20;
-  c->num_locks = 1u << 16;
+  c->num_locks = 1u << 22;  // 32 MB: rare false sharing between waves
   c->sort_bits = kDefaultSortBits;
   c->key_lo = 0;
   c->key_bits = 64;

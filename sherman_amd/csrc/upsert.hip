@@ -1,0 +1,261 @@
+// upsert.hip — in-place leaf upserts of a segmented insert batch, four
+// segments per wave: the no-split branch of Tree::insert's leaf_page_store
+// (src/Tree.cpp:828-920).
+//
+// The batch's sorted unique keys are grouped into segments, one per target
+// leaf (tree.cpp: segment()).  A wave takes G = 4 consecutive segments:
+//   * lock: lanes 0..G-1 atomicCAS(0 -> tag) their segment's lock word
+//     lock[CityHash64(page) % num_locks] (the reference's on-chip lock word,
+//     Tree.cpp:832-842, 205-242), all at once.  If any word is held by
+//     another wave, the wave drops what it took and takes the words one at a
+//     time in increasing order, so no two waves ever wait on each other in a
+//     cycle.  Every spin is bounded (kErrLock).
+//   * stage: the G pages by LDS-DMA, read under the locks
+//     (lock_and_read_page, Tree.cpp:851-852), checked with check_consistent
+//     (front == rear, Tree.cpp:857) and the fences of every key.
+//   * apply: lane group q (16 lanes x 4 consecutive entries) holds slot q's
+//     54 entries.  For each op of segment q in key order the valid slot
+//     holding the key is overwritten, else the first empty slot is taken;
+//     f_version++ and r_version = f_version, 4-bit (Tree.cpp:878-912).
+//   * write back only the changed 18 B entries (the reference writes the
+//     entry, not the page: write_page_and_unlock(update_addr, ...),
+//     Tree.cpp:915-920), then release the locks.
+// A segment whose page would reach 54 entries (the split point,
+// Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
+// k-way split path of insert.hip; seg_T / seg_ver feed that path exactly as
+// the plan kernel's outputs did.
+#include "device_common.h"
+#include "kernels.h"
+#include "lds_dma.h"
+#include "leaf_chunk.h"
+
+namespace shm {
+namespace dev {
+
+namespace {
+
+__device__ __forceinline__ uint32_t lock_word(uint64_t page, uint32_t n) {
+  return (uint32_t)(cityhash64_u64(page) % n);
+}
+
+// release the distinct lock words of the lanes in m (lane 0 stores); the
+// wave's page stores are performed first (write, then unlock, Tree.cpp:266-298)
+__device__ __forceinline__ void release_words(unsigned long long* lk, uint32_t lw, uint64_t m) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (uint64_t r = m; r; r &= r - 1) {
+    const int s = ctz64(r);
+    const uint32_t w = rl32(lw, s);
+    bool dup = false;
+    for (uint64_t e = m & ((1ull << s) - 1); e; e &= e - 1) dup = dup || rl32(lw, ctz64(e)) == w;
+    if (!dup && lane_id() == 0)
+      __hip_atomic_store(lk + w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+}  // namespace
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
+  constexpr int L = kWave / G;                       // lanes per page
+  constexpr int E = (kLeafCardinality + L - 1) / L;  // entries per lane
+  constexpr int CD = kLeafEntry * E / 4;             // dwords per lane chunk
+  constexpr uint64_t kGroupMask = L == 64 ? ~0ull : ((1ull << (L & 63)) - 1);
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * G * kPageDwords];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
+  const uint64_t g0 = wid * G;
+  if (g0 >= a.num_seg) return;  // wave-uniform
+  const uint32_t* buf = &s_pg[wv * G * kPageDwords];
+  const uint32_t buf_lds = lds_addr_of(buf);
+  uint32_t err = 0;
+
+  // ---- slot s (lane s < G) = segment g0 + s --------------------------------
+  const bool sl = lane < G && g0 + (uint64_t)lane < a.num_seg;
+  const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
+  const uint64_t page = sl ? a.seg_page[gs] : 0;
+  const bool pok = sl && ptr_ok(page, a.node, a.arena_bytes);
+  if (ballot(sl && !pok)) err |= kErrBadPtr;
+  const uint32_t st = sl ? a.seg_start[gs] : 0u;
+  const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
+
+  // ---- lock -------------------------------------------------------------------
+  unsigned long long* lk = reinterpret_cast<unsigned long long*>(a.locks);
+  const uint32_t lw = pok ? lock_word(page, a.num_locks) : 0u;
+  const unsigned long long tag = (unsigned long long)(a.tag_base + wid + 1);
+  const uint64_t wantm = ballot(pok);
+  bool own = false, have = !pok;
+  if (pok) {
+    // lanes sharing a word: the first takes it, the others see our tag
+    const unsigned long long o = atomicCAS(lk + lw, 0ull, tag);
+    own = o == 0ull;
+    have = own || o == tag;
+  }
+  bool locked = true;
+  if (ballot(!have)) {
+    release_words(lk, lw, ballot(own));
+    // one at a time, increasing word order
+    bool first = true;
+    uint32_t prev = 0;
+    for (int it = 0; it < G && locked; ++it) {
+      uint32_t best = ~0u;
+      bool found = false;
+      for (uint64_t r = wantm; r; r &= r - 1) {
+        const uint32_t w = rl32(lw, ctz64(r));
+        if ((first || w > prev) && (!found || w < best)) {
+          best = w;
+          found = true;
+        }
+      }
+      if (!found) break;
+      uint32_t ok = 0;
+      if (lane == 0) {
+        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+          if (atomicCAS(lk + best, 0ull, tag) == 0ull) {
+            ok = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (rl32(ok, 0) == 0) {
+        // give up: release the words below `best` and fail the group
+        uint64_t held = 0;
+        for (uint64_t r = wantm; r; r &= r - 1) {
+          const int s = ctz64(r);
+          if (!first && rl32(lw, s) <= prev) held |= 1ull << s;
+        }
+        release_words(lk, lw, held);
+        err |= kErrLock;
+        locked = false;
+      }
+      prev = best;
+      first = false;
+    }
+  }
+
+  // ---- stage the pages under the locks ---------------------------------------
+#pragma unroll
+  for (int s = 0; s < G; ++s)
+    glds16(a.arena + ga_offset(rl64(pok && locked ? page : 0, s)),
+           buf_lds + (uint32_t)(s * kPageSize));
+  wait_vm<0>();
+
+  // ---- per slot q: header, entries ---------------------------------------------
+  const int q = lane / L;
+  const int li = lane % L;
+  const uint32_t* hp = buf + q * kPageDwords;
+  const uint32_t h2 = hp[2], h3 = hp[3], h4 = hp[4], h7 = hp[7], h8 = hp[8], h9 = hp[9],
+                 h10 = hp[10], z = hp[kOffLeafRear / 4];
+  const uint64_t leftmost = (uint64_t)((h2 >> 8) | (h3 << 24)) |
+                            ((uint64_t)((h3 >> 8) | (h4 << 24)) << 32);
+  const uint32_t fver = h2 & 0xFF;
+  const uint64_t lowest = (uint64_t)h7 | ((uint64_t)h8 << 32);
+  const uint64_t highest = (uint64_t)h9 | ((uint64_t)h10 << 32);
+  const bool qpok = (shfl32(pok ? 1u : 0u, q) != 0) && locked;
+  const bool cons = leftmost == 0 && fver == (z & 0xFF);
+  if (ballot(qpok && !cons)) err |= kErrInconsistent;
+  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
+  const uint64_t qpage = shfl64(page, q);
+  bool live = qpok && cons;
+  const uint32_t nops = live ? qen - qst : 0u;
+
+  const int ebase = chunk_base<E>(li);
+  uint32_t D[CD];
+  {
+    const uint32_t* ep = hp + (kOffRecords + kLeafEntry * ebase) / 4;
+#pragma unroll
+    for (int i = 0; i < CD; ++i) D[i] = ep[i];
+  }
+  uint64_t ek[E], ev[E];
+  uint32_t ef[E], er[E];
+  chunk_entries<E>(D, ek, ev, ef, er);
+  bool mine[E], valid[E], dirty[E];
+  uint32_t cnt = 0;  // valid entries of slot q (the same in all its lanes)
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    mine[j] = ebase + j >= li * E;
+    valid[j] = mine[j] && ev[j] != kValueNull;
+    dirty[j] = false;
+    cnt += (uint32_t)popc64((ballot(valid[j]) >> (q * L)) & kGroupMask);
+  }
+
+  // ---- apply the ops in key order -------------------------------------------------
+  uint32_t T = cnt;
+  bool over = false, bad = false;
+  for (uint32_t t = 0; ballot(t < nops); ++t) {
+    const bool act = t < nops && !bad;
+    const uint64_t kq = act ? a.op_key[qst + t] : 0;
+    const uint64_t vq = act ? a.op_val[qst + t] : 0;
+    if (act && (kq < lowest || kq >= highest)) bad = true;  // not this page's key
+    const bool go = act && !bad;
+    int hj = -1;
+#pragma unroll
+    for (int j = E - 1; j >= 0; --j)
+      if (valid[j] && ek[j] == kq) hj = j;
+    const uint64_t mh = (ballot(go && hj >= 0) >> (q * L)) & kGroupMask;
+    bool take = false;
+    int tj = -1;
+    if (go && mh) {
+      take = li == ctz64(mh);  // the valid slot holding the key
+      tj = hj;
+    } else if (go) {
+      T += 1;  // a new key
+      if (T > (uint32_t)(kLeafCardinality - 1)) over = true;
+      int fj = -1;
+#pragma unroll
+      for (int j = E - 1; j >= 0; --j)
+        if (mine[j] && !valid[j]) fj = j;
+      const uint64_t me = (ballot(!over && fj >= 0) >> (q * L)) & kGroupMask;
+      if (!over && me) {
+        take = li == ctz64(me);  // the first empty slot
+        tj = fj;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (take && tj == j) {
+        ek[j] = kq;
+        ev[j] = vq;
+        const uint32_t f = ((ef[j] & 0xF) + 1) & 0xF;
+        ef[j] = (ef[j] & 0xF0) | f;
+        er[j] = (er[j] & 0xF0) | f;
+        valid[j] = true;
+        dirty[j] = true;
+      }
+    }
+  }
+  if (ballot(bad)) err |= kErrPlan;
+  live = live && !bad;
+
+  // ---- write back the changed entries of in-place segments -----------------------
+  if (live && !over) {
+    uint8_t* pg = a.arena + ga_offset(qpage);
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (dirty[j])
+        put_leaf_entry(reinterpret_cast<uint32_t*>(pg), ebase + j, ek[j], ev[j], ef[j], er[j]);
+  }
+  const uint64_t gq = g0 + (uint64_t)q;
+  if (li == 0 && q < G && gq < a.num_seg) {
+    const uint32_t P = (live && over) ? (T + kLeafSplitFill - 1) / kLeafSplitFill : 1u;
+    a.seg_T[gq] = live ? T : 0u;
+    a.seg_P[gq] = P;
+    a.seg_newpages[gq] = P - 1;
+    a.seg_ver[gq] = live ? fver : ~0u;
+  }
+  if (locked) release_words(lk, lw, wantm);
+  if (err) atomicOr(a.err, err);
+}
+
+void launch_leaf_upsert(const SegArgs& a, hipStream_t s) {
+  constexpr int G = 4;
+  if (!a.num_seg) return;
+  const uint64_t waves = (a.num_seg + G - 1) / G;
+  hipLaunchKernelGGL(k_leaf_upsert<G>, dim3((unsigned)((waves + kWavesPerBlock - 1) /
+                                                       kWavesPerBlock)),
+                     dim3(kBlock), 0, s, a);
+}
+
+}  // namespace dev
+}  // namespace shm

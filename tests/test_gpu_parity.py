@@ -450,3 +450,28 @@ def test_shard_key_range_hint(lib_ok):
     assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))
     compare_contents(t, orc)
     t.close()
+
+
+def test_insert_with_colliding_lock_words(lib_ok):
+    """Three lock words for the whole arena: every wave of the in-place
+    upsert (four leaves per wave) collides on its lock words with itself and
+    with other waves, so the ordered one-at-a-time acquisition path runs.
+    Contents must still equal the oracle's after updates, new keys and
+    splits."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16, num_locks=3)
+    orc = OracleTree(256 << 20)
+    base = hashed_keys(1, 60001)
+    bv = np.arange(1, base.size + 1, dtype=U64)
+    gpu_insert(t, base, bv)
+    orc.apply_batch(base, bv)
+    rng = np.random.default_rng(29)
+    for r in range(3):
+        upd = base[rng.integers(0, base.size, 30000)]             # updates + duplicates
+        new = hashed_keys(100000 + 20000 * r, 100000 + 20000 * r + 8000)
+        keys = np.concatenate([upd, new])
+        rng.shuffle(keys)
+        vals = np.arange(1, keys.size + 1, dtype=U64) + U64(10 ** 7 * (r + 1))
+        gpu_insert(t, keys, vals)
+        orc.apply_batch(keys, vals)
+    compare_contents(t, orc)
+    t.close()
