@@ -119,6 +119,24 @@ uint32_t partition_chunk_slots(uint64_t n);
 void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
                       uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
                       uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s);
+// insert ordering, step 2: the coarse pass alone over per-group
+// de-duplicated runs (group gi = keys [gi * 4096, ...) holds gcount[gi]
+// keys), carrying a u32 payload; bins = 2 x 256 words of (start, count)
+void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* gcount,
+                             const uint32_t* pay_in, uint64_t key_lo, uint32_t key_bits,
+                             uint32_t* M, uint32_t* S, uint64_t* keys1, uint32_t* pay1,
+                             uint32_t* bins, hipStream_t s);
+// insert ordering (isort.hip).  Step 1: every 4096-op tile reduced to its
+// last writer per key (LDS hash table, atomic max of the op index).  Step 3:
+// every coarse bin (<= 8192 keys) fully sorted by (key, op index) in place;
+// a larger bin sets kErrSortOverflow (the host then re-sorts with rocPRIM).
+constexpr int kIsortTile = 4096;
+constexpr uint32_t kErrSortOverflow = 1u << 30;
+constexpr uint32_t kErrKeyMax = 1u << 31;
+void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
+                       uint32_t* gcount, uint32_t* err, hipStream_t s);
+void launch_bin_sort(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint32_t* S,
+                     uint32_t* err, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);
@@ -127,8 +145,8 @@ void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
                   uint32_t* idx, hipStream_t s);
 // flags[i] = (last of equal-key run) * (v != 0 ? 1 : 1 << 32), key checks
 void launch_mark_unique(const uint64_t* sk, const uint32_t* sidx,
-                        const uint64_t* vals, uint64_t n, uint64_t* flags,
-                        uint32_t* err, hipStream_t s);
+                        const uint64_t* vals, uint64_t n, const uint32_t* bins,
+                        uint64_t* flags, uint32_t* err, hipStream_t s);
 void launch_compact_unique(const uint64_t* sk, const uint32_t* sidx,
                            const uint64_t* vals, const uint64_t* flags,
                            const uint64_t* pos, uint64_t n, uint64_t* uk,

@@ -37,6 +37,7 @@ constexpr int kTileGroup = 16;            // tiles per S row
 constexpr int kGroups = kMaxTiles / kTileGroup;
 static_assert(kGroups * kCoarse == kPartGroupWords, "S layout");
 static_assert(kFinePer * kPT == kFineCap, "fine cap");
+static_assert(kGrpKeys == kIsortTile, "insert tiles are the coarse pass's groups");
 static_assert(kCoarse == 256 && kFine == 256, "bin code assumes 256 bins");
 
 // a key's offset in the shard range [lo, lo + 2^bits), scaled to 64 bits
@@ -79,8 +80,15 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum) {
 
 }  // namespace
 
+// gcount (nullable): group gi (kGrpKeys keys from gi * kGrpKeys) holds only
+// its first gcount[gi] keys (the insert path's per-tile de-duplicated runs)
+__device__ __forceinline__ bool part_valid(uint64_t i, uint64_t n, const uint32_t* gcount) {
+  return i < n && (!gcount || (uint32_t)(i % kGrpKeys) < gcount[i / kGrpKeys]);
+}
+
 __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __restrict__ keys,
                                                           uint64_t n, KeyRange kr,
+                                                          const uint32_t* __restrict__ gcount,
                                                           uint32_t groups,
                                                           uint32_t* __restrict__ M,
                                                           uint32_t* __restrict__ S) {
@@ -94,7 +102,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __rest
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = base + (uint64_t)g * kGrpKeys + (uint64_t)r * kPT + t;
-      d[r] = i < n ? coarse_of(keys[i], kr) : ~0u;
+      d[r] = part_valid(i, n, gcount) ? coarse_of(keys[i], kr) : ~0u;
     }
 #pragma unroll
     for (int r = 0; r < kGrp; ++r)
@@ -109,11 +117,14 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_hist(const uint64_t* __rest
 }
 
 __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
-    const uint64_t* __restrict__ keys, uint64_t n, KeyRange kr, uint32_t groups, uint32_t tiles,
+    const uint64_t* __restrict__ keys, uint64_t n, KeyRange kr,
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ pay_in,
+    uint32_t groups, uint32_t tiles,
     const uint32_t* __restrict__ M, const uint32_t* __restrict__ S,
-    uint64_t* __restrict__ keys1, uint32_t* __restrict__ pos1,
-    uint32_t* __restrict__ chunks, uint32_t nchunk_slots) {
+    uint64_t* __restrict__ keys1, uint32_t* __restrict__ pay1, uint32_t* __restrict__ pos1,
+    uint32_t* __restrict__ chunks, uint32_t nchunk_slots, uint32_t* __restrict__ bins) {
   __shared__ uint64_t stage[kGrpKeys];
+  __shared__ uint32_t pstage[kGrpKeys];
   __shared__ uint32_t cnt[kCoarse], lex[kCoarse], gbase[kCoarse];
   __shared__ uint32_t part[6][kCoarse];
   __shared__ uint32_t wsum[4];
@@ -125,7 +136,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
 #pragma unroll
   for (int r = 0; r < kGrp; ++r) {
     const uint64_t i = tbase + (uint64_t)r * kPT + t;
-    k[r] = i < n ? keys[i] : 0;
+    k[r] = part_valid(i, n, gcount) ? keys[i] : 0;
   }
   {
     // thread (bin b, quarter q): q 0/1 sum S rows [8q, 8q+8) -> both the bin
@@ -158,7 +169,11 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
       t < kCoarse ? part[2][t] + part[3][t] + part[4][t] + part[5][t] : 0;
   const uint32_t cex = scan256(tot, wsum);
   if (t < kCoarse) gbase[t] = cex + toff;
-  if (tile == 0) {
+  if (tile == 0 && bins && t < kCoarse) {
+    bins[2 * t] = cex;  // bin table: (start, count) per coarse bin
+    bins[2 * t + 1] = tot;
+  }
+  if (tile == 0 && chunks) {
     // fine-pass chunk table: slot j -> (start, len); len 0 = no chunk
     const uint32_t nch = t < kCoarse ? (tot + kFineCap - 1) / kFineCap : 0;
     const uint32_t cpre = scan256(nch, wsum);
@@ -177,7 +192,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
 #pragma unroll
       for (int r = 0; r < kGrp; ++r) {
         const uint64_t i = gb + (uint64_t)r * kPT + t;
-        k[r] = i < n ? keys[i] : 0;
+        k[r] = part_valid(i, n, gcount) ? keys[i] : 0;
       }
     }
     if (t < kCoarse) cnt[t] = 0;
@@ -185,7 +200,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = gb + (uint64_t)r * kPT + t;
-      rank[r] = i < n ? atomicAdd(&cnt[coarse_of(k[r], kr)], 1u) : 0;
+      rank[r] = part_valid(i, n, gcount) ? atomicAdd(&cnt[coarse_of(k[r], kr)], 1u) : 0;
     }
     __syncthreads();
     const uint32_t c = t < kCoarse ? cnt[t] : 0;
@@ -195,15 +210,17 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint64_t i = gb + (uint64_t)r * kPT + t;
-      if (i < n) {
+      if (part_valid(i, n, gcount)) {
         const uint32_t b = coarse_of(k[r], kr);
         stage[lex[b] + rank[r]] = k[r];
-        pos1[i] = gbase[b] + rank[r];  // coalesced in i
+        if (pay_in) pstage[lex[b] + rank[r]] = pay_in[i];
+        if (pos1) pos1[i] = gbase[b] + rank[r];  // coalesced in i
       }
     }
     __syncthreads();
     // bin-major runs out to keys1
-    const uint32_t valid = (uint32_t)min((uint64_t)kGrpKeys, n > gb ? n - gb : 0);
+    uint32_t valid = (uint32_t)min((uint64_t)kGrpKeys, n > gb ? n - gb : 0);
+    if (gcount && valid) valid = min(valid, gcount[gb / kGrpKeys]);
 #pragma unroll
     for (int r = 0; r < kGrp; ++r) {
       const uint32_t j = (uint32_t)(r * kPT + t);
@@ -211,6 +228,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
         const uint64_t key = stage[j];
         const uint32_t b = coarse_of(key, kr);
         keys1[gbase[b] + (j - lex[b])] = key;
+        if (pay1) pay1[gbase[b] + (j - lex[b])] = pstage[j];
       }
     }
     __syncthreads();
@@ -314,13 +332,30 @@ void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_
   const uint32_t groups = (uint32_t)((all_groups + kMaxTiles - 1) / kMaxTiles);
   const uint32_t tiles = (uint32_t)((all_groups + groups - 1) / groups);
   const uint32_t slots = partition_chunk_slots(n);
-  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, groups, M,
-                     S);
-  hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, groups,
-                     tiles, (const uint32_t*)M, (const uint32_t*)S, keys1, pos1, chunks,
-                     slots);
+  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr,
+                     (const uint32_t*)nullptr, groups, M, S);
+  hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, groups, tiles,
+                     (const uint32_t*)M, (const uint32_t*)S, keys1, (uint32_t*)nullptr, pos1,
+                     chunks, slots, (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1, kr,
                      (const uint32_t*)chunks, S, keys_out, src);
+}
+
+void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* gcount,
+                             const uint32_t* pay_in, uint64_t key_lo, uint32_t key_bits,
+                             uint32_t* M, uint32_t* S, uint64_t* keys1, uint32_t* pay1,
+                             uint32_t* bins, hipStream_t s) {
+  if (!n) return;
+  const KeyRange kr{key_lo, key_bits};
+  const uint64_t all_groups = (n + kGrpKeys - 1) / kGrpKeys;
+  const uint32_t groups = (uint32_t)((all_groups + kMaxTiles - 1) / kMaxTiles);
+  const uint32_t tiles = (uint32_t)((all_groups + groups - 1) / groups);
+  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, gcount,
+                     groups, M, S);
+  hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, gcount,
+                     pay_in, groups, tiles, (const uint32_t*)M, (const uint32_t*)S, keys1, pay1,
+                     (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, bins);
 }
 
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,

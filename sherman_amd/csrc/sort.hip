@@ -13,11 +13,10 @@ namespace dev {
 
 size_t scan_temp_bytes(uint64_t n);
 
-// Onesweep for every size above one block: rocPRIM's default switches to a
-// block-sort + merge-sort cascade below 2^20 items, which took ~175 us (24
-// launches) on a 0.5 Mi-pair insert batch.
-using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                           rocprim::default_config, 0>;
+// rocPRIM's default dispatch (block sort / merge sort below 2^20 items /
+// onesweep).  Forcing onesweep at 0.5 Mi pairs was slower (217 us plus 17
+// buffer fills per sort) than the merge path (175 us).
+using SortCfg = rocprim::default_config;
 
 static size_t sort_bytes_at(uint64_t n, unsigned begin_bit) {
   size_t bytes = 0;

@@ -78,6 +78,8 @@ struct shm_tree {
   uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
   uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
+  uint32_t* gcount = nullptr;       // insert ordering: survivors per 4096-op tile
+  uint32_t* bins = nullptr;         // insert ordering: (start, count) per coarse bin
   // get start pages per key prefix (dev::launch_start_table); rebuilt before a
   // search when pages were added or the root moved since it was built
   uint64_t* start = nullptr;
@@ -422,24 +424,49 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   return total;
 }
 
-int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
-                 const uint64_t* vals, uint64_t n) {
-  // 1. stable sort (key, batch index)
-  dev::launch_iota(t->ia, n, s);
-  HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, t->ka, t->ia, t->ib, n, s));
-  DBG(s, "sort(insert)");
-  // 2. keep the last writer of each key; split upserts / deletes
-  dev::launch_mark_unique(t->ka, t->ib, vals, n, t->flags, t->d_err, s);
+// keys sorted with one op per key (the last writer) -> uk/uv (upserts) and
+// dk (deletes); counts in t->h_pin[0..2] (upserts, deletes, error bits)
+int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
+                    uint64_t n, bool fast) {
+  const uint32_t* bins = nullptr;
+  if (fast) {
+    // per-tile de-dup, coarse bins, per-bin LDS sort (isort.hip)
+    dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, s);
+    dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
+                                 t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
+    dev::launch_bin_sort(t->ka, t->ib, t->bins, t->part_S, t->d_err, s);
+    bins = t->bins;
+    DBG(s, "sort(insert, fast)");
+  } else {
+    // stable sort (key, batch index)
+    dev::launch_iota(t->ia, n, s);
+    HIP_OK(dev::sort_pairs(t->temp, t->temp_bytes, keys, t->ka, t->ia, t->ib, n, s));
+    DBG(s, "sort(insert)");
+  }
+  // keep the last writer of each key; split upserts / deletes
+  dev::launch_mark_unique(t->ka, t->ib, vals, n, bins, t->flags, t->d_err, s);
   HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, t->flags, t->pos, n, s));
   dev::launch_compact_unique(t->ka, t->ib, vals, t->flags, t->pos, n, t->uk,
                              t->uv, t->dk, t->d_counts, s);
   DBG(s, "compact");
   HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
-  int rc = readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
+  return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
+}
+
+int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                 const uint64_t* vals, uint64_t n) {
+  // 1-2. order by key, one op per key (last writer in batch order)
+  int rc = order_and_dedup(t, s, keys, vals, n, use_fast_insert());
   if (rc) return rc;
+  if ((uint32_t)t->h_pin[2] & dev::kErrSortOverflow) {
+    // a coarse bin too large for the LDS sort (skewed keys): rocPRIM instead
+    HIP_OK(hipMemsetAsync(t->d_err, 0, 4, s));
+    rc = order_and_dedup(t, s, keys, vals, n, false);
+    if (rc) return rc;
+  }
   const uint64_t n_up = t->h_pin[0], n_del = t->h_pin[1];
   const uint32_t e = (uint32_t)t->h_pin[2];
-  if (e & (1u << 31)) {  // kKeyMax in the batch: reject before mutating
+  if (e & dev::kErrKeyMax) {  // kKeyMax in the batch: reject before mutating
     HIP_OK(hipMemsetAsync(t->d_err, 0, 4, s));
     return SHM_EINVAL;
   }
@@ -515,7 +542,7 @@ void free_all(shm_tree* t) {
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
-  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir);
+  F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir); F(t->gcount); F(t->bins);
   for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -692,6 +719,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   rc |= dalloc(&t->start, 1ull << start_bits());
+  rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
+  rc |= dalloc(&t->bins, 2 * dev::kCoarse);
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));

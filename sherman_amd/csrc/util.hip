@@ -36,13 +36,20 @@ void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
 
 // last occurrence of each key in the (stable) sorted batch wins
 // (last writer in batch order); low word counts upserts, high word deletes.
+// bins (nullable): only the first bins[510] + bins[511] entries are ops (the
+// insert ordering's de-duplicated length, isort.hip); the rest get flag 0
 __global__ void k_mark_unique(const uint64_t* sk, const uint32_t* sidx,
-                              const uint64_t* vals, uint64_t n, uint64_t* flags,
-                              uint32_t* err) {
+                              const uint64_t* vals, uint64_t n, const uint32_t* bins,
+                              uint64_t* flags, uint32_t* err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const uint64_t nv = bins ? (uint64_t)bins[2 * kCoarse - 2] + bins[2 * kCoarse - 1] : n;
+  if (i >= nv) {
+    flags[i] = 0;
+    return;
+  }
   const uint64_t k = sk[i];
-  const bool last = i + 1 == n || sk[i + 1] != k;
+  const bool last = i + 1 == nv || sk[i + 1] != k;
   uint64_t f = 0;
   if (k == kKeyMax) {
     atomicOr(err, 1u << 31);  // EINVAL marker
@@ -52,9 +59,9 @@ __global__ void k_mark_unique(const uint64_t* sk, const uint32_t* sidx,
   flags[i] = f;
 }
 void launch_mark_unique(const uint64_t* sk, const uint32_t* sidx,
-                        const uint64_t* vals, uint64_t n, uint64_t* flags,
-                        uint32_t* err, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_mark_unique, grid1(n), dim3(kT), 0, s, sk, sidx, vals, n, flags, err);
+                        const uint64_t* vals, uint64_t n, const uint32_t* bins,
+                        uint64_t* flags, uint32_t* err, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_mark_unique, grid1(n), dim3(kT), 0, s, sk, sidx, vals, n, bins, flags, err);
 }
 
 __global__ void k_compact_unique(const uint64_t* sk, const uint32_t* sidx,

@@ -1,0 +1,23 @@
+"""Per-step kernel breakdown of a tools/profile_c3.sh trace: kernels from the
+first get walk of the timed C3 steps on, averaged per step."""
+import collections
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1] + "/trace/run_kernel_trace.csv")))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+is_get = lambda r: "k_get<4, 1, 4, false>" in r["Kernel_Name"]
+t0 = min(int(r["Start_Timestamp"]) for r in rows if is_get(r))
+c3 = [r for r in rows if int(r["Start_Timestamp"]) >= t0]
+steps = sum(1 for r in c3 if is_get(r))
+span = (int(c3[-1]["End_Timestamp"]) - t0) / 1e3
+agg = collections.defaultdict(lambda: [0, 0.0])
+for r in c3:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    agg[r["Kernel_Name"][:80]][0] += 1
+    agg[r["Kernel_Name"][:80]][1] += d
+tot = 0.0
+for n, (c, d) in sorted(agg.items(), key=lambda x: -x[1][1])[:24]:
+    tot += d
+    print(f"{d / steps:8.1f} us/step {c / steps:5.1f} calls  {n}")
+print(f"steps {steps}  kernel sum/step {tot / steps:.1f} us  span/step {span / steps:.1f} us")
