@@ -510,6 +510,10 @@ __global__ void k_empty_leaf(uint8_t* arena, uint64_t off) {
   store_page(arena, off, lp);
 }
 
+__global__ void k_write_superblock(uint8_t* arena, Superblock sb) {
+  if (threadIdx.x == 0) *reinterpret_cast<Superblock*>(arena) = sb;
+}
+
 // ---------------------------------------------------------------------------
 static dim3 seg_grid(uint64_t waves) {
   return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -538,6 +542,9 @@ void launch_int_update(const SegArgs& a, hipStream_t s) {
 void launch_new_root(uint8_t* arena, uint64_t off, uint64_t old_root,
                      uint32_t level, hipStream_t s) {
   hipLaunchKernelGGL(k_new_root, dim3(1), dim3(kWave), 0, s, arena, off, old_root, level);
+}
+void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s) {
+  hipLaunchKernelGGL(k_write_superblock, dim3(1), dim3(kWave), 0, s, arena, sb);
 }
 void launch_empty_leaf(uint8_t* arena, uint64_t off, hipStream_t s) {
   hipLaunchKernelGGL(k_empty_leaf, dim3(1), dim3(kWave), 0, s, arena, off);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "layout.h"
+
 namespace shm {
 namespace dev {
 
@@ -69,7 +71,8 @@ struct SegArgs {
   // segments (runs of ops targeting one page)
   const uint32_t* seg_start;  // [num_seg + 1]
   const uint64_t* seg_page;   // [num_seg]
-  uint32_t num_seg;
+  uint32_t num_seg;           // (an upper bound when num_seg_dev is set)
+  const uint32_t* num_seg_dev;  // device-side segment count (nullable)
   uint32_t* seg_T;            // entries after applying
   uint32_t* seg_P;            // pages after applying (1 = in place)
   uint32_t* seg_newpages;     // P - 1
@@ -99,6 +102,7 @@ void launch_int_update(const SegArgs& a, hipStream_t s);
 void launch_new_root(uint8_t* arena, uint64_t page_off, uint64_t old_root,
                      uint32_t level, hipStream_t s);
 void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
+void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s);
 
 // ---- utilities (util.hip) -----------------------------------------------------
 void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s);

@@ -87,6 +87,7 @@ struct shm_tree {
   // leaf directory (leafdir.hip): 2^dir_bits entries of 64 B over the whole
   // key space, rebuilt before a search once the tree grew by 1/32 since the
   // last build (stale entries only cost B-link right moves)
+  bool err_pending = false;  // kernels ran since d_err was last read back
   uint64_t* dir = nullptr;
   uint32_t dir_bits = 0;
   uint64_t dir_np = 0;
@@ -274,6 +275,8 @@ int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
   return SHM_OK;
 }
 
+// superblock mirror (layout.h), written by a one-wave kernel: stream-ordered,
+// no host synchronisation
 int write_superblock(shm_tree* t, hipStream_t s) {
   Superblock sb{};
   sb.magic = kSuperMagic;
@@ -284,13 +287,13 @@ int write_superblock(shm_tree* t, hipStream_t s) {
   sb.node_id = t->cfg.node_id;
   sb.batches = t->batches;
   sb.splits = t->splits;
-  memcpy(t->h_pin, &sb, sizeof(sb));
-  HIP_OK(hipMemcpyAsync(t->arena, t->h_pin, sizeof(sb), hipMemcpyHostToDevice, s));
-  HIP_OK(hipStreamSynchronize(s));
+  dev::launch_write_superblock(t->arena, sb, s);
+  HIP_OK(hipGetLastError());
   return SHM_OK;
 }
 
 int check_err(shm_tree* t, hipStream_t s) {
+  t->err_pending = false;
   int rc = readback(t, s, t->d_err, sizeof(uint32_t));
   if (rc) return rc;
   const uint32_t e = (uint32_t)t->h_pin[0];
@@ -304,9 +307,10 @@ int check_err(shm_tree* t, hipStream_t s) {
 }
 
 // Segment a sorted op list by the page its walk ends on at `level`.
-// Returns the segment count (or negative status).
+// Returns the segment count (or negative status); with sync == false the
+// count is left in d_counts[8] and n_ops (an upper bound) is returned.
 int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
-                uint64_t n_ops, int level) {
+                uint64_t n_ops, int level, bool sync = true) {
   dev::WalkArgs w = walk_args(t);
   w.keys = op_key;
   w.n = n_ops;
@@ -333,6 +337,7 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, t->seg_start,
                        t->seg_page, d_ns, s);
   DBG(s, "seg_fill");
+  if (!sync) return (int64_t)n_ops;  // an upper bound; the count stays on the device
   int rc = readback(t, s, d_ns, sizeof(uint32_t));
   if (rc) return rc;
   return (int64_t)(uint32_t)t->h_pin[0];
@@ -360,10 +365,13 @@ int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t res
   HIP_OK(hipMemcpyAsync(d_tot, t->seg_pbase + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
   HIP_OK(hipMemcpyAsync(d_tot + 1, t->seg_np + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
   HIP_OK(hipMemcpyAsync(d_tot + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
-  int rc = readback(t, s, d_tot, 3 * sizeof(uint32_t));
+  HIP_OK(hipMemcpyAsync(d_tot + 3, t->d_counts + 8, 4, hipMemcpyDeviceToDevice, s));
+  int rc = readback(t, s, d_tot, 4 * sizeof(uint32_t));
   if (rc) return rc;
+  t->err_pending = false;
   const uint32_t* h = reinterpret_cast<const uint32_t*>(t->h_pin);
   const uint64_t total = (uint64_t)h[0] + h[1];
+  if (a.num_seg_dev) a.num_seg = h[3];  // the device-side segment count, now known
   if (h[2]) return check_err(t, s);
   if (total > t->sep_cap) return SHM_ENOMEM;
   if (t->next_page + total + reserve > t->cap_pages) return SHM_ENOMEM;
@@ -375,7 +383,8 @@ int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t res
 int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                     const uint64_t* op_val, uint64_t n_ops, int level,
                     bool is_delete, int out) {
-  const int64_t ns = segment(t, s, op_key, n_ops, level);
+  const bool fast_leaf = level == 0 && !is_delete && use_fast_insert();
+  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf);
   if (ns < 0) return ns;
   if (ns == 0) return 0;
   dev::SegArgs a = seg_args(t);
@@ -383,6 +392,8 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   a.op_val = op_val;
   a.n_ops = n_ops;
   a.num_seg = (uint32_t)ns;
+  if (fast_leaf) a.num_seg_dev = reinterpret_cast<const uint32_t*>(t->d_counts + 8);
+  t->err_pending = true;
   a.level = level;
   a.is_delete = is_delete ? 1 : 0;
   a.sep_key = t->sep_key[out];
@@ -450,6 +461,7 @@ int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint
                              t->uv, t->dk, t->d_counts, s);
   DBG(s, "compact");
   HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
+  t->err_pending = false;
   return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
 }
 
@@ -847,7 +859,8 @@ int shm_insert_batch(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
   if (rc == SHM_OK) {
     t->batches += 1;
     rc = write_superblock(t, s);
-    if (rc == SHM_OK) rc = check_err(t, s);
+    // kernels that ran after the last error read-back: check them now
+    if (rc == SHM_OK && t->err_pending) rc = check_err(t, s);
   }
   return rc;
 }

@@ -65,13 +65,19 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   const int wv = threadIdx.x >> 6;
   const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
   const uint64_t g0 = wid * G;
-  if (g0 >= a.num_seg) return;  // wave-uniform
+  // the grid may be sized for an upper bound of the segment count
+  const uint32_t num_seg = a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
+  if (g0 >= num_seg) {
+    // past the last segment: zero the new-page counts the host scans
+    if (lane < G && g0 + (uint64_t)lane < a.num_seg) a.seg_newpages[g0 + lane] = 0;
+    return;  // wave-uniform
+  }
   const uint32_t* buf = &s_pg[wv * G * kPageDwords];
   const uint32_t buf_lds = lds_addr_of(buf);
   uint32_t err = 0;
 
   // ---- slot s (lane s < G) = segment g0 + s --------------------------------
-  const bool sl = lane < G && g0 + (uint64_t)lane < a.num_seg;
+  const bool sl = lane < G && g0 + (uint64_t)lane < num_seg;
   const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
   const uint64_t page = sl ? a.seg_page[gs] : 0;
   const bool pok = sl && ptr_ok(page, a.node, a.arena_bytes);
@@ -180,11 +186,27 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
     cnt += (uint32_t)popc64((ballot(valid[j]) >> (q * L)) & kGroupMask);
   }
 
+  // ---- entries after the batch: T = valid + ops - ops whose key is present
+  // (as the plan kernel counted them); a page that would fill is left to the
+  // split path without touching its ops one by one ---------------------------------
+  uint32_t hits = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    bool h = false;
+    if (valid[j] && nops) {
+      const uint64_t x = lower_bound64(a.op_key, qst, qen, ek[j]);
+      h = x < qen && a.op_key[x] == ek[j];
+    }
+    hits += (uint32_t)popc64((ballot(h) >> (q * L)) & kGroupMask);
+  }
+  const uint32_t T = cnt + nops - hits;
+  const bool over = T > (uint32_t)(kLeafCardinality - 1);
+  const uint32_t nloop = over ? 0u : nops;
+
   // ---- apply the ops in key order -------------------------------------------------
-  uint32_t T = cnt;
-  bool over = false, bad = false;
-  for (uint32_t t = 0; ballot(t < nops); ++t) {
-    const bool act = t < nops && !bad;
+  bool bad = false;
+  for (uint32_t t = 0; ballot(t < nloop); ++t) {
+    const bool act = t < nloop && !bad;
     const uint64_t kq = act ? a.op_key[qst + t] : 0;
     const uint64_t vq = act ? a.op_val[qst + t] : 0;
     if (act && (kq < lowest || kq >= highest)) bad = true;  // not this page's key
@@ -200,14 +222,13 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
       take = li == ctz64(mh);  // the valid slot holding the key
       tj = hj;
     } else if (go) {
-      T += 1;  // a new key
-      if (T > (uint32_t)(kLeafCardinality - 1)) over = true;
+      // a new key: the first empty slot (T <= 53 guarantees one)
       int fj = -1;
 #pragma unroll
       for (int j = E - 1; j >= 0; --j)
         if (mine[j] && !valid[j]) fj = j;
-      const uint64_t me = (ballot(!over && fj >= 0) >> (q * L)) & kGroupMask;
-      if (!over && me) {
+      const uint64_t me = (ballot(fj >= 0) >> (q * L)) & kGroupMask;
+      if (me) {
         take = li == ctz64(me);  // the first empty slot
         tj = fj;
       }
@@ -237,7 +258,8 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
         put_leaf_entry(reinterpret_cast<uint32_t*>(pg), ebase + j, ek[j], ev[j], ef[j], er[j]);
   }
   const uint64_t gq = g0 + (uint64_t)q;
-  if (li == 0 && q < G && gq < a.num_seg) {
+  if (li == 0 && q < G && gq >= num_seg && gq < a.num_seg) a.seg_newpages[gq] = 0;
+  if (li == 0 && q < G && gq < num_seg) {
     const uint32_t P = (live && over) ? (T + kLeafSplitFill - 1) / kLeafSplitFill : 1u;
     a.seg_T[gq] = live ? T : 0u;
     a.seg_P[gq] = P;

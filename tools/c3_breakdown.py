@@ -1,5 +1,6 @@
-"""Per-step kernel breakdown of a tools/profile_c3.sh trace: kernels from the
-first get walk of the timed C3 steps on, averaged per step."""
+"""Per-step kernel breakdown of a kernel trace (tools/profile_c3.sh, or
+tools/profile.sh for C2): kernels from the first get walk on, averaged per
+get walk.  usage: python tools/c3_breakdown.py OUTDIR"""
 import collections
 import csv
 import sys
