@@ -186,22 +186,26 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
     cnt += (uint32_t)popc64((ballot(valid[j]) >> (q * L)) & kGroupMask);
   }
 
-  // ---- entries after the batch: T = valid + ops - ops whose key is present
-  // (as the plan kernel counted them); a page that would fill is left to the
-  // split path without touching its ops one by one ---------------------------------
-  uint32_t hits = 0;
+  // ---- entries after the batch T = valid + new keys.  More than 53 ops can
+  // never stay in place (T >= ops): count their hits by binary search, as the
+  // plan kernel did, and skip the per-op loop; smaller segments count while
+  // applying and discard the result if the page would fill ------------------------
+  const bool big = nops > (uint32_t)(kLeafCardinality - 1);
+  uint32_t T = cnt;
+  if (ballot(big)) {
+    uint32_t hits = 0;
 #pragma unroll
-  for (int j = 0; j < E; ++j) {
-    bool h = false;
-    if (valid[j] && nops) {
-      const uint64_t x = lower_bound64(a.op_key, qst, qen, ek[j]);
-      h = x < qen && a.op_key[x] == ek[j];
+    for (int j = 0; j < E; ++j) {
+      bool h = false;
+      if (big && valid[j]) {
+        const uint64_t x = lower_bound64(a.op_key, qst, qen, ek[j]);
+        h = x < qen && a.op_key[x] == ek[j];
+      }
+      hits += (uint32_t)popc64((ballot(h) >> (q * L)) & kGroupMask);
     }
-    hits += (uint32_t)popc64((ballot(h) >> (q * L)) & kGroupMask);
+    if (big) T = cnt + nops - hits;
   }
-  const uint32_t T = cnt + nops - hits;
-  const bool over = T > (uint32_t)(kLeafCardinality - 1);
-  const uint32_t nloop = over ? 0u : nops;
+  const uint32_t nloop = big ? 0u : nops;
 
   // ---- apply the ops in key order -------------------------------------------------
   bool bad = false;
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
       take = li == ctz64(mh);  // the valid slot holding the key
       tj = hj;
     } else if (go) {
-      // a new key: the first empty slot (T <= 53 guarantees one)
+      T += 1;  // a new key: the first empty slot (one exists while T <= 53)
       int fj = -1;
 #pragma unroll
       for (int j = E - 1; j >= 0; --j)
@@ -248,6 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   }
   if (ballot(bad)) err |= kErrPlan;
   live = live && !bad;
+  const bool over = T > (uint32_t)(kLeafCardinality - 1);
 
   // ---- write back the changed entries of in-place segments -----------------------
   if (live && !over) {
