@@ -17,7 +17,17 @@ Default workload, C2 (BASELINE.json configs[1]) — the headline line:
   * A step is one batch: its gets see the previous batch's state, then its
     inserts apply in batch order.
 
-N > 1 (python -m torch.distributed.run ... bench.py --gpus N, C2):
+--workload c5 (BASELINE.json configs[4], N >= 1):
+  * The C2 tree(s), then batches of 1 Mi ops per GPU.
+  * Key = to_key(1 + zipf(0.99) over the global key set).
+  * 5 % of the ops are range scans [key, key + span] with span =
+    --scan-keys * 2^64 / (global keys) (about that many stored keys per
+    scan), the other 95 % inserts of value (global op index + 1).
+  * A step is one batch: its scans see the previous batch's state, then its
+    inserts apply.  N > 1: scans are cut at shard boundaries and routed, and
+    inserts routed to their owners, with RCCL all-to-all.
+
+N > 1 (python -m torch.distributed.run ... bench.py --gpus N, C2 / C5):
   * The key space is range-partitioned, one shard per GPU: shard s owns
     [s*2^64/N, (s+1)*2^64/N).
   * Each rank holds 2^26 keys of a 2^26*N global key set.
@@ -48,11 +58,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    p.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2")
     p.add_argument("--keys-log2", type=int, default=26, help="keys per GPU = 2^k")
     p.add_argument("--batch-log2", type=int, default=20, help="ops per step per GPU")
     p.add_argument("--theta", type=float, default=0.99, help="c3 zipf skew")
     p.add_argument("--read-ratio", type=int, default=50, help="c3 get percentage")
+    p.add_argument("--scan-ratio", type=int, default=5, help="c5 range-scan percentage")
+    p.add_argument("--scan-keys", type=int, default=64,
+                   help="c5: expected stored keys per range scan")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0)
     p.add_argument("--no-sort", action="store_true", help="walk gets in input order")
@@ -119,7 +132,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
-    assert args.workload == "c2" or world == 1, "c3 is a single-GPU config"
+    assert args.workload != "c3" or world == 1, "c3 is a single-GPU config"
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -177,6 +190,38 @@ def main():
                 tree.search_batch(q, vals, found)
             else:
                 route.search(q, vals, found)
+    elif args.workload == "c5":
+        from sherman_amd.shard import umin
+        assert not sim, "--sim-world is a C2 option"
+        n_glob = n_keys * world
+        span = (1 << 64) // n_glob * args.scan_keys
+        zipf = Zipf(n_glob, args.theta, dev)
+        mixed = []
+        for b in range(N_BATCHES):
+            ids = zipf.sample(batch, g) + 1
+            k = torch.empty_like(ids)
+            tree.hash_keys(ids, k)
+            is_scan = op_is_get(batch, args.scan_ratio, dev, g)
+            op_idx = torch.arange(b * batch, (b + 1) * batch, dtype=torch.int64, device=dev)
+            op_idx += (rank * N_BATCHES) * batch
+            lo = k[is_scan].contiguous()
+            hi = lo + span  # wraps past 2^64 - 1 ...
+            hi = torch.where((hi ^ (-(1 << 63))) < (lo ^ (-(1 << 63))),
+                             torch.full_like(lo, -1), hi)  # ... so saturate
+            mixed.append((lo, umin(hi, torch.full_like(lo, -2)), k[~is_scan].contiguous(),
+                          (op_idx[~is_scan] + 1).contiguous()))
+        del keys_local
+        route = ShardRouter(tree, world, dist) if world > 1 else None
+        scan_out = {}
+
+        def step(i):
+            lo, hi, pk, pv = mixed[i % N_BATCHES]
+            if route is None:
+                scan_out["r"] = tree.range_query_batch(lo, hi)
+                tree.insert_batch(pk, pv)
+            else:
+                scan_out["r"] = route.range_query(lo, hi)
+                route.insert(pk, pv)
     else:
         zipf = Zipf(n_keys, args.theta, dev)
         mixed = []
@@ -200,6 +245,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
             cpu, parity = cpu_baseline_get(tree, qs, vals, found, args, step)
+        elif args.workload == "c5":
+            cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step)
         else:
             cpu, parity = cpu_baseline_mixed(tree, mixed, vals, found, args, step)
 
@@ -221,6 +268,9 @@ def main():
     torch.cuda.synchronize()
     if args.workload == "c2":
         hit_rate = float(found.float().mean().item())
+    elif args.workload == "c5":
+        c, _ = scan_out["r"]
+        hit_rate = float(c.float().mean().item())  # mean values per scan
     else:
         n_get = mixed[(args.steps - 1) % N_BATCHES][0].numel()
         hit_rate = float(found[:n_get].float().mean().item())
@@ -233,6 +283,10 @@ def main():
     prof = tree.profile_read(reset=True)
     tree.profile(False)
     walk_ms = prof["walk_ms"] / max(prof["calls"], 1)
+    ins_ms = prof["insert_ms"] / max(prof["insert_calls"], 1)
+    ups_ms = prof["upsert_ms"] / max(prof["insert_calls"], 1)
+    ins_per_launch = prof["insert_ops"] / max(prof["insert_calls"], 1)
+    range_ms = prof["range_ms"] / max(prof["range_calls"], 1)
     order_ms = prof["order_ms"] / max(prof["calls"], 1)
     q_per_launch = prof["queries"] / max(prof["calls"], 1)
     achieved = q_per_launch * ALG_BYTES_PER_GET / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
@@ -264,6 +318,15 @@ def main():
                             args.keys_log2, args.batch_log2, args.theta, args.read_ratio,
                             100 - args.read_ratio))
             data = "synthetic: key(i)=CityHash64(i)+1 preload, zipf op stream"
+        if args.workload == "c5":
+            metric = ("write-heavy insert + range-scan Mops/s (zipf %.2f, %d%% insert, "
+                      "%d%% scan)" % (args.theta, 100 - args.scan_ratio, args.scan_ratio))
+            workload = ("C5: 2^%d uint64 keys/GPU, 2^%d-op batches/GPU, key=to_key(1+zipf(%.2f) "
+                        "over the global key set), %d%% inserts (value = op index + 1), %d%% "
+                        "range scans of ~%d keys%s" % (
+                            args.keys_log2, args.batch_log2, args.theta, 100 - args.scan_ratio,
+                            args.scan_ratio, args.scan_keys,
+                            "" if world == 1 else ", range shards + RCCL all-to-all"))
         out = {
             "metric": metric,
             "value": round(mops, 2),
@@ -303,6 +366,22 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if args.workload == "c5":
+            # the insert pipeline dominates: ops x 1074 B over its measured
+            # chunk time (HIP events on the insert stream)
+            ach = ins_per_launch * ALG_BYTES_PER_INSERT / (ins_ms * 1e-3) / 1e9 if ins_ms else 0.0
+            out["config"]["hit_rate"] = None
+            out["config"]["values_per_scan"] = round(hit_rate, 2)
+            out["roofline"].update({
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "kernel": "insert_batch chunk (ordering + locate + k_leaf_upsert + splits)",
+                "alg_bytes_per_insert": ALG_BYTES_PER_INSERT,
+                "insert_ms_per_launch": round(ins_ms, 4),
+                "upsert_ms_per_launch": round(ups_ms, 4),
+                "inserts_per_launch": int(ins_per_launch),
+                "range_ms_per_launch": round(range_ms, 4),
+                "walk_ms_per_launch": None, "order_ms_per_launch": None,
+                "queries_per_launch": None, "alg_bytes_per_get": None})
         if args.workload == "c3":
             # whole-step algorithmic rate (gets 1040 B, inserts 1074 B per op)
             step_s = elapsed / args.steps
@@ -359,6 +438,56 @@ def cpu_baseline_get(tree, qs, vals, found, args, step):
         "sample": f"{done} uniform gets ({done // q0.size} x 1 Mi batch) over the "
                   f"GPU-built tree image, oracle Tree::search restatement, "
                   f"{threads} pinned threads on {cpu_name()}",
+    }
+    return cpu, parity
+
+
+def cpu_baseline_c5(tree, mixed, scan_out, args, step):
+    """C5 batches on the oracle over the GPU's image: the batch's range scans
+    (restated Tree::range_query, one call per scan) then its inserts (restated
+    Tree::insert), single-threaded, for ~args.cpu_seconds.  Parity: the first
+    two batches' scans return the GPU's values per scan (as multisets: leaf
+    boundaries after the batched splits may differ from the one-op-at-a-time
+    oracle's, and slots inside a leaf are unsorted)."""
+    import numpy as np
+    import torch
+
+    orc = _oracle_on_gpu_image(tree)
+    parity = True
+    done, secs, b = 0, 0.0, 0
+    cap = 1 << 16
+    while secs < args.cpu_seconds or b < 2:
+        lo, hi, pk, pv = mixed[b % N_BATCHES]
+        if b < 2:
+            step(b)
+            torch.cuda.synchronize()
+            gc, gv = scan_out["r"]
+            gc = gc.cpu().numpy()
+            gv = gv.cpu().numpy().view(np.uint64)
+            goff = np.concatenate([[0], np.cumsum(gc)])
+        loh = lo.cpu().numpy().view(np.uint64)
+        hih = hi.cpu().numpy().view(np.uint64)
+        pkh = pk.cpu().numpy().view(np.uint64)
+        pvh = pv.cpu().numpy().view(np.uint64)
+        t0 = time.perf_counter()
+        res = [orc.range_query(int(a), int(z), cap) for a, z in zip(loh, hih)]
+        orc.apply_batch(pkh, pvh)
+        secs += time.perf_counter() - t0
+        if b < 2:
+            for i, (v, cnt) in enumerate(res):
+                ok = cnt == gc[i] and np.array_equal(np.sort(v), np.sort(gv[goff[i]:goff[i + 1]]))
+                parity = parity and bool(ok)
+        done += loh.size + pkh.size
+        b += 1
+    orc.close()
+    cpu = {
+        "value": round(done / secs / 1e6, 3),
+        "unit": "Mops/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{b} C5 1 Mi-op batches ({done} ops) over the GPU-built tree image: "
+                  f"range scans then inserts, oracle Tree::range_query / Tree::insert "
+                  f"restatement, 1 thread on {cpu_name()}",
     }
     return cpu, parity
 

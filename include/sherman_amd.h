@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 2
+#define SHM_ABI_VERSION 3
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -128,13 +128,22 @@ int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
 int shm_synchronize(shm_tree *t);
 
 /* per-kernel timing with HIP events recorded on the launch stream around the
- * get path's phases (order = top-bits sort, walk = the page walk kernel).
- * Enabled handles pay two event records per phase per call. */
+ * hot path's phases (get: order = top-bits sort, walk = the page walk kernel;
+ * insert: the whole chunk and its in-place leaf upsert kernel; range: each
+ * shm_range_query launch).  Enabled handles pay one event record per phase
+ * boundary per call. */
 typedef struct shm_profile_t {
-  uint64_t calls;       /* search_batch calls (chunks) timed */
-  uint64_t queries;     /* queries in those calls */
-  double order_ms;      /* sum of get-ordering (partition) time */
-  double walk_ms;       /* sum of k_walk kernel time */
+  uint64_t calls;        /* search_batch calls (chunks) timed */
+  uint64_t queries;      /* queries in those calls */
+  double order_ms;       /* sum of get-ordering (partition) time */
+  double walk_ms;        /* sum of k_get (page walk) kernel time */
+  uint64_t insert_calls; /* insert_batch chunks timed */
+  uint64_t insert_ops;   /* ops in those chunks (before dedup) */
+  double insert_ms;      /* sum of whole-chunk insert time */
+  double upsert_ms;      /* sum of k_leaf_upsert kernel time */
+  uint64_t range_calls;  /* shm_range_query launches timed (count + fill) */
+  uint64_t range_queries;/* scans in those launches */
+  double range_ms;       /* sum of k_range kernel time */
 } shm_profile_t;
 int shm_profile_enable(shm_tree *t, int on);
 int shm_profile_read(shm_tree *t, shm_profile_t *out, int reset);

@@ -80,10 +80,18 @@ class ShmProfile(ctypes.Structure):
         ("queries", u64),
         ("order_ms", ctypes.c_double),
         ("walk_ms", ctypes.c_double),
+        ("insert_calls", u64),
+        ("insert_ops", u64),
+        ("insert_ms", ctypes.c_double),
+        ("upsert_ms", ctypes.c_double),
+        ("range_calls", u64),
+        ("range_queries", u64),
+        ("range_ms", ctypes.c_double),
     ]
 
 
 _lib = None
+ABI_VERSION = 3  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -129,6 +137,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.shm_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI {L.shm_abi_version()}, this package "
+                              f"expects {ABI_VERSION}: rebuild with `make -C sherman_amd`")
         _lib = L
     return _lib
 

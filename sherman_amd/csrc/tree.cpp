@@ -95,11 +95,17 @@ struct shm_tree {
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
+  enum ProfKind { kProfGet = 0, kProfInsert = 1, kProfRange = 2 };
+  // get: e0 order e1 walk e2; insert chunk: e0 .. e1 upsert e2 .. e3;
+  // range launch: e0 kernel e1
   struct ProfRec {
-    hipEvent_t e0, e1, e2;
+    hipEvent_t e[4];
     uint64_t n;
+    int kind;
+    bool upsert_done;
   };
   std::vector<ProfRec> prof_pending;
+  ProfRec* prof_ins = nullptr;  // the insert chunk being timed
   std::vector<hipEvent_t> event_pool;
   shm_profile_t prof_acc{};
 };
@@ -409,8 +415,14 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   int64_t total;
   if (leaf && use_fast_insert()) {
     // in-place segments are applied here; the rest go the k-way split path
+    shm_tree::ProfRec* pi = t->prof_ins;
+    if (pi && !pi->upsert_done) HIP_OK(hipEventRecord(pi->e[1], s));
     dev::launch_leaf_upsert(a, s);
     DBG(s, "leaf_upsert");
+    if (pi && !pi->upsert_done) {
+      HIP_OK(hipEventRecord(pi->e[2], s));
+      pi->upsert_done = true;
+    }
     total = new_page_total(t, s, a, reserve);
     if (total <= 0) return total;
     a.split_only = 1;
@@ -465,8 +477,8 @@ int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint
   return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
 }
 
-int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
-                 const uint64_t* vals, uint64_t n) {
+int insert_chunk_impl(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                      const uint64_t* vals, uint64_t n) {
   // 1-2. order by key, one op per key (last writer in batch order)
   int rc = order_and_dedup(t, s, keys, vals, n, use_fast_insert());
   if (rc) return rc;
@@ -514,6 +526,28 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
   return SHM_OK;
 }
 
+hipEvent_t take_event(shm_tree* t);
+int prof_begin(shm_tree* t, hipStream_t s, int kind, uint64_t n, int ne, shm_tree::ProfRec& r);
+
+// insert_chunk_impl, timed with events when profiling is on
+int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                 const uint64_t* vals, uint64_t n) {
+  if (!t->prof_on) return insert_chunk_impl(t, s, keys, vals, n);
+  shm_tree::ProfRec pr{};
+  int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
+  if (rc) return rc;
+  t->prof_ins = &pr;
+  rc = insert_chunk_impl(t, s, keys, vals, n);
+  t->prof_ins = nullptr;
+  if (!pr.upsert_done) {  // no in-place pass ran: zero-length upsert interval
+    HIP_OK(hipEventRecord(pr.e[1], s));
+    HIP_OK(hipEventRecord(pr.e[2], s));
+  }
+  HIP_OK(hipEventRecord(pr.e[3], s));
+  t->prof_pending.push_back(pr);
+  return rc;
+}
+
 hipEvent_t take_event(shm_tree* t) {
   if (!t->event_pool.empty()) {
     hipEvent_t e = t->event_pool.back();
@@ -525,22 +559,44 @@ hipEvent_t take_event(shm_tree* t) {
   return e;
 }
 
-// fold finished event triples into the accumulator
+// fold finished event records into the accumulator
 int drain_profile(shm_tree* t) {
   for (auto& r : t->prof_pending) {
-    HIP_OK(hipEventSynchronize(r.e2));
-    float a = 0.f, b = 0.f;
-    HIP_OK(hipEventElapsedTime(&a, r.e0, r.e1));
-    HIP_OK(hipEventElapsedTime(&b, r.e1, r.e2));
-    t->prof_acc.calls += 1;
-    t->prof_acc.queries += r.n;
-    t->prof_acc.order_ms += a;
-    t->prof_acc.walk_ms += b;
-    t->event_pool.push_back(r.e0);
-    t->event_pool.push_back(r.e1);
-    t->event_pool.push_back(r.e2);
+    const int ne = r.kind == shm_tree::kProfInsert ? 4 : r.kind == shm_tree::kProfGet ? 3 : 2;
+    HIP_OK(hipEventSynchronize(r.e[ne - 1]));
+    float d[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i + 1 < ne; ++i) HIP_OK(hipEventElapsedTime(&d[i], r.e[i], r.e[i + 1]));
+    auto& a = t->prof_acc;
+    if (r.kind == shm_tree::kProfGet) {
+      a.calls += 1;
+      a.queries += r.n;
+      a.order_ms += d[0];
+      a.walk_ms += d[1];
+    } else if (r.kind == shm_tree::kProfInsert) {
+      a.insert_calls += 1;
+      a.insert_ops += r.n;
+      a.insert_ms += d[0] + d[1] + d[2];
+      a.upsert_ms += d[1];
+    } else {
+      a.range_calls += 1;
+      a.range_queries += r.n;
+      a.range_ms += d[0];
+    }
+    for (int i = 0; i < ne; ++i) t->event_pool.push_back(r.e[i]);
   }
   t->prof_pending.clear();
+  return SHM_OK;
+}
+
+// start a ProfRec with `ne` events, e[0] recorded now on s
+int prof_begin(shm_tree* t, hipStream_t s, int kind, uint64_t n, int ne,
+               shm_tree::ProfRec& r) {
+  r = shm_tree::ProfRec{{nullptr, nullptr, nullptr, nullptr}, n, kind, false};
+  for (int i = 0; i < ne; ++i) {
+    r.e[i] = take_event(t);
+    if (!r.e[i]) return SHM_EIO;
+  }
+  HIP_OK(hipEventRecord(r.e[0], s));
   return SHM_OK;
 }
 
@@ -555,7 +611,9 @@ void free_all(shm_tree* t) {
   F(t->seg_pbase); F(t->seg_ver);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
   F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir); F(t->gcount); F(t->bins);
-  for (auto& r : t->prof_pending) t->event_pool.insert(t->event_pool.end(), {r.e0, r.e1, r.e2});
+  for (auto& r : t->prof_pending)
+    for (hipEvent_t e : r.e)
+      if (e) t->event_pool.push_back(e);
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
@@ -787,13 +845,10 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
     bool gathered = false;
-    shm_tree::ProfRec pr{nullptr, nullptr, nullptr, m};
+    shm_tree::ProfRec pr{};
     if (t->prof_on) {
-      pr.e0 = take_event(t);
-      pr.e1 = take_event(t);
-      pr.e2 = take_event(t);
-      if (!pr.e0 || !pr.e1 || !pr.e2) return SHM_EIO;
-      HIP_OK(hipEventRecord(pr.e0, s));
+      const int rc = prof_begin(t, s, shm_tree::kProfGet, m, 3, pr);
+      if (rc) return rc;
     }
     if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
@@ -824,7 +879,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.keys = keys + off;
       a.perm = nullptr;
     }
-    if (t->prof_on) HIP_OK(hipEventRecord(pr.e1, s));
+    if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
     if (get_kernel_v4()) {
       dev::launch_walk(a, m, kWalkDepth, false, s);
     } else {
@@ -833,7 +888,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     }
     DBG(s, "walk(get)");
     if (t->prof_on) {
-      HIP_OK(hipEventRecord(pr.e2, s));
+      HIP_OK(hipEventRecord(pr.e[2], s));
       t->prof_pending.push_back(pr);
     }
     if (gathered) {
@@ -890,9 +945,18 @@ int shm_range_query(shm_tree* t, const uint64_t* from, const uint64_t* to,
   if (offsets && !vals_out) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
+  shm_tree::ProfRec pr{};
+  if (t->prof_on) {
+    const int rc = prof_begin(t, s, shm_tree::kProfRange, n, 2, pr);
+    if (rc) return rc;
+  }
   dev::launch_range_count(t->arena, t->arena_bytes, t->cfg.node_id, t->root,
                           from, to, n, counts_out, offsets, vals_out, t->d_err, s);
   HIP_OK(hipGetLastError());
+  if (t->prof_on) {
+    HIP_OK(hipEventRecord(pr.e[1], s));
+    t->prof_pending.push_back(pr);
+  }
   return SHM_OK;
 }
 

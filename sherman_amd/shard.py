@@ -16,6 +16,12 @@ the GPU box, gloo in the CPU tests):
            bucketing is stable, so the receiver applies the union of all
            ranks' batches in rank-major batch order (last writer wins), which
            is one valid linearisation of Sherman's concurrent inserts.
+  range  : a scan [lo, hi] is cut at shard boundaries into pieces, each piece
+           goes to its owner (all_to_all of bounds), the owners scan their
+           trees (range_query_batch), and counts then values come back
+           (all_to_all); scan i's values are its pieces' values in shard
+           order, i.e. in key order across shards (Tree::range_query,
+           Tree.cpp:461-540, intended semantics).
 
 `local` is the per-rank shard: a sherman_amd.Tree on the GPU path.  Any
 object with the same five methods works (the multi-rank CPU tests plug in an
@@ -29,6 +35,29 @@ def owner_of(keys, world):
     hi = (keys >> 32) & 0xFFFFFFFF
     lo = keys & 0xFFFFFFFF
     return (hi * world + ((lo * world) >> 32)) >> 32
+
+
+_SIGN = -(1 << 63)  # int64 bit pattern of 2^63
+
+
+def _u64(x):
+    """Python int in [0, 2^64) -> the int64 holding the same bits."""
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def shard_bounds(world, device):
+    """int64 tensor of the P + 1 u64 shard boundaries ceil(s * 2^64 / P)."""
+    b = [_u64((s * (1 << 64) + world - 1) // world) for s in range(world)] + [_u64((1 << 64) - 1)]
+    return torch.tensor(b, dtype=torch.int64, device=device)
+
+
+def umax(a, b):
+    """element-wise max of u64 values held as int64 (compare with the sign bit flipped)"""
+    return torch.where((a ^ _SIGN) >= (b ^ _SIGN), a, b)
+
+
+def umin(a, b):
+    return torch.where((a ^ _SIGN) <= (b ^ _SIGN), a, b)
 
 
 def shard_range(rank, world):
@@ -92,3 +121,56 @@ class ShardRouter:
         self._a2a(rk, kb, rcnt, cnt)
         self._a2a(rv, vb, rcnt, cnt)
         self.local.insert_batch(rk, rv)
+
+    def range_query(self, lo, hi):
+        """Batched range scans [lo_i, hi_i] (inclusive, u64 held as int64).
+        Returns (counts[n] int64, values): scan i's values are
+        values[sum(counts[:i]) : sum(counts[:i+1])], in key order across shards
+        (leaf order, then slot order, inside a shard)."""
+        n, dev, P = lo.numel(), lo.device, self.world
+        s0 = owner_of(lo, P)
+        s1 = torch.maximum(owner_of(hi, P), s0)        # lo > hi: one empty piece
+        s1 = torch.where((lo ^ _SIGN) > (hi ^ _SIGN), s0, s1)
+        npc = s1 - s0 + 1
+        total = int(npc.sum().item()) if n else 0
+        scan = torch.repeat_interleave(torch.arange(n, device=dev), npc)
+        first = torch.cumsum(npc, 0) - npc
+        shard = s0[scan] + (torch.arange(total, device=dev) - first[scan])
+        bnd = shard_bounds(P, dev)
+        plo = umax(lo[scan], bnd[shard])
+        last = torch.where(shard + 1 < P, bnd[(shard + 1).clamp(max=P - 1)] - 1, bnd[P])
+        phi = umin(hi[scan], last)
+        # bucket the pieces by owner (stable) and exchange their bounds
+        kb, perm, cnt, rcnt = self._bucket(plo)
+        hb = self._buf("rq_hb", total, torch.int64, dev)
+        self.local.route_permute(phi, perm, hb)
+        nrecv = sum(rcnt)
+        rlo = self._buf("rq_rlo", nrecv, torch.int64, dev)
+        rhi = self._buf("rq_rhi", nrecv, torch.int64, dev)
+        self._a2a(rlo, kb, rcnt, cnt)
+        self._a2a(rhi, hb, rcnt, cnt)
+        rc, rv = self.local.range_query_batch(rlo, rhi)
+        # counts back (piece order as sent), then values with per-rank splits
+        bc = self._buf("rq_bc", total, torch.int64, dev)
+        self._a2a(bc, rc.to(torch.int64), cnt, rcnt)
+        seg = torch.repeat_interleave(torch.arange(P, device=dev),
+                                      torch.tensor(rcnt, device=dev))
+        vsend = torch.zeros(P, dtype=torch.int64, device=dev).index_add_(0, seg, rc.to(torch.int64))
+        vrecv = self._buf("rq_vr", P, torch.int64, dev)
+        self._a2a(vrecv, vsend)
+        vs, vr = vsend.tolist(), vrecv.tolist()
+        bv = self._buf("rq_bv", sum(vr), torch.int64, dev)
+        self._a2a(bv, rv, vr, vs)
+        # bucketed piece p is original piece perm[p]; reorder values to scan order
+        pc = torch.empty(total, dtype=torch.int64, device=dev)
+        pc[perm.long()] = bc
+        src_off = torch.cumsum(bc, 0) - bc                # offsets in bv (bucketed order)
+        src_of_orig = torch.empty(total, dtype=torch.int64, device=dev)
+        src_of_orig[perm.long()] = src_off
+        dst_off = torch.cumsum(pc, 0) - pc
+        nv = int(pc.sum().item()) if total else 0
+        shift = torch.repeat_interleave(src_of_orig - dst_off, pc)
+        values = bv[torch.arange(nv, device=dev) + shift] if nv else bv[:0]
+        counts = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, scan, pc)
+        return counts, values
+

@@ -12,7 +12,9 @@ Checked against ONE unsharded oracle tree:
     contents of applying rank 0's batch, then rank 1's, ... in batch order;
   * every shard holds only keys of its own range;
   * routed gets (hits and misses) return the unsharded tree's answers in
-    input order.
+    input order;
+  * routed range scans (boundary-crossing, whole-space, empty, single-key)
+    return the unsharded tree's values per scan.
 """
 import os
 import socket
@@ -57,6 +59,13 @@ class OracleShard:
     def insert_batch(self, keys, vals):
         self.t.apply_batch(keys.numpy().view(U64), vals.numpy().view(U64))
 
+    def range_query_batch(self, lo, hi):
+        lo, hi = lo.numpy().view(U64), hi.numpy().view(U64)
+        outs = [self.t.range_query(int(a), int(b))[0] for a, b in zip(lo, hi)]
+        counts = torch.tensor([o.size for o in outs], dtype=torch.int64)
+        vals = np.concatenate(outs) if outs else np.zeros(0, dtype=U64)
+        return counts, torch.from_numpy(vals.view(np.int64).copy())
+
 
 def rank_batches(rank, rounds=3, n=3000):
     """Insert batches of one rank: a key pool shared by all ranks (cross-rank
@@ -78,6 +87,36 @@ def query_batch(rank, n=5000):
     return np.array([to_key(int(i)) for i in ids], dtype=U64)
 
 
+def scan_batch(rank, world, n=60):
+    """Range scans of one rank: short and long spans, spans crossing one or
+    several shard boundaries, the whole key space, lo > hi (empty), and
+    single-key scans."""
+    rng = np.random.default_rng(700 + rank)
+    lo, hi = [], []
+    top = (1 << 64) - 1
+    bnd = [(s * (1 << 64) + world - 1) // world for s in range(1, world)]
+    for i in range(n):
+        c = i % 6
+        if c == 0:
+            a = int(rng.integers(0, 1 << 63)) * 2
+            b = min(top, a + (1 << 58))
+        elif c == 1:    # straddle a shard boundary
+            m = bnd[int(rng.integers(0, len(bnd)))]
+            a, b = m - (1 << 57), m + (1 << 57)
+        elif c == 2:    # cover everything
+            a, b = 0, top
+        elif c == 3:    # inverted: empty
+            a = int(rng.integers(1 << 40, 1 << 62))
+            b = a - 1
+        elif c == 4:    # one stored key exactly
+            a = b = int(to_key(int(rng.integers(1, 4001))))
+        else:           # from a boundary to the top
+            a, b = bnd[-1], top
+        lo.append(a)
+        hi.append(b)
+    return np.array(lo, dtype=U64), np.array(hi, dtype=U64)
+
+
 def worker(rank, world, port, outdir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
                             rank=rank, world_size=world)
@@ -91,9 +130,13 @@ def worker(rank, world, port, outdir):
     vals = torch.empty(q.size, dtype=torch.int64)
     found = torch.empty(q.size, dtype=torch.uint8)
     router.search(torch.from_numpy(q.view(np.int64)), vals, found)
+    slo, shi = scan_batch(rank, world)
+    counts, svals = router.range_query(torch.from_numpy(slo.view(np.int64)),
+                                       torch.from_numpy(shi.view(np.int64)))
     keys, values = shard.t.dump()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), keys=keys, values=values,
-             vals=vals.numpy(), found=found.numpy(), check=np.array([shard.t.check()[0]]))
+             vals=vals.numpy(), found=found.numpy(), check=np.array([shard.t.check()[0]]),
+             scounts=counts.numpy(), svals=svals.numpy())
     shard.t.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -134,4 +177,18 @@ def test_sharded_insert_and_get_match_unsharded_oracle(world):
             ov, of = ref.search_batch(q)
             assert np.array_equal(x["vals"].view(U64), ov)
             assert np.array_equal(x["found"], of)
+            # routed scans: per scan the unsharded tree's values (as a multiset:
+            # slots inside a leaf are unsorted, and leaf boundaries differ)
+            slo, shi = scan_batch(r, world)
+            key_of = dict(zip(rv.tolist(), rk.tolist()))  # values are unique
+            off = np.concatenate([[0], np.cumsum(x["scounts"])])
+            assert off[-1] == x["svals"].size
+            for i in range(slo.size):
+                want, _ = ref.range_query(int(slo[i]), int(shi[i]))
+                got = x["svals"][off[i]:off[i + 1]].view(U64)
+                assert np.array_equal(np.sort(got), np.sort(want)), i
+                # pieces come back in shard order (key order across shards)
+                ks = np.array([key_of[v] for v in got.tolist()], dtype=U64)
+                own = owner_of(torch.from_numpy(ks.view(np.int64)), world)
+                assert bool((own[1:] >= own[:-1]).all()), i
         ref.close()
