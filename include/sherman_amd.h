@@ -49,6 +49,8 @@ extern "C" {
 
 /* flags for shm_config.flags */
 #define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key before the walk */
+#define SHM_FLAG_LEAF_DIR 0x2u   /* start gets / leaf locates at the leaf
+                                    directory (default on) */
 
 typedef struct shm_tree shm_tree;
 

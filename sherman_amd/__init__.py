@@ -24,6 +24,7 @@ SHM_EIO = -5
 SHM_EAGAIN = -11
 SHM_E2BIG = -7
 SHM_FLAG_SORT_GETS = 0x1
+SHM_FLAG_LEAF_DIR = 0x2
 
 KEY_MAX = (1 << 64) - 1
 PAGE_SIZE = 1024
@@ -173,8 +174,8 @@ class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
-                 node_id=0, sort_gets=True, num_locks=None, sort_bits=16,
-                 key_lo=0, key_bits=64):
+                 node_id=0, sort_gets=False, num_locks=None, sort_bits=16,
+                 key_lo=0, key_bits=64, leaf_dir=True):
         L = lib()
         cfg = ShmConfig()
         _check(L.shm_config_init(ctypes.byref(cfg)), "config")
@@ -187,7 +188,8 @@ class Tree:
         cfg.sort_bits = sort_bits
         cfg.key_lo = key_lo
         cfg.key_bits = key_bits
-        cfg.flags = SHM_FLAG_SORT_GETS if sort_gets else 0
+        cfg.flags = ((SHM_FLAG_SORT_GETS if sort_gets else 0) |
+                     (SHM_FLAG_LEAF_DIR if leaf_dir else 0))
         h = vp()
         _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")
         self.h = h

@@ -198,14 +198,14 @@ bool use_fast_insert() {
   return on;
 }
 
-// SHM_LEAF_DIR=0 starts gets from the prefix start table instead of the
-// leaf directory (A/B switch)
-bool use_leaf_dir() {
-  static const bool on = [] {
+// leaf directory on (SHM_FLAG_LEAF_DIR); SHM_LEAF_DIR=0 turns it off for
+// A/B runs (gets then start at the prefix start table or the root)
+bool use_leaf_dir(const shm_tree* t) {
+  static const bool env_on = [] {
     const char* e = getenv("SHM_LEAF_DIR");
     return !(e && strcmp(e, "0") == 0);
   }();
-  return on;
+  return env_on && (t->cfg.flags & SHM_FLAG_LEAF_DIR) != 0;
 }
 
 // (re)build the leaf directory when missing or the tree grew by > 1/32;
@@ -324,7 +324,7 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   w.target_level = level;
   if (level == 0 && use_fast_insert()) {
     // the grouped get walk as a leaf locate, started from the leaf directory
-    if (use_leaf_dir()) {
+    if (use_leaf_dir(t)) {
       const int rc = refresh_dir(t, s);
       if (rc) return rc;
       w.dir = t->dir;
@@ -721,7 +721,7 @@ int shm_config_init(shm_config* c) {
   c->struct_size = sizeof(shm_config);
   c->device = 0;
   c->node_id = 0;
-  c->flags = SHM_FLAG_SORT_GETS;
+  c->flags = SHM_FLAG_LEAF_DIR;
   c->arena_bytes = 1ull << 30;
   c->max_batch = 1ull << 20;
   c->num_locks = 1u << 22;  // 32 MB: rare false sharing between waves
@@ -828,11 +828,14 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   if (!t || (n && (!keys || !vals_out))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
-  const bool use_start = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
-  if (use_start && use_leaf_dir()) {
+  // start pages: the leaf directory (any batch), else for ordered batches
+  // the prefix start table, else the root
+  const bool ordered = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
+  const bool dir = use_leaf_dir(t);
+  if (dir) {
     const int rc = refresh_dir(t, s);
     if (rc) return rc;
-  } else if (use_start && (t->start_np != t->next_page || t->start_root != t->root)) {
+  } else if (ordered && (t->start_np != t->next_page || t->start_root != t->root)) {
     dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, start_bits(),
                             t->start, t->d_err, s);
     t->start_np = t->next_page;
@@ -850,7 +853,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       const int rc = prof_begin(t, s, shm_tree::kProfGet, m, 3, pr);
       if (rc) return rc;
     }
-    if ((t->cfg.flags & SHM_FLAG_SORT_GETS) && m >= kSortMinGets) {
+    if (ordered && m >= kSortMinGets) {
       // order the batch by its top key bits so queries that share pages are
       // walked by the same wave (one page read per group, not per query)
       // (keys1 = kb, pos1 = ia, walk order = ka, src = ib); the walk stores
@@ -864,7 +867,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.out_val = t->kb;
       a.out_found = nullptr;
       a.xcd_remap = getenv("SHM_XCD_REMAP") ? atoi(getenv("SHM_XCD_REMAP")) : 1;
-      if (use_leaf_dir()) {
+      if (dir) {
         a.dir = t->dir;
         a.dir_lo = t->cfg.key_lo;
         a.dir_shift = t->cfg.key_bits - t->dir_bits;
@@ -875,6 +878,19 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       }
       gathered = true;
       DBG(s, "sort(get)");
+    } else if (dir) {
+      // unordered (default): every wave sorts its own 64 keys and starts at
+      // the leaf directory; results land in input order (no unpartition pass).
+      // With the directory a get reads one leaf, so the batch-wide key order
+      // only buys page sharing between waves, which costs more to set up than
+      // it saves (uniform and zipf 0.99 alike)
+      a.keys = keys + off;
+      a.perm = nullptr;
+      a.xcd_remap = 0;
+      a.dir = t->dir;
+      a.dir_lo = t->cfg.key_lo;
+      a.dir_shift = t->cfg.key_bits - t->dir_bits;
+      a.dir_n = 1ull << t->dir_bits;
     } else {
       a.keys = keys + off;
       a.perm = nullptr;

@@ -317,10 +317,17 @@ def test_route_bucket_roundtrip(lib_ok):
     t.close()
 
 
-def test_uniform_get_large_vs_oracle(lib_ok):
-    """2^21 hashed keys, 2^20 uniform queries (sorted-get path) vs oracle."""
+# get start modes: (sort_gets, leaf_dir); the default is unordered from the
+# leaf directory
+START_MODES = [(False, True), (True, True), (True, False), (False, False)]
+
+
+@pytest.mark.parametrize("sort_gets,leaf_dir", START_MODES[:2])
+def test_uniform_get_large_vs_oracle(lib_ok, sort_gets, leaf_dir):
+    """2^21 hashed keys, 2^20 uniform queries vs oracle."""
     n = 1 << 21
-    t = shm.Tree(arena_bytes=1 << 30, max_batch=1 << 20)
+    t = shm.Tree(arena_bytes=1 << 30, max_batch=1 << 20, sort_gets=sort_gets,
+                 leaf_dir=leaf_dir)
     keys = torch.empty(n, dtype=torch.int64, device="cuda")
     t.gen_keys(1, n, keys)
     vals = (torch.arange(1, n + 1, device="cuda", dtype=torch.int64) * 2)
@@ -339,10 +346,13 @@ def test_uniform_get_large_vs_oracle(lib_ok):
     t.close()
 
 
-def test_sorted_get_skewed_and_ragged(lib_ok):
-    """Sorted-get partition under skew: one 16-bit bucket far larger than a
-    fine-pass chunk, next to uniform keys, with a ragged batch length."""
-    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 18)
+@pytest.mark.parametrize("sort_gets,leaf_dir", START_MODES)
+def test_sorted_get_skewed_and_ragged(lib_ok, sort_gets, leaf_dir):
+    """Gets under skew: one 16-bit bucket far larger than a fine-pass chunk of
+    the sorted-get partition, next to uniform keys, with a ragged batch
+    length, in every start mode."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 18, sort_gets=sort_gets,
+                 leaf_dir=leaf_dir)
     orc = OracleTree(256 << 20)
     dense = np.arange(1, 60001, dtype=U64) * U64(3)           # all in bucket 0
     spread = hashed_keys(1, 40001)
@@ -361,14 +371,15 @@ def test_sorted_get_skewed_and_ragged(lib_ok):
     t.close()
 
 
-def test_mixed_zipf_batches_vs_oracle(lib_ok):
+@pytest.mark.parametrize("sort_gets", [False, True])
+def test_mixed_zipf_batches_vs_oracle(lib_ok, sort_gets):
     """Config C3 at small scale: zipf(0.99) key stream, 50 % get / 50 % insert
     (oracle generators = the reference's zipf.h / rand_r restatement), batch
     semantics of SURVEY §8a: each batch's gets see the previous batch's state,
     then its inserts apply in batch order.  Every get result and the final
     contents must equal the oracle's."""
     n_items, batch = 1 << 16, 1 << 14
-    t = shm.Tree(arena_bytes=128 << 20, max_batch=1 << 15)
+    t = shm.Tree(arena_bytes=128 << 20, max_batch=1 << 15, sort_gets=sort_gets)
     orc = OracleTree(128 << 20)
     pre = hashed_keys(1, n_items + 1)
     pv = np.arange(1, n_items + 1, dtype=U64) * U64(2)
