@@ -19,7 +19,8 @@ Default workload, C2 (BASELINE.json configs[1]) — the headline line:
 
 --workload c5 (BASELINE.json configs[4], N >= 1):
   * The C2 tree(s), then batches of 1 Mi ops per GPU.
-  * Key = to_key(1 + zipf(0.99) over the global key set).
+  * Key = to_key(1 + zipf(0.99) over twice the global key set): the ids past
+    the preload are new keys, so leaves split (within their shard).
   * 5 % of the ops are range scans [key, key + span] with span =
     --scan-keys * 2^64 / (global keys) (about that many stored keys per
     scan), the other 95 % inserts of value (global op index + 1).
@@ -64,7 +65,7 @@ def parse():
     p.add_argument("--theta", type=float, default=0.99, help="c3 zipf skew")
     p.add_argument("--read-ratio", type=int, default=50, help="c3 get percentage")
     p.add_argument("--scan-ratio", type=int, default=5, help="c5 range-scan percentage")
-    p.add_argument("--scan-keys", type=int, default=64,
+    p.add_argument("--scan-keys", type=int, default=100,
                    help="c5: expected stored keys per range scan")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0)
@@ -196,7 +197,7 @@ def main():
         assert not sim, "--sim-world is a C2 option"
         n_glob = n_keys * world
         span = (1 << 64) // n_glob * args.scan_keys
-        zipf = Zipf(n_glob, args.theta, dev)
+        zipf = Zipf(2 * n_glob, args.theta, dev)  # ids > n_glob: new keys
         mixed = []
         for b in range(N_BATCHES):
             ids = zipf.sample(batch, g) + 1
@@ -255,6 +256,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     barrier()
+    splits0 = tree.stats()["splits"]
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -264,6 +266,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    st_end = tree.stats()
     total_ops = batch * args.steps * world
     mops = total_ops / elapsed / 1e6
     torch.cuda.synchronize()
@@ -323,7 +326,7 @@ def main():
             metric = ("write-heavy insert + range-scan Mops/s (zipf %.2f, %d%% insert, "
                       "%d%% scan)" % (args.theta, 100 - args.scan_ratio, args.scan_ratio))
             workload = ("C5: 2^%d uint64 keys/GPU, 2^%d-op batches/GPU, key=to_key(1+zipf(%.2f) "
-                        "over the global key set), %d%% inserts (value = op index + 1), %d%% "
+                        "over 2x the global key set), %d%% inserts (value = op index + 1), %d%% "
                         "range scans of ~%d keys%s" % (
                             args.keys_log2, args.batch_log2, args.theta, 100 - args.scan_ratio,
                             args.scan_ratio, args.scan_keys,
@@ -350,6 +353,8 @@ def main():
                 "sorted_gets": args.sort,
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
+                "splits_in_timed_steps": st_end["splits"] - splits0,
+                "pages_after": st_end["pages_used"],
             },
             "roofline": {
                 "bound": "hbm",
@@ -396,10 +401,10 @@ def main():
     tree.close()
 
 
-def _oracle_on_gpu_image(tree):
+def _oracle_on_gpu_image(tree, spare_bytes=0):
     from oracle.pyoracle import OracleTree
     img, root = tree.dump_image()
-    orc = OracleTree(image=img, root_ptr=root, node_id=tree.node_id)
+    orc = OracleTree(image=img, root_ptr=root, node_id=tree.node_id, spare_bytes=spare_bytes)
     del img
     return orc
 
@@ -453,10 +458,9 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     import numpy as np
     import torch
 
-    orc = _oracle_on_gpu_image(tree)
+    orc = _oracle_on_gpu_image(tree, spare_bytes=2 << 30)  # C5 inserts new keys
     parity = True
     done, secs, b = 0, 0.0, 0
-    cap = 1 << 16
     while secs < args.cpu_seconds or b < 2:
         lo, hi, pk, pv = mixed[b % N_BATCHES]
         if b < 2:
@@ -471,13 +475,15 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
         pkh = pk.cpu().numpy().view(np.uint64)
         pvh = pv.cpu().numpy().view(np.uint64)
         t0 = time.perf_counter()
-        res = [orc.range_query(int(a), int(z), cap) for a, z in zip(loh, hih)]
+        oc, ov = orc.range_query_batch(loh, hih)
         orc.apply_batch(pkh, pvh)
         secs += time.perf_counter() - t0
         if b < 2:
-            for i, (v, cnt) in enumerate(res):
-                ok = cnt == gc[i] and np.array_equal(np.sort(v), np.sort(gv[goff[i]:goff[i + 1]]))
-                parity = parity and bool(ok)
+            ooff = np.concatenate([[0], np.cumsum(oc)]).astype(np.int64)
+            parity = parity and bool(np.array_equal(oc.astype(np.int64), gc))
+            for i in range(loh.size if parity else 0):
+                parity = parity and bool(np.array_equal(
+                    np.sort(ov[ooff[i]:ooff[i + 1]]), np.sort(gv[goff[i]:goff[i + 1]])))
         done += loh.size + pkh.size
         b += 1
     orc.close()

@@ -32,7 +32,7 @@ def lib():
         L.orc_tree_create.restype = vp
         L.orc_tree_create.argtypes = [u64]
         L.orc_tree_wrap_image.restype = vp
-        L.orc_tree_wrap_image.argtypes = [vp, u64, u64, ctypes.c_uint16]
+        L.orc_tree_wrap_image.argtypes = [vp, u64, u64, u64, ctypes.c_uint16]
         L.orc_tree_destroy.argtypes = [vp]
         L.orc_search.restype = ctypes.c_int
         L.orc_search.argtypes = [vp, u64, ctypes.POINTER(u64)]
@@ -41,6 +41,8 @@ def lib():
         L.orc_del.argtypes = [vp, u64]
         L.orc_range_query.restype = u64
         L.orc_range_query.argtypes = [vp, u64, u64, vp, u64]
+        L.orc_range_query_batch.restype = u64
+        L.orc_range_query_batch.argtypes = [vp, vp, vp, u64, vp, vp, u64]
         L.orc_search_batch.argtypes = [vp, vp, u64, vp, vp]
         L.orc_search_batch_mt.restype = ctypes.c_double
         L.orc_search_batch_mt.argtypes = [vp, vp, u64, vp, vp, ctypes.c_int]
@@ -79,12 +81,20 @@ def _p(a):
 class OracleTree:
     """Reference-semantics tree on a host arena (the checker)."""
 
-    def __init__(self, arena_bytes=1 << 26, image=None, root_ptr=0, node_id=0):
+    def __init__(self, arena_bytes=1 << 26, image=None, root_ptr=0, node_id=0,
+                 spare_bytes=0):
+        """New tree, or (image=...) a tree over a page image; spare_bytes of
+        free pages after the image take the splits of later inserts."""
         L = lib()
         self._image = None
         if image is not None:
-            self._image = np.ascontiguousarray(image, dtype=np.uint8)
-            self.h = L.orc_tree_wrap_image(_p(self._image), self._image.nbytes,
+            used = image.nbytes
+            if spare_bytes:
+                self._image = np.zeros(used + spare_bytes, dtype=np.uint8)
+                self._image[:used] = np.asarray(image, dtype=np.uint8).reshape(-1)
+            else:
+                self._image = np.ascontiguousarray(image, dtype=np.uint8)
+            self.h = L.orc_tree_wrap_image(_p(self._image), used, self._image.nbytes,
                                            root_ptr, node_id)
         else:
             self.h = L.orc_tree_create(arena_bytes)
@@ -117,6 +127,20 @@ class OracleTree:
         out = np.zeros(cap, dtype=np.uint64)
         n = lib().orc_range_query(self.h, lo, hi, _p(out), cap)
         return out[: min(n, cap)].copy(), n
+
+    def range_query_batch(self, lo, hi):
+        """Scans [lo_i, hi_i] in order: (counts, values concatenated)."""
+        lo = np.ascontiguousarray(lo, dtype=np.uint64)
+        hi = np.ascontiguousarray(hi, dtype=np.uint64)
+        counts = np.zeros(lo.size, dtype=np.uint64)
+        cap = max(1024, 128 * lo.size)
+        while True:
+            out = np.empty(cap, dtype=np.uint64)
+            total = lib().orc_range_query_batch(self.h, _p(lo), _p(hi), lo.size, _p(counts),
+                                                _p(out), cap)
+            if total <= cap:
+                return counts, out[:total].copy()
+            cap = int(total)
 
     def search_batch(self, keys):
         keys = np.ascontiguousarray(keys, dtype=np.uint64)

@@ -116,7 +116,6 @@ static uint8_t *page_at(orc_tree *t, uint64_t ga) {
 /* DSM::alloc (include/DSM.h:198-224) -> bump inside the arena; offset 0 is
  * reserved as Null like chunk 0 (GlobalAllocator.h:24-26). */
 static uint64_t orc_alloc(orc_tree *t) {
-  ORC_ASSERT(t->owns);
   if (t->next_off + K_PAGE > t->arena_bytes) {
     fprintf(stderr, "oracle: shared memory space run out\n");
     abort();
@@ -190,10 +189,12 @@ orc_tree *orc_tree_create(uint64_t arena_bytes) {
 }
 
 orc_tree *orc_tree_wrap_image(uint8_t *image, uint64_t image_bytes,
-                              uint64_t root_ptr, uint16_t node_id) {
+                              uint64_t capacity_bytes, uint64_t root_ptr,
+                              uint16_t node_id) {
   orc_tree *t = (orc_tree *)calloc(1, sizeof(orc_tree));
   t->arena = image;
-  t->arena_bytes = image_bytes;
+  /* pages past image_bytes (up to capacity_bytes) are free for splits */
+  t->arena_bytes = capacity_bytes > image_bytes ? capacity_bytes : image_bytes;
   t->next_off = image_bytes;
   t->owns = 0;
   t->node_id = node_id;
@@ -599,6 +600,20 @@ uint64_t orc_range_query(orc_tree *t, uint64_t from, uint64_t to,
 }
 
 /* ---- batched helpers ------------------------------------------------------- */
+/* scans i = 0..n-1 one after the other: counts[i] = matches of scan i, values
+ * concatenated into out (truncated at cap); returns the total count */
+uint64_t orc_range_query_batch(orc_tree *t, const uint64_t *from, const uint64_t *to,
+                               uint64_t n, uint64_t *counts, uint64_t *out,
+                               uint64_t cap) {
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t room = total < cap ? cap - total : 0;
+    counts[i] = orc_range_query(t, from[i], to[i], out + (room ? total : 0), room);
+    total += counts[i];
+  }
+  return total;
+}
+
 void orc_search_batch(orc_tree *t, const uint64_t *keys, uint64_t n,
                       uint64_t *vals, uint8_t *found) {
   for (uint64_t i = 0; i < n; ++i) {

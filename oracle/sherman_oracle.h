@@ -38,10 +38,13 @@ orc_tree *orc_tree_create(uint64_t arena_bytes);
 void orc_tree_destroy(orc_tree *t);
 
 /* Wrap an externally produced tree image (e.g. a GPU arena copied to host).
- * `image` must stay alive; offsets in GlobalAddresses index into it; the
- * node id bits (low 16) of every pointer must equal `node_id`. */
+ * `image` must stay alive and hold `capacity_bytes` (>= image_bytes): the
+ * pages past image_bytes are allocated by later splits; offsets in
+ * GlobalAddresses index into it; the node id bits (low 16) of every pointer
+ * must equal `node_id`. */
 orc_tree *orc_tree_wrap_image(uint8_t *image, uint64_t image_bytes,
-                              uint64_t root_ptr, uint16_t node_id);
+                              uint64_t capacity_bytes, uint64_t root_ptr,
+                              uint16_t node_id);
 
 /* operations (single op, reference semantics) ------------------------------ */
 /* Tree::search  src/Tree.cpp:405-459 */
@@ -56,6 +59,9 @@ void orc_del(orc_tree *t, uint64_t k);
  * values are written). */
 uint64_t orc_range_query(orc_tree *t, uint64_t from, uint64_t to,
                          uint64_t *out, uint64_t cap);
+uint64_t orc_range_query_batch(orc_tree *t, const uint64_t *from, const uint64_t *to,
+                               uint64_t n, uint64_t *counts, uint64_t *out,
+                               uint64_t cap);
 
 /* batched helpers ----------------------------------------------------------- */
 void orc_search_batch(orc_tree *t, const uint64_t *keys, uint64_t n,

@@ -60,11 +60,8 @@ class OracleShard:
         self.t.apply_batch(keys.numpy().view(U64), vals.numpy().view(U64))
 
     def range_query_batch(self, lo, hi):
-        lo, hi = lo.numpy().view(U64), hi.numpy().view(U64)
-        outs = [self.t.range_query(int(a), int(b))[0] for a, b in zip(lo, hi)]
-        counts = torch.tensor([o.size for o in outs], dtype=torch.int64)
-        vals = np.concatenate(outs) if outs else np.zeros(0, dtype=U64)
-        return counts, torch.from_numpy(vals.view(np.int64).copy())
+        c, v = self.t.range_query_batch(lo.numpy().view(U64), hi.numpy().view(U64))
+        return torch.from_numpy(c.view(np.int64)), torch.from_numpy(v.view(np.int64))
 
 
 def rank_batches(rank, rounds=3, n=3000):
