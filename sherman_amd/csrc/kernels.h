@@ -44,6 +44,9 @@ void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
 // the same walk as a leaf locate (insert path): out_page[i] = leaf of keys[i]
 void launch_locate_leaf(const WalkArgs& a, uint64_t n, hipStream_t s);
+// header-only descent, lane = op (locate.hip): out_page[i] = the page of
+// a.target_level holding keys[i]; starts at the leaf directory for level 0
+void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
 // start[p] = the deepest page whose fences cover every key with prefix p
 // (key >> (64 - bits) == p), found by walking from root.  A page's lowest
 // fence never changes (a split keeps the left half in place), so a start page

@@ -1,0 +1,124 @@
+// locate.hip — the insert path's descent (Tree::insert down to the target
+// level, src/Tree.cpp:353-403, with page_search's fence / sibling rule,
+// Tree.cpp:593-663): out_page[i] = the page of level `target_level` whose
+// fences [lowest, highest) hold keys[i].
+//
+// A locate needs a page's header, not its entries: lane = op, and each hop
+// reads the 44 B header plus the rear version word straight from global
+// memory (two 64 B lines instead of the 1 KB page a get must scan).
+//   * target level 0 starts at the leaf directory entry of the key (leafdir.hip;
+//     usually the leaf itself, else a covering internal page), level >= 1 at
+//     the root;
+//   * version check front == rear (Tree.h:306-327), re-read on mismatch;
+//   * k >= highest -> sibling (B-link turn right), k < lowest -> error;
+//   * internal page above the target: branchless search over its sorted keys
+//     (child = #keys <= k, internal_page_search, Tree.cpp:665-685), 6 dependent
+//     8 B loads from L2-resident upper levels.
+// Op keys arrive sorted, so neighbouring lanes read the same header lines.
+#include "device_common.h"
+#include "kernels.h"
+
+namespace shm {
+namespace dev {
+
+namespace {
+
+constexpr int kLocBlock = 256;
+
+__device__ __forceinline__ uint64_t g_u64(const uint32_t* p, int d) {
+  return (uint64_t)p[d] | ((uint64_t)p[d + 1] << 32);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * kLocBlock + threadIdx.x;
+  const uint64_t n = a.n_dev ? *a.n_dev : a.n;
+  if (i >= n) return;
+  const uint64_t k = a.keys[i];
+  uint64_t ptr = a.root;
+  if (a.dir && a.target_level == 0) {
+    const uint64_t p = (k - a.dir_lo) >> a.dir_shift;
+    if (k >= a.dir_lo && p < a.dir_n) {
+      const u32x4* e = reinterpret_cast<const u32x4*>(a.dir + 8 * p);
+      const u32x4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+      const uint64_t sep1 = (uint64_t)e2.x | ((uint64_t)e2.y << 32);
+      const uint64_t sep2 = (uint64_t)e2.z | ((uint64_t)e2.w << 32);
+      const uint64_t sep3 = (uint64_t)e3.x | ((uint64_t)e3.y << 32);
+      const uint32_t cnt = e3.z;
+      const uint32_t j = (uint32_t)(cnt > 1 && k >= sep1) + (uint32_t)(cnt > 2 && k >= sep2) +
+                         (uint32_t)(cnt > 3 && k >= sep3);
+      const uint32_t lo32 = j == 0 ? e0.x : j == 1 ? e0.z : j == 2 ? e1.x : e1.z;
+      const uint32_t hi32 = j == 0 ? e0.y : j == 1 ? e0.w : j == 2 ? e1.y : e1.w;
+      ptr = (uint64_t)lo32 | ((uint64_t)hi32 << 32);
+    }
+  }
+  uint32_t err = 0;
+  int retries = 0;
+  uint64_t out = 0;
+  for (int hop = 0;; ++hop) {
+    if (hop > kMaxRounds) {
+      err |= kErrRounds;
+      break;
+    }
+    if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
+      err |= kErrBadPtr;
+      break;
+    }
+    const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + ga_offset(ptr));
+    const u32x4 A = *reinterpret_cast<const u32x4*>(pg);      // dwords 0..3
+    const u32x4 B = *reinterpret_cast<const u32x4*>(pg + 4);  // dwords 4..7
+    const u32x4 C = *reinterpret_cast<const u32x4*>(pg + 8);  // dwords 8..11
+    const uint2 Z = *reinterpret_cast<const uint2*>(pg + 254);
+    const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
+                              ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
+    const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
+                             ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
+    const int level = (int)((B.z >> 8) & 0xFF);  // byte 25
+    const int cnt = (int)(int16_t)(B.z >> 16) + 1;
+    const uint64_t lowest = (uint64_t)B.w | ((uint64_t)C.x << 32);
+    const uint64_t highest = (uint64_t)C.y | ((uint64_t)C.z << 32);
+    const bool is_leaf = leftmost == 0;
+    const uint32_t rver = (is_leaf ? Z.x : Z.y) & 0xFF;
+    if ((A.z & 0xFF) != rver) {  // torn page: read it again
+      if (++retries > kMaxRetries) {
+        err |= kErrInconsistent;
+        break;
+      }
+      continue;
+    }
+    if (k >= highest && sibling != 0) {  // turn right (Tree.cpp:626-629)
+      ptr = sibling;
+      continue;
+    }
+    if (k < lowest || k >= highest || level < a.target_level) {
+      err |= kErrFence;
+      break;
+    }
+    if (level == a.target_level) {
+      out = ptr;
+      break;
+    }
+    // internal page above the target: number of keys <= k (keys increase)
+    int pos = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+      const int idx = pos + step - 1;
+      const int ci = idx < 60 ? idx : 60;
+      const uint64_t kk = g_u64(pg, 11 + 4 * ci);
+      pos += (idx < cnt && kk <= k) ? step : 0;
+    }
+    ptr = pos == 0 ? leftmost : g_u64(pg, 13 + 4 * (pos - 1));
+  }
+  if (err) atomicOr(a.err, err);
+  a.out_page[i] = out;
+}
+
+void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {
+  if (n_upper == 0) return;
+  hipLaunchKernelGGL(k_locate, dim3((unsigned)((n_upper + kLocBlock - 1) / kLocBlock)),
+                     dim3(kLocBlock), 0, s, a);
+}
+
+}  // namespace dev
+}  // namespace shm

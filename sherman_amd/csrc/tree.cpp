@@ -315,6 +315,16 @@ int check_err(shm_tree* t, hipStream_t s) {
 // Segment a sorted op list by the page its walk ends on at `level`.
 // Returns the segment count (or negative status); with sync == false the
 // count is left in d_counts[8] and n_ops (an upper bound) is returned.
+// SHM_LOCATE: 0 = header-only k_locate (default), 1 = the grouped k_get walk
+// for leaves, 2 = the LDS page walk k_walk (A/B switches)
+int locate_kernel() {
+  static const int v = [] {
+    const char* e = getenv("SHM_LOCATE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                 uint64_t n_ops, int level, bool sync = true) {
   dev::WalkArgs w = walk_args(t);
@@ -322,9 +332,9 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   w.n = n_ops;
   w.out_page = t->pages;
   w.target_level = level;
-  if (level == 0 && use_fast_insert()) {
-    // the grouped get walk as a leaf locate, started from the leaf directory
-    if (use_leaf_dir(t)) {
+  if (locate_kernel() != 2 && (level > 0 || use_fast_insert())) {
+    // header-only descent, lane per op; leaves start at the leaf directory
+    if (level == 0 && use_leaf_dir(t)) {
       const int rc = refresh_dir(t, s);
       if (rc) return rc;
       w.dir = t->dir;
@@ -332,7 +342,10 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
       w.dir_shift = t->cfg.key_bits - t->dir_bits;
       w.dir_n = 1ull << t->dir_bits;
     }
-    dev::launch_locate_leaf(w, n_ops, s);
+    if (locate_kernel() == 1 && level == 0)
+      dev::launch_locate_leaf(w, n_ops, s);  // the grouped get walk (A/B)
+    else
+      dev::launch_locate(w, n_ops, s);
   } else {
     dev::launch_walk(w, n_ops, 4, true, s);
   }
