@@ -46,6 +46,7 @@ extern "C" {
 #define SHM_EIO (-5)       /* HIP failure or tree inconsistency detected */
 #define SHM_EAGAIN (-11)   /* optimistic version/lock check failed */
 #define SHM_E2BIG (-7)     /* batch larger than cfg.max_batch */
+#define SHM_ENOSPC (-28)   /* output buffer too small (size reported) */
 
 /* flags for shm_config.flags */
 #define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key before the walk */
@@ -113,6 +114,15 @@ int shm_del_batch(shm_tree *t, const uint64_t *keys, uint64_t n, void *stream);
 int shm_range_query(shm_tree *t, const uint64_t *from, const uint64_t *to,
                     uint64_t n, uint64_t *counts_out, const uint64_t *offsets,
                     uint64_t *vals_out, void *stream);
+/* The same scans sized in one call: counts_out, offsets_out (exclusive scan
+ * of the counts, absolute) and *total_out are always produced (one host
+ * synchronisation); the values are written to vals_out when total <=
+ * vals_cap, else SHM_ENOSPC is returned and the caller fills a larger buffer
+ * with shm_range_query(..., offsets_out, vals). */
+int shm_range_query_batch(shm_tree *t, const uint64_t *from, const uint64_t *to,
+                          uint64_t n, uint64_t *counts_out, uint64_t *offsets_out,
+                          uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_out,
+                          void *stream);
 
 /* introspection / images (host pointers) ------------------------------------- */
 int shm_stats(shm_tree *t, shm_stats_t *out);

@@ -23,6 +23,7 @@ SHM_ENOMEM = -12
 SHM_EIO = -5
 SHM_EAGAIN = -11
 SHM_E2BIG = -7
+SHM_ENOSPC = -28
 SHM_FLAG_SORT_GETS = 0x1
 SHM_FLAG_LEAF_DIR = 0x2
 
@@ -105,6 +106,8 @@ _SIGNATURES = [
     ("shm_insert_batch", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_del_batch", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
+    ("shm_range_query_batch", ctypes.c_int,
+     [vp, vp, vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
     ("shm_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmStats)]),
     ("shm_dump_image", ctypes.c_int, [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
@@ -225,20 +228,27 @@ class Tree:
                                    _stream_ptr(stream)), "del_batch")
 
     def range_query_batch(self, lo, hi, stream=None):
-        """Returns (counts, values concatenated in query order)."""
+        """Batched inclusive scans [lo_i, hi_i]: (counts, values concatenated
+        in query order), both on the device; one host synchronisation (the
+        total).  Results are stream-ordered on `stream`."""
         import torch
         n = lo.numel()
-        counts = torch.empty(n, dtype=torch.int64, device=lo.device)
-        _check(lib().shm_range_query(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
-                                     None, None, _stream_ptr(stream)), "range_query")
-        self.synchronize()
-        offs = torch.cumsum(counts, 0) - counts
-        total = int(counts.sum().item()) if n else 0
-        vals = torch.empty(max(total, 1), dtype=torch.int64, device=lo.device)
-        _check(lib().shm_range_query(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
-                                     _ptr(offs), _ptr(vals), _stream_ptr(stream)),
-               "range_query")
-        self.synchronize()
+        dev = lo.device
+        counts = torch.empty(n, dtype=torch.int64, device=dev)
+        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        cap = getattr(self, "_rq_cap", 1 << 16)
+        vals = torch.empty(cap, dtype=torch.int64, device=dev)
+        total = u64(0)
+        rc = lib().shm_range_query_batch(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
+                                         _ptr(offs), _ptr(vals), cap, ctypes.byref(total),
+                                         _stream_ptr(stream))
+        total = int(total.value)
+        if rc == SHM_ENOSPC:
+            vals = torch.empty(total, dtype=torch.int64, device=dev)
+            rc = lib().shm_range_query(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
+                                       _ptr(offs), _ptr(vals), _stream_ptr(stream))
+        _check(rc, "range_query_batch")
+        self._rq_cap = max(cap, total + total // 4)
         return counts, vals[:total]
 
     # -- reference single-op API (Tree.h:47-54) -------------------------------

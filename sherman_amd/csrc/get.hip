@@ -83,20 +83,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   uint64_t ptr = a.root;
   if (a.dir) {
     // leaf directory: start at the leaf (or the covering internal page)
-    const uint64_t p = (k - a.dir_lo) >> a.dir_shift;
-    if (k >= a.dir_lo && p < a.dir_n && k != kKeyMax) {
-      const u32x4* e = reinterpret_cast<const u32x4*>(a.dir + 8 * p);
-      const u32x4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-      const uint64_t sep1 = (uint64_t)e2.x | ((uint64_t)e2.y << 32);
-      const uint64_t sep2 = (uint64_t)e2.z | ((uint64_t)e2.w << 32);
-      const uint64_t sep3 = (uint64_t)e3.x | ((uint64_t)e3.y << 32);
-      const uint32_t cnt = e3.z;
-      const uint32_t i = (uint32_t)(cnt > 1 && k >= sep1) + (uint32_t)(cnt > 2 && k >= sep2) +
-                         (uint32_t)(cnt > 3 && k >= sep3);
-      const uint32_t lo32 = i == 0 ? e0.x : i == 1 ? e0.z : i == 2 ? e1.x : e1.z;
-      const uint32_t hi32 = i == 0 ? e0.y : i == 1 ? e0.w : i == 2 ? e1.y : e1.w;
-      ptr = (uint64_t)lo32 | ((uint64_t)hi32 << 32);
-    }
+    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, k, ptr);
   } else if (a.start) {
     ptr = a.start[k >> a.start_shift];
   }

@@ -178,11 +178,31 @@ void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64
                     hipStream_t s);
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
                       uint64_t* out, hipStream_t s);
-void launch_range_count(const uint8_t* arena, uint64_t arena_bytes,
-                        uint16_t node, uint64_t root, const uint64_t* from,
-                        const uint64_t* to, uint64_t n, uint64_t* counts,
-                        const uint64_t* offsets, uint64_t* vals,
-                        uint32_t* err, hipStream_t s);
+// batched range scans (range.hip)
+struct RangeArgs {
+  const uint8_t* arena;
+  uint64_t arena_bytes;
+  uint16_t node;
+  uint64_t root;
+  const uint64_t* from;
+  const uint64_t* to;
+  uint64_t n;
+  uint64_t* counts;
+  const uint64_t* offsets;  // nullptr -> count only
+  uint64_t* vals;
+  uint32_t* err;
+  // leaf directory (nullable), as in WalkArgs
+  const uint64_t* dir;
+  uint64_t dir_lo;
+  uint64_t dir_n;
+  uint32_t dir_shift;
+};
+void launch_range(const RangeArgs& a, hipStream_t s);
+// out[0] = offsets[n-1] + counts[n-1], out[1] = *err  (n >= 1)
+void launch_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_t n,
+                        const uint32_t* err, uint64_t* out, hipStream_t s);
+// x[i] += c for i < n
+void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 
 }  // namespace dev
 }  // namespace shm

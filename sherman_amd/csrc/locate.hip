@@ -37,22 +37,8 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   if (i >= n) return;
   const uint64_t k = a.keys[i];
   uint64_t ptr = a.root;
-  if (a.dir && a.target_level == 0) {
-    const uint64_t p = (k - a.dir_lo) >> a.dir_shift;
-    if (k >= a.dir_lo && p < a.dir_n) {
-      const u32x4* e = reinterpret_cast<const u32x4*>(a.dir + 8 * p);
-      const u32x4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-      const uint64_t sep1 = (uint64_t)e2.x | ((uint64_t)e2.y << 32);
-      const uint64_t sep2 = (uint64_t)e2.z | ((uint64_t)e2.w << 32);
-      const uint64_t sep3 = (uint64_t)e3.x | ((uint64_t)e3.y << 32);
-      const uint32_t cnt = e3.z;
-      const uint32_t j = (uint32_t)(cnt > 1 && k >= sep1) + (uint32_t)(cnt > 2 && k >= sep2) +
-                         (uint32_t)(cnt > 3 && k >= sep3);
-      const uint32_t lo32 = j == 0 ? e0.x : j == 1 ? e0.z : j == 2 ? e1.x : e1.z;
-      const uint32_t hi32 = j == 0 ? e0.y : j == 1 ? e0.w : j == 2 ? e1.y : e1.w;
-      ptr = (uint64_t)lo32 | ((uint64_t)hi32 << 32);
-    }
-  }
+  if (a.dir && a.target_level == 0)
+    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, k, ptr);
   uint32_t err = 0;
   int retries = 0;
   uint64_t out = 0;

@@ -724,6 +724,7 @@ const char* shm_strerror(int s) {
     case SHM_EIO: return "HIP failure or tree inconsistency";
     case SHM_EAGAIN: return "optimistic check failed";
     case SHM_E2BIG: return "batch larger than max_batch";
+    case SHM_ENOSPC: return "output buffer too small";
     default: return "unknown status";
   }
 }
@@ -967,6 +968,49 @@ int shm_del_batch(shm_tree* t, const uint64_t* keys, uint64_t n, void* stream) {
   return rc;
 }
 
+namespace {
+
+dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to, uint64_t n,
+                          uint64_t* counts, const uint64_t* offsets, uint64_t* vals) {
+  dev::RangeArgs a{};
+  a.arena = t->arena;
+  a.arena_bytes = t->arena_bytes;
+  a.node = t->cfg.node_id;
+  a.root = t->root;
+  a.from = from;
+  a.to = to;
+  a.n = n;
+  a.counts = counts;
+  a.offsets = offsets;
+  a.vals = vals;
+  a.err = t->d_err;
+  if (use_leaf_dir(t)) {
+    a.dir = t->dir;
+    a.dir_lo = t->cfg.key_lo;
+    a.dir_shift = t->cfg.key_bits - t->dir_bits;
+    a.dir_n = 1ull << t->dir_bits;
+  }
+  return a;
+}
+
+// one timed k_range launch
+int range_launch(shm_tree* t, hipStream_t s, const dev::RangeArgs& a) {
+  shm_tree::ProfRec pr{};
+  if (t->prof_on) {
+    const int rc = prof_begin(t, s, shm_tree::kProfRange, a.n, 2, pr);
+    if (rc) return rc;
+  }
+  dev::launch_range(a, s);
+  HIP_OK(hipGetLastError());
+  if (t->prof_on) {
+    HIP_OK(hipEventRecord(pr.e[1], s));
+    t->prof_pending.push_back(pr);
+  }
+  return SHM_OK;
+}
+
+}  // namespace
+
 int shm_range_query(shm_tree* t, const uint64_t* from, const uint64_t* to,
                     uint64_t n, uint64_t* counts_out, const uint64_t* offsets,
                     uint64_t* vals_out, void* stream) {
@@ -974,18 +1018,62 @@ int shm_range_query(shm_tree* t, const uint64_t* from, const uint64_t* to,
   if (offsets && !vals_out) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
-  shm_tree::ProfRec pr{};
-  if (t->prof_on) {
-    const int rc = prof_begin(t, s, shm_tree::kProfRange, n, 2, pr);
+  if (use_leaf_dir(t)) {
+    const int rc = refresh_dir(t, s);
     if (rc) return rc;
   }
-  dev::launch_range_count(t->arena, t->arena_bytes, t->cfg.node_id, t->root,
-                          from, to, n, counts_out, offsets, vals_out, t->d_err, s);
-  HIP_OK(hipGetLastError());
-  if (t->prof_on) {
-    HIP_OK(hipEventRecord(pr.e[1], s));
-    t->prof_pending.push_back(pr);
+  t->err_pending = true;
+  return range_launch(t, s, range_args(t, from, to, n, counts_out, offsets, vals_out));
+}
+
+int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to, uint64_t n,
+                          uint64_t* counts_out, uint64_t* offsets_out, uint64_t* vals_out,
+                          uint64_t vals_cap, uint64_t* total_out, void* stream) {
+  if (!t || !total_out || (n && (!from || !to || !counts_out || !offsets_out))) return SHM_EINVAL;
+  if (vals_cap && !vals_out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(t, stream);
+  *total_out = 0;
+  if (n == 0) return SHM_OK;
+  if (use_leaf_dir(t)) {
+    const int rc = refresh_dir(t, s);
+    if (rc) return rc;
   }
+  // pass 1 per chunk (the scan workspace holds nmax): counts, exclusive scan,
+  // chunk total and error word back in one read
+  uint64_t total = 0;
+  std::vector<uint64_t> base;
+  for (uint64_t off = 0; off < n; off += t->nmax) {
+    const uint64_t m = std::min(t->nmax, n - off);
+    int rc = range_launch(t, s, range_args(t, from + off, to + off, m, counts_out + off,
+                                           nullptr, nullptr));
+    if (rc) return rc;
+    HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, counts_out + off,
+                                   offsets_out + off, m, s));
+    dev::launch_range_total(offsets_out + off, counts_out + off, m, t->d_err,
+                            t->d_counts + 12, s);
+    rc = readback(t, s, t->d_counts + 12, 2 * sizeof(uint64_t));
+    if (rc) return rc;
+    if (t->h_pin[1]) return check_err(t, s);
+    base.push_back(total);
+    total += t->h_pin[0];
+  }
+  t->err_pending = false;
+  *total_out = total;
+  // offsets are chunk-relative until shifted by the totals before them
+  for (size_t c = 1; c < base.size(); ++c) {
+    const uint64_t off = c * t->nmax;
+    dev::launch_add_u64(offsets_out + off, std::min(t->nmax, n - off), base[c], s);
+  }
+  if (total > vals_cap) return SHM_ENOSPC;  // counts / offsets stay valid
+  // pass 2: values
+  for (uint64_t off = 0, c = 0; off < n; off += t->nmax, ++c) {
+    const uint64_t m = std::min(t->nmax, n - off);
+    const int rc = range_launch(t, s, range_args(t, from + off, to + off, m, counts_out + off,
+                                                 offsets_out + off, vals_out));
+    if (rc) return rc;
+  }
+  t->err_pending = true;
   return SHM_OK;
 }
 

@@ -308,77 +308,5 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
   if (n) hipLaunchKernelGGL(k_unpermute, grid1(n), dim3(kT), 0, s, in, perm, n, out);
 }
 
-// ---- batched range scan (intended Tree::range_query, Tree.cpp:461-540) ----
-// One wave per query: descend to the leaf holding `from` (ballot child
-// select), then follow sibling links while the leaf may hold keys <= to,
-// collecting valid entries in slot order.  offsets == nullptr -> count only.
-__global__ __launch_bounds__(kBlock) void k_range(
-    const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
-    const uint64_t* from, const uint64_t* to, uint64_t n, uint64_t* counts,
-    const uint64_t* offsets, uint64_t* vals, uint32_t* err) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_page[kWavesPerBlock][kPageDwords + 8];
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const uint64_t q = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  if (q >= n) return;
-  uint32_t* lp = s_page[wv];
-  const uint64_t lo = from[q], hi = to[q];
-  uint64_t cnt = 0;
-  uint64_t out = offsets ? offsets[q] : 0;
-  if (lo <= hi) {
-    uint64_t p = root;
-    int hops = 0;
-    // descend
-    for (;;) {
-      if (++hops > kMaxRounds || !ptr_ok(p, node, arena_bytes)) {
-        if (lane == 0) atomicOr(err, kErrBadPtr);
-        p = 0;
-        break;
-      }
-      const u32x4 w = load_page_slice(arena, ga_offset(p));
-      const Hdr h = parse_hdr(w);
-      if (lo >= h.highest && h.sibling) {
-        p = h.sibling;
-        continue;
-      }
-      if (h.leftmost == 0) break;
-      const IntRec r = internal_record(w);
-      const int c = popc64(ballot(lane >= 3 && lane - 3 < h.last_index + 1 && r.key <= lo));
-      p = c == 0 ? h.leftmost : rl64(r.ptr, c + 2);
-    }
-    // scan leaves
-    while (p) {
-      if (++hops > (1 << 24) || !ptr_ok(p, node, arena_bytes)) {
-        if (lane == 0) atomicOr(err, kErrBadPtr);
-        break;
-      }
-      const u32x4 w = load_page_slice(arena, ga_offset(p));
-      const Hdr h = parse_hdr(w);
-      stage_page(lp, w);
-      wave_lds_sync();
-      const LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
-      const bool hit = lane < kLeafCardinality && e.val != kValueNull &&
-                       (e.fraw & 0xF) == (e.rraw & 0xF) && e.key >= lo && e.key <= hi;
-      const uint64_t m = ballot(hit);
-      if (offsets && hit) vals[out + cnt + popc64(m & lanemask_lt())] = e.val;
-      cnt += popc64(m);
-      if (h.sibling == 0 || h.highest > hi) break;
-      p = h.sibling;
-      wave_lds_sync();
-    }
-  }
-  if (lane == 0) counts[q] = cnt;
-}
-void launch_range_count(const uint8_t* arena, uint64_t arena_bytes,
-                        uint16_t node, uint64_t root, const uint64_t* from,
-                        const uint64_t* to, uint64_t n, uint64_t* counts,
-                        const uint64_t* offsets, uint64_t* vals, uint32_t* err,
-                        hipStream_t s) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_range, grid1(n, kWavesPerBlock), dim3(kBlock), 0, s,
-                     arena, arena_bytes, node, root, from, to, n, counts,
-                     offsets, vals, err);
-}
-
 }  // namespace dev
 }  // namespace shm

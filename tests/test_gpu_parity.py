@@ -205,8 +205,15 @@ def test_image_conformance_gpu_to_oracle(lib_ok):
     t.close()
 
 
-def test_range_query_vs_oracle(lib_ok):
-    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 17)
+@pytest.mark.parametrize("max_batch,cap,leaf_dir", [(1 << 17, None, True),
+                                                    (128, 16, True),
+                                                    (1 << 17, None, False)])
+def test_range_query_vs_oracle(lib_ok, max_batch, cap, leaf_dir):
+    """Batched scans vs the oracle; (128, 16): scans in chunks of max_batch
+    and a values buffer too small at first (SHM_ENOSPC, then the fill)."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=max_batch, leaf_dir=leaf_dir)
+    if cap is not None:
+        t._rq_cap = cap
     orc = OracleTree(256 << 20)
     ks = hashed_keys(1, 50001)
     gpu_insert(t, ks, ks + U64(9))
