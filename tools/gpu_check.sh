@@ -21,3 +21,6 @@ cat $OUT/bench_c2.json
 timeout -k 10 400 python -u bench.py --workload c3 > $OUT/bench_c3.json 2> $OUT/bench_c3.err \
   || { tail -30 $OUT/bench_c3.err; exit 1; }
 cat $OUT/bench_c3.json
+timeout -k 10 400 python -u bench.py --workload c5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err \
+  || { tail -30 $OUT/bench_c5.err; exit 1; }
+cat $OUT/bench_c5.json
