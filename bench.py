@@ -135,11 +135,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     assert args.workload != "c3" or world == 1, "c3 is a single-GPU config"
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the N > 1 path
+    # on a 1-GPU box with SHM_DIST_BACKEND=gloo) share the GPUs round robin
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        backend = os.environ.get("SHM_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if dist is not None:

@@ -61,7 +61,7 @@ typedef struct shm_config {
   uint16_t node_id;      /* GlobalAddress.nodeID of this shard (= GPU id) */
   uint16_t reserved0;
   uint32_t flags;        /* SHM_FLAG_* */
-  uint64_t arena_bytes;  /* HBM page arena (1 KB pages) */
+  uint64_t arena_bytes;  /* HBM page arena (1 KB pages), at most 4 TB (else SHM_EINVAL) */
   uint64_t max_batch;    /* largest n accepted by a batch call */
   uint32_t num_locks;    /* HBM lock table words (reference: 16384) */
   uint32_t sort_bits;    /* top key bits that order gets: 0 or 16 */

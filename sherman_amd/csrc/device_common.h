@@ -193,25 +193,29 @@ __device__ __forceinline__ void store_page(uint8_t* arena, uint64_t off,
 }
 
 // leaf directory lookup (leafdir.hip): the start page for key k, `fallback`
-// when k is outside the directory.  Entry p = {ptr0..3, sep1..3, count}: the
-// leaves covering prefix p split at sep1..3 (count 0: ptr0 is the deepest
-// internal page covering the prefix).
+// when k is outside the directory.  Entry p is 32 B, u32[8] =
+// {pg0..pg3, t1..t3, count}: the leaves covering prefix p as page indices
+// (GlobalAddress offset / 1 KB) and their split points t_i, the top 32 bits
+// of (sep_i - lo_p) within the prefix (exact when the prefix spans <= 2^32
+// keys); count 0: pg0 is the deepest internal page covering the prefix.
+// Leaf i is taken only when t_i < t(k), which proves k > sep_i; on a tie the
+// walk starts one leaf to the left and moves right (B-link, Tree.cpp:626-629).
 __device__ __forceinline__ uint64_t dir_start(const uint64_t* dir, uint64_t dir_lo,
                                               uint32_t dir_shift, uint64_t dir_n,
-                                              uint64_t k, uint64_t fallback) {
+                                              uint16_t node, uint64_t k, uint64_t fallback) {
   const uint64_t p = (k - dir_lo) >> dir_shift;
   if (k < dir_lo || p >= dir_n || k == kKeyMax) return fallback;
-  const u32x4* e = reinterpret_cast<const u32x4*>(dir + 8 * p);
-  const u32x4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-  const uint64_t sep1 = (uint64_t)e2.x | ((uint64_t)e2.y << 32);
-  const uint64_t sep2 = (uint64_t)e2.z | ((uint64_t)e2.w << 32);
-  const uint64_t sep3 = (uint64_t)e3.x | ((uint64_t)e3.y << 32);
-  const uint32_t cnt = e3.z;
-  const uint32_t i = (uint32_t)(cnt > 1 && k >= sep1) + (uint32_t)(cnt > 2 && k >= sep2) +
-                     (uint32_t)(cnt > 3 && k >= sep3);
-  const uint32_t lo32 = i == 0 ? e0.x : i == 1 ? e0.z : i == 2 ? e1.x : e1.z;
-  const uint32_t hi32 = i == 0 ? e0.y : i == 1 ? e0.w : i == 2 ? e1.y : e1.w;
-  return (uint64_t)lo32 | ((uint64_t)hi32 << 32);
+  const u32x4* e = reinterpret_cast<const u32x4*>(dir + 4 * p);
+  const u32x4 e0 = e[0], e1 = e[1];
+  const uint64_t off = (k - dir_lo) - (p << dir_shift);
+  const bool exact = dir_shift <= 32;
+  const uint32_t tk = exact ? (uint32_t)off : (uint32_t)(off >> (dir_shift - 32));
+  const uint32_t cnt = e1.w;
+  auto past = [&](uint32_t t) { return t < tk || (exact && t == tk); };
+  const uint32_t i = (uint32_t)(cnt > 1 && past(e1.x)) + (uint32_t)(cnt > 2 && past(e1.y)) +
+                     (uint32_t)(cnt > 3 && past(e1.z));
+  const uint32_t pg = i == 0 ? e0.x : i == 1 ? e0.y : i == 2 ? e0.z : e0.w;
+  return dir_page_ga(pg, node);
 }
 
 __device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,

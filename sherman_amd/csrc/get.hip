@@ -83,7 +83,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   uint64_t ptr = a.root;
   if (a.dir) {
     // leaf directory: start at the leaf (or the covering internal page)
-    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, k, ptr);
+    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
   } else if (a.start) {
     ptr = a.start[k >> a.start_shift];
   }
@@ -136,7 +136,10 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
           off = ga_offset(rl64(pload, ctz64(hi)));
           hi &= hi - 1;
         }
-        glds16(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+        if (a.nt)
+          glds16_nt(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+        else
+          glds16(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
       }
     };
 #pragma unroll

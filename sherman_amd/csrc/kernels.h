@@ -34,6 +34,8 @@ struct WalkArgs {
   uint32_t dir_shift;
   // GET: map blocks to chunks XCD-contiguously (see get.hip)
   int xcd_remap;
+  // GET: page DMAs with the non-temporal policy (nt; streamed once per batch)
+  int nt;
   // diagnostics (nullable): per wave {start, end} s_memrealtime stamps
   uint64_t* stamps;
 };

@@ -60,6 +60,11 @@ SHM_HD uint64_t ga_make(uint16_t node, uint64_t off) {
 }
 SHM_HD uint64_t ga_offset(uint64_t ga) { return ga >> 16; }
 SHM_HD uint16_t ga_node(uint64_t ga) { return (uint16_t)(ga & 0xFFFF); }
+// leaf-directory page index <-> GlobalAddress (1 KB pages, offset < 4 TB)
+SHM_HD uint64_t dir_page_ga(uint32_t pg, uint16_t node) {
+  return ((uint64_t)pg << 26) | (uint64_t)node;
+}
+SHM_HD uint32_t dir_page_index(uint64_t ga) { return (uint32_t)(ga_offset(ga) >> 10); }
 
 // Superblock in page 0 of the arena (offset 0 is Null, like chunk 0 in
 // GlobalAllocator.h:24-26); it plays the role of root_ptr_ptr

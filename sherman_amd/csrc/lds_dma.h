@@ -23,6 +23,18 @@ __device__ __forceinline__ void glds16(const uint8_t* page, uint32_t lds_addr) {
       : "memory", "m0");
 }
 
+// the same with the non-temporal policy: a leaf read once per batch should
+// not displace the lines that are reused (directory, upper levels)
+__device__ __forceinline__ void glds16_nt(const uint8_t* page, uint32_t lds_addr) {
+  const uint64_t ga = (uint64_t)(page + 16 * lane_id());
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "global_load_lds_dwordx4 %0, off nt"
+      :
+      : "v"(ga), "s"(lds_addr)
+      : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -4,12 +4,15 @@
 // CacheEntry.h: cached level-1 pages let a search jump straight to its leaf;
 // dead in the reference fork, Directory.cpp:8/77-79) for the batched get.
 // Entry p covers keys [lo_p, lo_p + 2^shift), lo_p = dir_lo + (p << shift),
-// and lists the up to four leaves that cover that range, in key order:
-//   u64[8] = {ptr0, ptr1, ptr2, ptr3, sep1, sep2, sep3, n}
-// with sep_i = lowest fence of ptr_i; a query k starts at ptr_i for the
-// largest i < n with sep_i <= k.  n == 0 marks a prefix spanning more than
-// four leaves: ptr0 is then the deepest internal page whose fences cover the
-// whole prefix.
+// and lists the up to four leaves that cover that range, in key order, in
+// 32 B (four entries per 128 B L2 line):
+//   u32[8] = {pg0, pg1, pg2, pg3, t1, t2, t3, n}
+// pg_i = page index of leaf i (GlobalAddress offset / 1 KB), t_i = the top
+// 32 bits of (sep_i - lo_p) with sep_i = lowest fence of leaf i (all of it
+// when shift <= 32).  A query k starts at leaf i for the largest i < n whose
+// t_i is below k's (dir_start, device_common.h).  n == 0 marks a prefix
+// spanning more than four leaves: pg0 is then the deepest internal page whose
+// fences cover the whole prefix.
 //
 // Stale entries stay correct: a page's lowest fence never changes (a split
 // keeps the left half in place, Tree.cpp:926-945), so ptr_i remains a valid
@@ -107,11 +110,15 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
     for (int i = 0; i < 8; ++i) out[i] = 0;
     out[0] = root;
   }
-  u32x4* e = reinterpret_cast<u32x4*>(dir + 8 * p);
+  // out = {ptr0..3, sep1..3, n} -> the 32 B entry
+  const uint32_t sh = shift > 32 ? shift - 32 : 0;
+  uint32_t t[3];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    e[i] = u32x4{(uint32_t)out[2 * i], (uint32_t)(out[2 * i] >> 32), (uint32_t)out[2 * i + 1],
-                 (uint32_t)(out[2 * i + 1] >> 32)};
+  for (int i = 0; i < 3; ++i) t[i] = (uint32_t)((out[4 + i] - lo) >> sh);
+  u32x4* e = reinterpret_cast<u32x4*>(dir + 4 * p);
+  e[0] = u32x4{dir_page_index(out[0]), dir_page_index(out[1]), dir_page_index(out[2]),
+               dir_page_index(out[3])};
+  e[1] = u32x4{t[0], t[1], t[2], (uint32_t)out[7]};
 }
 
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   const uint64_t k = a.keys[i];
   uint64_t ptr = a.root;
   if (a.dir && a.target_level == 0)
-    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, k, ptr);
+    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
   uint32_t err = 0;
   int retries = 0;
   uint64_t out = 0;

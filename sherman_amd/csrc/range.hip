@@ -30,7 +30,7 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
   const uint64_t out = a.offsets ? a.offsets[q] : 0;
   uint32_t err = 0;
   if (lo <= hi) {
-    uint64_t p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, lo, a.root) : a.root;
+    uint64_t p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
     int hops = 0;
     u32x4 w;
     // descend to the leaf whose fences hold lo

@@ -84,7 +84,7 @@ struct shm_tree {
   // search when pages were added or the root moved since it was built
   uint64_t* start = nullptr;
   uint64_t start_np = ~0ull, start_root = ~0ull;
-  // leaf directory (leafdir.hip): 2^dir_bits entries of 64 B over the whole
+  // leaf directory (leafdir.hip): 2^dir_bits entries of 32 B over the whole
   // key space, rebuilt before a search once the tree grew by 1/32 since the
   // last build (stale entries only cost B-link right moves)
   bool err_pending = false;  // kernels ran since d_err was last read back
@@ -147,6 +147,17 @@ bool get_kernel_v4() {
     return e && strcmp(e, "walk") == 0;
   }();
   return v4;
+}
+
+// SHM_WALK_NT=0/1: leaf-page DMAs of the get walk with the default or the
+// non-temporal cache policy (A/B knob; default 1: a leaf is read once per
+// batch, and nt keeps it from displacing the directory: C2 +5 %)
+int walk_nt() {
+  static const int v = [] {
+    const char* e = getenv("SHM_WALK_NT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 // SHM_GET_STAMPS=<file>: append the per-wave {start, end} s_memrealtime
@@ -221,7 +232,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
       HIP_OK(hipFree(t->dir));
       t->dir = nullptr;
     }
-    if (dalloc(&t->dir, 8ull << bits)) return SHM_ENOMEM;
+    if (dalloc(&t->dir, 4ull << bits)) return SHM_ENOMEM;  // 32 B per entry
     t->dir_bits = bits;
   }
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
@@ -747,7 +758,9 @@ int shm_config_init(shm_config* c) {
 
 int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (!cfg || !out || cfg->struct_size != sizeof(shm_config)) return SHM_EINVAL;
-  if (cfg->arena_bytes < 4 * kPageSize || cfg->max_batch == 0 ||
+  // arena < 4 TB: the leaf directory holds 32-bit page indices
+  if (cfg->arena_bytes < 4 * kPageSize || cfg->arena_bytes > (1ull << 42) ||
+      cfg->max_batch == 0 ||
       cfg->max_batch > (1ull << 31) || cfg->num_locks == 0 ||
       (cfg->sort_bits != 0 && cfg->sort_bits != kDefaultSortBits) || cfg->key_bits > 64)
     return SHM_EINVAL;
@@ -909,6 +922,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.keys = keys + off;
       a.perm = nullptr;
     }
+    a.nt = walk_nt();
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
     if (get_kernel_v4()) {
       dev::launch_walk(a, m, kWalkDepth, false, s);
