@@ -69,8 +69,9 @@ def parse():
                    help="c5: expected stored keys per range scan")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0)
-    p.add_argument("--sort", action="store_true",
-                   help="order each get batch by key before the walk (SHM_FLAG_SORT_GETS)")
+    p.add_argument("--sort", choices=("auto", "on", "off"), default="auto",
+                   help="order get batches by key before the walk: always "
+                        "(SHM_FLAG_SORT_GETS), never, or when dense (default)")
     p.add_argument("--profile-steps", type=int, default=10)
     p.add_argument("--sim-world", type=int, default=1,
                    help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
@@ -163,7 +164,7 @@ def main():
     key_lo, key_bits = (0, 64) if args.no_range_hint else shard_range(s_rank, s_world)
     # N > 1: a rank receives ~batch routed keys (+ a few %), keep one chunk
     tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch + (batch >> 2 if world > 1 else 0)), device=local,
-                    node_id=rank, sort_gets=args.sort, key_lo=key_lo, key_bits=key_bits)
+                    node_id=rank, sort_gets={"on": True, "off": False}.get(args.sort, "auto"), key_lo=key_lo, key_bits=key_bits)
 
     t0 = time.time()
     keys_local, inserted = build_shard(tree, n_keys, s_world, s_rank, dev)
@@ -357,7 +358,7 @@ def main():
                 "batch_per_gpu": batch,
                 "tree_height": st["height"],
                 "pages": st["pages_used"],
-                "sorted_gets": args.sort,
+                "get_order": args.sort,
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
                 "splits_in_timed_steps": st_end["splits"] - splits0,

@@ -52,6 +52,9 @@ extern "C" {
 #define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key before the walk */
 #define SHM_FLAG_LEAF_DIR 0x2u   /* start gets / leaf locates at the leaf
                                     directory (default on) */
+#define SHM_FLAG_AUTO_SORT_GETS 0x4u /* reorder a get batch by key when it is
+                                    dense enough that queries share leaves
+                                    (>= 0.4 queries per page; default on) */
 
 typedef struct shm_tree shm_tree;
 

@@ -26,6 +26,7 @@ SHM_E2BIG = -7
 SHM_ENOSPC = -28
 SHM_FLAG_SORT_GETS = 0x1
 SHM_FLAG_LEAF_DIR = 0x2
+SHM_FLAG_AUTO_SORT_GETS = 0x4
 
 KEY_MAX = (1 << 64) - 1
 PAGE_SIZE = 1024
@@ -177,7 +178,7 @@ class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
-                 node_id=0, sort_gets=False, num_locks=None, sort_bits=16,
+                 node_id=0, sort_gets="auto", num_locks=None, sort_bits=16,
                  key_lo=0, key_bits=64, leaf_dir=True):
         L = lib()
         cfg = ShmConfig()
@@ -191,7 +192,10 @@ class Tree:
         cfg.sort_bits = sort_bits
         cfg.key_lo = key_lo
         cfg.key_bits = key_bits
-        cfg.flags = ((SHM_FLAG_SORT_GETS if sort_gets else 0) |
+        # sort_gets: True (always order get batches by key), False (never),
+        # "auto" (order dense batches, SHM_FLAG_AUTO_SORT_GETS)
+        cfg.flags = ((SHM_FLAG_SORT_GETS if sort_gets is True else 0) |
+                     (SHM_FLAG_AUTO_SORT_GETS if sort_gets == "auto" else 0) |
                      (SHM_FLAG_LEAF_DIR if leaf_dir else 0))
         h = vp()
         _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")

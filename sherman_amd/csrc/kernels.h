@@ -127,7 +127,7 @@ uint32_t partition_chunk_slots(uint64_t n);
 // [key_lo, key_lo + 2^key_bits) (keys outside clamp to the first/last bucket)
 void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
                       uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
-                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s);
+                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, bool direct, hipStream_t s);
 // insert ordering, step 2: the coarse pass alone over per-group
 // de-duplicated runs (group gi = keys [gi * 4096, ...) holds gcount[gi]
 // keys), carrying a u32 payload; bins = 2 x 256 words of (start, count)

@@ -18,6 +18,9 @@
 //   fine           : one block per <= kFineCap-key chunk of a coarse bin:
 //                    counting sort on the next 8 bits inside the chunk's own
 //                    range -> keys_out[p], src[p] = keys1 slot it came from
+//                    (direct mode: the coarse pass carries each key's input
+//                    index instead of writing pos1, src[p] = that index, the
+//                    walk stores results in input order, no unpartition)
 //   (walk)         : result of slot p stored at vals1[src[p]] — a scatter
 //                    confined to the chunk's range, which stays in L2
 //   unpartition    : out[i] = vals1[pos1[i]], found[i] = out[i] != 0
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
       if (part_valid(i, n, gcount)) {
         const uint32_t b = coarse_of(k[r], kr);
         stage[lex[b] + rank[r]] = k[r];
-        if (pay_in) pstage[lex[b] + rank[r]] = pay_in[i];
+        if (pay1) pstage[lex[b] + rank[r]] = pay_in ? pay_in[i] : (uint32_t)i;
         if (pos1) pos1[i] = gbase[b] + rank[r];  // coalesced in i
       }
     }
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
   }
 }
 
-__global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ keys1, KeyRange kr,
+__global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ keys1,
+                                                   const uint32_t* __restrict__ pay1, KeyRange kr,
                                                    const uint32_t* __restrict__ chunks,
                                                    uint32_t* __restrict__ S,
                                                    uint64_t* __restrict__ keys_out,
@@ -258,10 +262,13 @@ __global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ 
   if (ch.len == 0) return;  // block-uniform: grid sized for the worst case
   if (t < kFine) h[t] = 0;
   uint64_t k[kFinePer];
+  uint32_t pl[kFinePer];
 #pragma unroll
   for (int r = 0; r < kFinePer; ++r) {
     const uint32_t o = (uint32_t)(r * kPT + t);
     k[r] = o < ch.len ? keys1[ch.start + o] : 0;
+    pl[r] = (uint32_t)ch.start + o;
+    if (pay1 && o < ch.len) pl[r] = pay1[ch.start + o];
   }
   __syncthreads();
   uint32_t rank[kFinePer];
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(kPT) void k_part_fine(const uint64_t* __restrict__ 
     if (o < ch.len) {
       const uint32_t lp = h[fine_of(k[r], kr)] + rank[r];
       stage[lp] = k[r];
-      sq[lp] = (uint32_t)ch.start + o;
+      sq[lp] = pl[r];
     }
   }
   __syncthreads();
@@ -325,7 +332,8 @@ uint32_t partition_chunk_slots(uint64_t n) {
 
 void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
                       uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
-                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s) {
+                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, bool direct,
+                      hipStream_t s) {
   if (!n) return;
   const KeyRange kr{key_lo, key_bits};
   const uint64_t all_groups = (n + kGrpKeys - 1) / kGrpKeys;
@@ -336,9 +344,11 @@ void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_
                      (const uint32_t*)nullptr, groups, M, S);
   hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, groups, tiles,
-                     (const uint32_t*)M, (const uint32_t*)S, keys1, (uint32_t*)nullptr, pos1,
+                     (const uint32_t*)M, (const uint32_t*)S, keys1,
+                     direct ? pos1 : (uint32_t*)nullptr, direct ? (uint32_t*)nullptr : pos1,
                      chunks, slots, (uint32_t*)nullptr);
-  hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1, kr,
+  hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1,
+                     direct ? (const uint32_t*)pos1 : (const uint32_t*)nullptr, kr,
                      (const uint32_t*)chunks, S, keys_out, src);
 }
 

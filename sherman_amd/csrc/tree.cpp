@@ -160,6 +160,16 @@ int walk_nt() {
   return v;
 }
 
+// SHM_GET_DIRECT=1: ordered gets carry each query's input index through the
+// partition and the walk stores results in input order (no unpartition pass)
+bool get_direct() {
+  static const bool v = [] {
+    const char* e = getenv("SHM_GET_DIRECT");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 // SHM_GET_STAMPS=<file>: append the per-wave {start, end} s_memrealtime
 // stamps (100 MHz) of every get walk launch to <file> (diagnostics only;
 // synchronises the stream after each launch).
@@ -746,7 +756,7 @@ int shm_config_init(shm_config* c) {
   c->struct_size = sizeof(shm_config);
   c->device = 0;
   c->node_id = 0;
-  c->flags = SHM_FLAG_LEAF_DIR;
+  c->flags = SHM_FLAG_LEAF_DIR | SHM_FLAG_AUTO_SORT_GETS;
   c->arena_bytes = 1ull << 30;
   c->max_batch = 1ull << 20;
   c->num_locks = 1u << 22;  // 32 MB: rare false sharing between waves
@@ -857,7 +867,12 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   hipStream_t s = pick(t, stream);
   // start pages: the leaf directory (any batch), else for ordered batches
   // the prefix start table, else the root
-  const bool ordered = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
+  // Ordering pays when queries share leaves: a batch of q uniform queries
+  // over L leaves reads L(1 - e^(-q/L)) of them sorted, q unsorted (C2, q/L
+  // 0.58: 24 % fewer page reads for ~35 us of partition + gather, +4 %; C3's
+  // get half, q/L 0.29: 13 % fewer, -3 %).  Auto mode orders at q/L >= 0.4.
+  const bool dense = (t->cfg.flags & SHM_FLAG_AUTO_SORT_GETS) && 5 * n >= 2 * t->next_page;
+  const bool ordered = ((t->cfg.flags & SHM_FLAG_SORT_GETS) || dense) && n >= kSortMinGets;
   const bool dir = use_leaf_dir(t);
   if (dir) {
     const int rc = refresh_dir(t, s);
@@ -885,14 +900,17 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       // walked by the same wave (one page read per group, not per query)
       // (keys1 = kb, pos1 = ia, walk order = ka, src = ib); the walk stores
       // result p at vals1[src[p]] (kb, inside p's chunk), unpartition gathers
+      const bool direct = get_direct();
       dev::launch_partition(keys + off, m, t->cfg.key_lo, t->cfg.key_bits, t->part_hist,
                             t->part_S, t->part_chunks,
                             t->kb, t->ia,
-                            t->ka, t->ib, s);
+                            t->ka, t->ib, direct, s);
       a.keys = t->ka;
       a.perm = t->ib;
-      a.out_val = t->kb;
-      a.out_found = nullptr;
+      if (!direct) {  // else results go straight to input order (ib = input index)
+        a.out_val = t->kb;
+        a.out_found = nullptr;
+      }
       a.xcd_remap = getenv("SHM_XCD_REMAP") ? atoi(getenv("SHM_XCD_REMAP")) : 1;
       if (dir) {
         a.dir = t->dir;
@@ -903,7 +921,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
         a.start = t->start;
         a.start_shift = 64 - start_bits();
       }
-      gathered = true;
+      gathered = !direct;
       DBG(s, "sort(get)");
     } else if (dir) {
       // unordered (default): every wave sorts its own 64 keys and starts at
