@@ -225,6 +225,25 @@ __device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,
          off >= kPageSize && off + kPageSize <= arena_bytes;
 }
 
+// a key's offset in the shard range [lo, lo + 2^bits), scaled to 64 bits
+// (clamped outside the range): the ordering key of both passes
+struct KeyRange {
+  uint64_t lo;
+  uint32_t bits;
+};
+__device__ __forceinline__ uint64_t rel_key(uint64_t k, KeyRange r) {
+  if (r.bits >= 64) return k;
+  if (k < r.lo) return 0;
+  const uint64_t d = k - r.lo;
+  return (d >> r.bits) ? ~0ull : d << (64 - r.bits);
+}
+__device__ __forceinline__ uint32_t coarse_of(uint64_t k, KeyRange r) {
+  return (uint32_t)(rel_key(k, r) >> 56);
+}
+__device__ __forceinline__ uint32_t fine_of(uint64_t k, KeyRange r) {
+  return (uint32_t)(rel_key(k, r) >> 48) & 0xFF;
+}
+
 // in-wave ascending bitonic sort of (key, tag) over 64 lanes; branch-free
 // compare-exchange (xor shuffles with constant masks)
 __device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& tag) {

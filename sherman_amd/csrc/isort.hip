@@ -181,6 +181,223 @@ __global__ __launch_bounds__(kIT) void k_bin_sort(uint64_t* __restrict__ keys1,
   }
 }
 
+// ---- step 3 + 4 without the library scan: per-bin dedup, sort, emit --------
+//
+// k_bin_unique, one block per coarse bin (<= kUniqCap ops):
+//   a. LDS hash table of the bin's keys keeping each key's last op (atomic
+//      max of the op index); a key lives in exactly one bin, so the
+//      survivors are the batch's last writers (Tree.cpp:878-889 applied in
+//      batch order leaves exactly these);
+//   b. counting sort of the survivors by the next 8 key bits (the bin's
+//      keys share the top 8 bits of their offset in the shard range);
+//   c. two passes of in-register wave sorts over 64-key windows, the second
+//      offset by 32: a sub-bucket of <= 32 keys lies inside one window of
+//      one of the passes, and windows never reorder keys across sub-buckets,
+//      so the bin ends fully sorted.  A sub-bucket > 32 (skewed keys) sorts
+//      the whole bin with the LDS bitonic network instead;
+//   d. each survivor's value classifies it as an upsert or a delete (value 0
+//      = kValueNull, Tree.cpp:881); local ranks by one block scan.
+// Survivors go back to the bin's slots of keys1 / pay1 (op index), their
+// local rank to lrank (bit 31 = delete), the bin's (upserts, deletes) to
+// bcnt.  k_bin_emit then places every bin at its prefix: uk / uv (upserts,
+// key order) and dk (deletes), totals in counts[0..1].
+constexpr int kUniqSlots = 8192;  // LDS hash slots (96 KB with the op indices)
+constexpr int kUniqCap = 6144;    // ops per bin handled here (load <= 0.75)
+constexpr int kUniqPer = kUniqCap / kIT;
+
+__global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1,
+                                                   uint32_t* __restrict__ pay1,
+                                                   const uint32_t* __restrict__ bins,
+                                                   KeyRange kr,
+                                                   const uint64_t* __restrict__ vals,
+                                                   uint32_t* __restrict__ lrank,
+                                                   uint32_t* __restrict__ bcnt,
+                                                   uint32_t* __restrict__ S, uint32_t* err) {
+  constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
+  __shared__ unsigned long long hkey[kUniqSlots];  // hash, then the sorted keys
+  __shared__ uint32_t hidx[kUniqSlots];            // 1 + op index, then op index
+  __shared__ uint32_t hist[kFine];
+  __shared__ uint32_t wsum[kIT / kWave];
+  __shared__ uint32_t s_big;
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const uint32_t b = blockIdx.x;
+  // the coarse pass is complete: clear its group sums for the next batch
+  if (b == 0)
+    for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
+  const uint32_t start = bins[2 * b], cnt = bins[2 * b + 1];
+  if (cnt > (uint32_t)kUniqCap) {  // block-uniform
+    if (t == 0) {
+      atomicOr(err, kErrSortOverflow);  // the host re-orders with rocPRIM
+      bcnt[2 * b] = bcnt[2 * b + 1] = 0;
+    }
+    return;
+  }
+  // a. last writer per key
+#pragma unroll
+  for (int r = 0; r < SPT; ++r) {
+    hkey[r * kIT + t] = kKeyMax;  // kKeyMax is never a stored key
+    hidx[r * kIT + t] = 0;
+  }
+  if (t < kFine) hist[t] = 0;
+  if (t == 0) s_big = 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kUniqPer; ++r) {
+    const uint32_t o = (uint32_t)(r * kIT + t);
+    if (o >= cnt) continue;
+    const uint64_t k = keys1[start + o];
+    const uint32_t ix = pay1[start + o];
+    uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 51) & (kUniqSlots - 1);
+    for (int probe = 0; probe < kUniqSlots; ++probe) {
+      const unsigned long long old = atomicCAS(&hkey[h], (unsigned long long)kKeyMax,
+                                               (unsigned long long)k);
+      if (old == kKeyMax || old == k) {
+        atomicMax(&hidx[h], ix + 1u);
+        break;
+      }
+      h = (h + 1) & (kUniqSlots - 1);
+    }
+  }
+  __syncthreads();
+  // b. survivors (this thread's SPT slots) ranked by the fine digit
+  uint64_t sk[SPT];
+  uint32_t si[SPT], rk[SPT];
+#pragma unroll
+  for (int r = 0; r < SPT; ++r) {
+    sk[r] = hkey[SPT * t + r];
+    si[r] = hidx[SPT * t + r] - 1u;
+    rk[r] = sk[r] != kKeyMax ? atomicAdd(&hist[fine_of(sk[r], kr)], 1u) : 0u;
+  }
+  __syncthreads();
+  const uint32_t hc = t < kFine ? hist[t] : 0u;
+  if (hc > 32) s_big = 1;
+  uint32_t u;
+  const uint32_t hex = block_scan(hc, wsum, &u);  // ends with a barrier
+  if (t < kFine) hist[t] = hex;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SPT; ++r) {
+    if (sk[r] != kKeyMax) {
+      const uint32_t p = hist[fine_of(sk[r], kr)] + rk[r];
+      hkey[p] = sk[r];
+      hidx[p] = si[r];
+    }
+  }
+  __syncthreads();
+  // c. finish the order
+  if (!s_big) {
+    for (int pass = 0; pass < 2; ++pass) {
+      const uint32_t off = pass ? 32u : 0u;
+      for (uint32_t w0 = off + 64u * (uint32_t)wv; w0 < u; w0 += 64u * (kIT / kWave)) {
+        const uint32_t o = w0 + (uint32_t)lane;
+        uint64_t k = o < u ? hkey[o] : kKeyMax;
+        uint32_t ix = o < u ? hidx[o] : ~0u;
+        wave_sort64(k, ix);
+        if (o < u) {
+          hkey[o] = k;
+          hidx[o] = ix;
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    uint32_t m = 2;
+    while (m < u) m <<= 1;
+    for (uint32_t o = u + (uint32_t)t; o < m; o += kIT) {
+      hkey[o] = kKeyMax;
+      hidx[o] = ~0u;
+    }
+    __syncthreads();
+    lds_bitonic<kUniqSlots / kIT>(reinterpret_cast<uint64_t*>(hkey), hidx, m);
+  }
+  // d. classify and rank: thread t owns survivors [E t, E t + E)
+  constexpr int E = (kUniqCap + kIT - 1) / kIT;
+  const uint32_t o0 = (uint32_t)(E * t);
+  uint32_t isdel = 0, nloc = 0;  // bit r: survivor o0 + r is a delete
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t o = o0 + (uint32_t)r;
+    if (o < u) {
+      const uint64_t k = hkey[o];
+      const uint32_t ix = hidx[o];
+      keys1[start + o] = k;
+      pay1[start + o] = ix;
+      if (vals[ix] == kValueNull) isdel |= 1u << r;
+      ++nloc;
+    }
+  }
+  const uint32_t ndl = (uint32_t)__builtin_popcount(isdel);
+  // one scan of (upserts << 16 | deletes): a bin holds <= 6144 survivors
+  uint32_t tot;
+  const uint32_t ex = block_scan(((nloc - ndl) << 16) | ndl, wsum, &tot);
+  uint32_t ru = ex >> 16, rd = ex & 0xFFFF;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t o = o0 + (uint32_t)r;
+    if (o < u) lrank[start + o] = (isdel >> r) & 1u ? (0x80000000u | rd++) : ru++;
+  }
+  if (t == 0) {
+    bcnt[2 * b] = tot >> 16;
+    bcnt[2 * b + 1] = tot & 0xFFFF;
+  }
+}
+
+// place every bin's survivors at its prefix over the earlier bins
+__global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ keys1,
+                                                 const uint32_t* __restrict__ pay1,
+                                                 const uint32_t* __restrict__ lrank,
+                                                 const uint32_t* __restrict__ bins,
+                                                 const uint32_t* __restrict__ bcnt,
+                                                 const uint64_t* __restrict__ vals,
+                                                 uint64_t* __restrict__ uk,
+                                                 uint64_t* __restrict__ uv,
+                                                 uint64_t* __restrict__ dk,
+                                                 uint64_t* __restrict__ counts) {
+  __shared__ uint32_t su[4], sd[4];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  // prefix over bins < b (and the totals): thread t holds bin t
+  uint32_t cu = bcnt[2 * t], cd = bcnt[2 * t + 1];
+  uint32_t pu = (uint32_t)t < b ? cu : 0u, pd = (uint32_t)t < b ? cd : 0u;
+  for (int off = 32; off > 0; off >>= 1) {
+    pu += (uint32_t)__shfl_xor((int)pu, off);
+    pd += (uint32_t)__shfl_xor((int)pd, off);
+    cu += (uint32_t)__shfl_xor((int)cu, off);
+    cd += (uint32_t)__shfl_xor((int)cd, off);
+  }
+  if (lane_id() == 0) {
+    su[t >> 6] = pu;
+    sd[t >> 6] = pd;
+  }
+  __syncthreads();
+  const uint32_t bu = su[0] + su[1] + su[2] + su[3];
+  const uint32_t bd = sd[0] + sd[1] + sd[2] + sd[3];
+  if (b == gridDim.x - 1) {
+    __syncthreads();
+    if (lane_id() == 0) {
+      su[t >> 6] = cu;
+      sd[t >> 6] = cd;
+    }
+    __syncthreads();
+    if (t == 0) {
+      counts[0] = (uint64_t)su[0] + su[1] + su[2] + su[3];
+      counts[1] = (uint64_t)sd[0] + sd[1] + sd[2] + sd[3];
+    }
+  }
+  const uint32_t start = bins[2 * b];
+  const uint32_t u = bcnt[2 * b] + bcnt[2 * b + 1];
+  for (uint32_t o = (uint32_t)t; o < u; o += 256) {
+    const uint32_t r = lrank[start + o];
+    const uint64_t k = keys1[start + o];
+    if (r & 0x80000000u) {
+      dk[bd + (r & 0x7FFFFFFFu)] = k;
+    } else {
+      uk[bu + r] = k;
+      uv[bu + r] = vals[pay1[start + o]];
+    }
+  }
+}
+
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, hipStream_t s) {
   if (!n) return;
@@ -191,6 +408,18 @@ void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uin
 void launch_bin_sort(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint32_t* S,
                      uint32_t* err, hipStream_t s) {
   hipLaunchKernelGGL(k_bin_sort, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, S, err);
+}
+
+void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
+                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
+                       uint64_t* uk, uint64_t* uv, uint64_t* dk, uint64_t* counts, uint32_t* S,
+                       uint32_t* err, hipStream_t s) {
+  const KeyRange kr{key_lo, key_bits};
+  hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
+                     lrank, bcnt, S, err);
+  hipLaunchKernelGGL(k_bin_emit, dim3(kCoarse), dim3(256), 0, s, (const uint64_t*)keys1,
+                     (const uint32_t*)pay1, (const uint32_t*)lrank, bins,
+                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts);
 }
 
 }  // namespace dev

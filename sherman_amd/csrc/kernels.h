@@ -146,6 +146,14 @@ void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uin
                        uint32_t* gcount, uint32_t* err, hipStream_t s);
 void launch_bin_sort(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint32_t* S,
                      uint32_t* err, hipStream_t s);
+// steps 3-4 in two launches: per-bin last-writer dedup + sort (<= 6144 ops
+// per bin, else kErrSortOverflow), then uk / uv / dk at the bins' prefixes
+// and (upserts, deletes) in counts[0..1]; bcnt = 2 x 256 words, lrank = one
+// u32 per op
+void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
+                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
+                       uint64_t* uk, uint64_t* uv, uint64_t* dk, uint64_t* counts, uint32_t* S,
+                       uint32_t* err, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);

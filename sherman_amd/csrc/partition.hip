@@ -43,25 +43,6 @@ static_assert(kFinePer * kPT == kFineCap, "fine cap");
 static_assert(kGrpKeys == kIsortTile, "insert tiles are the coarse pass's groups");
 static_assert(kCoarse == 256 && kFine == 256, "bin code assumes 256 bins");
 
-// a key's offset in the shard range [lo, lo + 2^bits), scaled to 64 bits
-// (clamped outside the range): the ordering key of both passes
-struct KeyRange {
-  uint64_t lo;
-  uint32_t bits;
-};
-__device__ __forceinline__ uint64_t rel_key(uint64_t k, KeyRange r) {
-  if (r.bits >= 64) return k;
-  if (k < r.lo) return 0;
-  const uint64_t d = k - r.lo;
-  return (d >> r.bits) ? ~0ull : d << (64 - r.bits);
-}
-__device__ __forceinline__ uint32_t coarse_of(uint64_t k, KeyRange r) {
-  return (uint32_t)(rel_key(k, r) >> 56);
-}
-__device__ __forceinline__ uint32_t fine_of(uint64_t k, KeyRange r) {
-  return (uint32_t)(rel_key(k, r) >> 48) & 0xFF;
-}
-
 // Exclusive scan of v over threads 0..255 of the block (others pass 0 and get
 // garbage).  Every thread of the block calls it; it ends with a barrier, so
 // `wsum` may be reused by the next call.

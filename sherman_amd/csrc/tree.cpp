@@ -160,6 +160,16 @@ int walk_nt() {
   return v;
 }
 
+// SHM_BIN_UNIQUE=0 orders insert batches with the per-bin bitonic sort and
+// the mark / scan / compact passes instead of k_bin_unique (A/B knob)
+bool bin_unique() {
+  static const bool v = [] {
+    const char* e = getenv("SHM_BIN_UNIQUE");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return v;
+}
+
 // SHM_GET_DIRECT=1: ordered gets carry each query's input index through the
 // partition and the walk stores results in input order (no unpartition pass)
 bool get_direct() {
@@ -491,6 +501,16 @@ int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint
     dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, s);
     dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
                                  t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
+    if (bin_unique()) {
+      // per-bin dedup + sort + emit: uk / uv / dk and the counts directly
+      dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals,
+                             t->ia, t->bins + 2 * dev::kCoarse, t->uk, t->uv, t->dk,
+                             t->d_counts, t->part_S, t->d_err, s);
+      DBG(s, "bin_unique");
+      HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
+      t->err_pending = false;
+      return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
+    }
     dev::launch_bin_sort(t->ka, t->ib, t->bins, t->part_S, t->d_err, s);
     bins = t->bins;
     DBG(s, "sort(insert, fast)");
@@ -827,7 +847,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   rc |= dalloc(&t->start, 1ull << start_bits());
   rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
-  rc |= dalloc(&t->bins, 2 * dev::kCoarse);
+  rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count), then (upserts, deletes)
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
