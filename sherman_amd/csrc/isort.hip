@@ -352,7 +352,8 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
                                                  uint64_t* __restrict__ uk,
                                                  uint64_t* __restrict__ uv,
                                                  uint64_t* __restrict__ dk,
-                                                 uint64_t* __restrict__ counts) {
+                                                 uint64_t* __restrict__ counts,
+                                                 const uint32_t* __restrict__ err) {
   __shared__ uint32_t su[4], sd[4];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
@@ -382,6 +383,7 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
     if (t == 0) {
       counts[0] = (uint64_t)su[0] + su[1] + su[2] + su[3];
       counts[1] = (uint64_t)sd[0] + sd[1] + sd[2] + sd[3];
+      counts[2] = *err;  // set by k_tile_dedup / k_bin_unique, read back with the counts
     }
   }
   const uint32_t start = bins[2 * b];
@@ -419,7 +421,7 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                      lrank, bcnt, S, err);
   hipLaunchKernelGGL(k_bin_emit, dim3(kCoarse), dim3(256), 0, s, (const uint64_t*)keys1,
                      (const uint32_t*)pay1, (const uint32_t*)lrank, bins,
-                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts);
+                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts, (const uint32_t*)err);
 }
 
 }  // namespace dev

@@ -148,7 +148,7 @@ void launch_bin_sort(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint
                      uint32_t* err, hipStream_t s);
 // steps 3-4 in two launches: per-bin last-writer dedup + sort (<= 6144 ops
 // per bin, else kErrSortOverflow), then uk / uv / dk at the bins' prefixes
-// and (upserts, deletes) in counts[0..1]; bcnt = 2 x 256 words, lrank = one
+// and (upserts, deletes, error word) in counts[0..2]; bcnt = 2 x 256 words, lrank = one
 // u32 per op
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
@@ -206,11 +206,19 @@ struct RangeArgs {
   uint64_t dir_lo;
   uint64_t dir_n;
   uint32_t dir_shift;
+  // staging (nullable): the count pass also keeps up to stage_cap values of
+  // scan q at stage[q * stage_cap]; the fill pass copies those scans from
+  // there instead of walking their leaves again
+  uint64_t* stage;
+  uint32_t stage_cap;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // out[0] = offsets[n-1] + counts[n-1], out[1] = *err  (n >= 1)
 void launch_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_t n,
                         const uint32_t* err, uint64_t* out, hipStream_t s);
+// dst[i] = *s_i (one launch instead of four device-to-device copies)
+void launch_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
+                        const uint32_t* s2, const uint32_t* s3, hipStream_t s);
 // x[i] += c for i < n
 void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 

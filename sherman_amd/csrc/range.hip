@@ -2,6 +2,9 @@
 // (src/Tree.cpp:461-540: every leaf overlapping [from, to] in key order via
 // the sibling chain, valid entries in slot order, Tree.cpp:509-516).
 //
+// The count pass stages each scan's first stage_cap values; the fill pass
+// then copies the scans that fit and walks only the longer ones again.
+//
 // One wave per scan.  The start leaf comes from the leaf directory (or a
 // descent from the covering internal page / the root with a ballot child
 // select); B-link right turns fix a stale start.  Along the leaf chain the
@@ -29,6 +32,13 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
   uint64_t cnt = 0;
   const uint64_t out = a.offsets ? a.offsets[q] : 0;
   uint32_t err = 0;
+  uint64_t* stq = a.stage ? a.stage + q * (uint64_t)a.stage_cap : nullptr;
+  if (a.offsets && stq && a.counts[q] <= a.stage_cap) {
+    // fill pass, staged scan: copy its values out, no second walk
+    const uint64_t c = a.counts[q];
+    for (uint64_t i = (uint64_t)lane; i < c; i += kWave) a.vals[out + i] = stq[i];
+    return;
+  }
   if (lo <= hi) {
     uint64_t p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
     int hops = 0;
@@ -69,7 +79,9 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
       const bool hit = lane < kLeafCardinality && e.val != kValueNull &&
                        (e.fraw & 0xF) == (e.rraw & 0xF) && e.key >= lo && e.key <= hi;
       const uint64_t m = ballot(hit);
-      if (a.offsets && hit) a.vals[out + cnt + popc64(m & lanemask_lt())] = e.val;
+      const uint64_t slot = cnt + popc64(m & lanemask_lt());
+      if (a.offsets && hit) a.vals[out + slot] = e.val;
+      if (!a.offsets && stq && hit && slot < a.stage_cap) stq[slot] = e.val;
       cnt += popc64(m);
       wave_lds_sync();  // LDS reads done before the next stage
       if (!more) break;
@@ -101,6 +113,22 @@ __global__ void k_range_total(const uint64_t* offsets, const uint64_t* counts, u
 void launch_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_t n,
                         const uint32_t* err, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_range_total, dim3(1), dim3(64), 0, s, offsets, counts, n, err, out);
+}
+
+// dst[i] = *src[i], i < 4: gathers scattered u32 results for one read-back
+__global__ void k_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
+                              const uint32_t* s2, const uint32_t* s3) {
+  if (threadIdx.x == 0) {
+    dst[0] = *s0;
+    dst[1] = *s1;
+    dst[2] = *s2;
+    dst[3] = *s3;
+  }
+}
+
+void launch_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
+                        const uint32_t* s2, const uint32_t* s3, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather4_u32, dim3(1), dim3(64), 0, s, dst, s0, s1, s2, s3);
 }
 
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {

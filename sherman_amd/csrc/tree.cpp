@@ -38,6 +38,8 @@ uint32_t start_bits() {
   }();
   return b;
 }
+constexpr uint32_t kRangeStage = 160;      // staged values per range scan
+constexpr uint64_t kRangeStageBytes = 256ull << 20;  // staging budget
 constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
 
 }  // namespace
@@ -53,6 +55,8 @@ struct shm_tree {
   uint64_t* d_counts = nullptr;  // 16 words of device scratch
   uint32_t* route_scratch = nullptr;
   uint64_t* h_pin = nullptr;     // 16 words pinned host scratch
+  uint64_t* rstage = nullptr;    // range-scan value staging (RangeArgs.stage)
+  uint64_t rstage_words = 0;
   // host-authoritative tree metadata (superblock mirror)
   uint64_t root = 0;
   uint32_t root_level = 0;
@@ -412,10 +416,8 @@ int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t res
                                  a.num_seg, s));
   // total = pbase[last] + np[last]
   uint32_t* d_tot = reinterpret_cast<uint32_t*>(t->d_counts + 10);
-  HIP_OK(hipMemcpyAsync(d_tot, t->seg_pbase + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemcpyAsync(d_tot + 1, t->seg_np + (a.num_seg - 1), 4, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemcpyAsync(d_tot + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemcpyAsync(d_tot + 3, t->d_counts + 8, 4, hipMemcpyDeviceToDevice, s));
+  dev::launch_gather4_u32(d_tot, t->seg_pbase + (a.num_seg - 1), t->seg_np + (a.num_seg - 1),
+                          t->d_err, reinterpret_cast<const uint32_t*>(t->d_counts + 8), s);
   int rc = readback(t, s, d_tot, 4 * sizeof(uint32_t));
   if (rc) return rc;
   t->err_pending = false;
@@ -506,8 +508,7 @@ int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint
       dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals,
                              t->ia, t->bins + 2 * dev::kCoarse, t->uk, t->uv, t->dk,
                              t->d_counts, t->part_S, t->d_err, s);
-      DBG(s, "bin_unique");
-      HIP_OK(hipMemcpyAsync(t->d_counts + 2, t->d_err, 4, hipMemcpyDeviceToDevice, s));
+      DBG(s, "bin_unique");  // k_bin_emit also copies the error word to d_counts[2]
       t->err_pending = false;
       return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
     }
@@ -669,6 +670,7 @@ void free_all(shm_tree* t) {
     for (hipEvent_t e : r.e)
       if (e) t->event_pool.push_back(e);
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
+  if (t->rstage) (void)hipFree(t->rstage);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
 }
@@ -1092,13 +1094,33 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
     if (rc) return rc;
   }
   // pass 1 per chunk (the scan workspace holds nmax): counts, exclusive scan,
-  // chunk total and error word back in one read
+  // chunk total and error word back in one read.  A single chunk whose
+  // staging fits kRangeStageBytes keeps its values for pass 2.
   uint64_t total = 0;
   std::vector<uint64_t> base;
+  const bool staged = n <= t->nmax && n * kRangeStage * 8 <= kRangeStageBytes;
+  if (staged && t->rstage_words < n * kRangeStage) {
+    if (t->rstage) {
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipFree(t->rstage));
+      t->rstage = nullptr;
+      t->rstage_words = 0;
+    }
+    const uint64_t words = std::max<uint64_t>(n, 1u << 14) * kRangeStage;
+    if (dalloc(&t->rstage, words)) return SHM_ENOMEM;
+    t->rstage_words = words;
+  }
+  auto rargs = [&](uint64_t off, uint64_t m, const uint64_t* offs, uint64_t* vals) {
+    dev::RangeArgs a = range_args(t, from + off, to + off, m, counts_out + off, offs, vals);
+    if (staged) {
+      a.stage = t->rstage;
+      a.stage_cap = kRangeStage;
+    }
+    return a;
+  };
   for (uint64_t off = 0; off < n; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
-    int rc = range_launch(t, s, range_args(t, from + off, to + off, m, counts_out + off,
-                                           nullptr, nullptr));
+    int rc = range_launch(t, s, rargs(off, m, nullptr, nullptr));
     if (rc) return rc;
     HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, counts_out + off,
                                    offsets_out + off, m, s));
@@ -1121,8 +1143,7 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
   // pass 2: values
   for (uint64_t off = 0, c = 0; off < n; off += t->nmax, ++c) {
     const uint64_t m = std::min(t->nmax, n - off);
-    const int rc = range_launch(t, s, range_args(t, from + off, to + off, m, counts_out + off,
-                                                 offsets_out + off, vals_out));
+    const int rc = range_launch(t, s, rargs(off, m, offsets_out + off, vals_out));
     if (rc) return rc;
   }
   t->err_pending = true;

@@ -84,6 +84,15 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   if (ballot(sl && !pok)) err |= kErrBadPtr;
   const uint32_t st = sl ? a.seg_start[gs] : 0u;
   const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
+  // prefetch: lane li of group q holds op li of segment q (ops >= L are read
+  // in the apply loop), so the loop below makes no global round trip for the
+  // first L ops; the loads overlap the lock and the page staging
+  const int q = lane / L;
+  const int li = lane % L;
+  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
+  const bool pf = (uint32_t)li < qen - qst;
+  const uint64_t pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
+  const uint64_t pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
 
   // ---- lock -------------------------------------------------------------------
   unsigned long long* lk = reinterpret_cast<unsigned long long*>(a.locks);
@@ -148,8 +157,6 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   wait_vm<0>();
 
   // ---- per slot q: header, entries ---------------------------------------------
-  const int q = lane / L;
-  const int li = lane % L;
   const uint32_t* hp = buf + q * kPageDwords;
   const uint32_t h2 = hp[2], h3 = hp[3], h4 = hp[4], h7 = hp[7], h8 = hp[8], h9 = hp[9],
                  h10 = hp[10], z = hp[kOffLeafRear / 4];
@@ -161,7 +168,6 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   const bool qpok = (shfl32(pok ? 1u : 0u, q) != 0) && locked;
   const bool cons = leftmost == 0 && fver == (z & 0xFF);
   if (ballot(qpok && !cons)) err |= kErrInconsistent;
-  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
   const uint64_t qpage = shfl64(page, q);
   bool live = qpok && cons;
   const uint32_t nops = live ? qen - qst : 0u;
@@ -211,8 +217,10 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   bool bad = false;
   for (uint32_t t = 0; ballot(t < nloop); ++t) {
     const bool act = t < nloop && !bad;
-    const uint64_t kq = act ? a.op_key[qst + t] : 0;
-    const uint64_t vq = act ? a.op_val[qst + t] : 0;
+    const int src = q * L + (t < (uint32_t)L ? (int)t : L - 1);
+    const uint64_t sk = shfl64(pk, src), sv = shfl64(pv, src);
+    const uint64_t kq = act ? (t < (uint32_t)L ? sk : a.op_key[qst + t]) : 0;
+    const uint64_t vq = act ? (t < (uint32_t)L ? sv : a.op_val[qst + t]) : 0;
     if (act && (kq < lowest || kq >= highest)) bad = true;  // not this page's key
     const bool go = act && !bad;
     int hj = -1;
