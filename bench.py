@@ -73,6 +73,9 @@ def parse():
                    help="order get batches by key before the walk: always "
                         "(SHM_FLAG_SORT_GETS), never, or when dense (default)")
     p.add_argument("--profile-steps", type=int, default=10)
+    p.add_argument("--streams", type=int, default=2, choices=(1, 2),
+                   help="c2, N=1: consecutive batches alternate over this many HIP "
+                        "streams, so one batch's ordering overlaps the previous walk")
     p.add_argument("--sim-world", type=int, default=1,
                    help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
                         "range partition (the per-GPU work of an N-GPU run, no exchange)")
@@ -193,13 +196,23 @@ def main():
                 tree.hash_keys(ids, k)
                 qs.append(k)
         route = ShardRouter(tree, world, dist) if world > 1 else None
+        # N = 1: independent batches alternate over two streams (each with its
+        # own result buffers); the library orders them on the device
+        nstr = args.streams if route is None else 1
+        streams = [torch.cuda.Stream() for _ in range(nstr)] if nstr > 1 else [None]
+        outs = [(vals, found)] + [(torch.empty_like(vals), torch.empty_like(found))
+                                  for _ in range(nstr - 1)]
+        for sx in streams:
+            if sx is not None:
+                sx.wait_stream(torch.cuda.current_stream())
 
         def step(i):
             q = qs[i % N_BATCHES]
+            v, f = outs[i % nstr]
             if route is None:
-                tree.search_batch(q, vals, found)
+                tree.search_batch(q, v, f, stream=streams[i % nstr])
             else:
-                route.search(q, vals, found)
+                route.search(q, v, f)
     elif args.workload == "c5":
         from sherman_amd.shard import umin
         assert not sim, "--sim-world is a C2 option"
@@ -279,7 +292,7 @@ def main():
     mops = total_ops / elapsed / 1e6
     torch.cuda.synchronize()
     if args.workload == "c2":
-        hit_rate = float(found.float().mean().item())
+        hit_rate = float(outs[(args.steps - 1) % len(outs)][1].float().mean().item())
     elif args.workload == "c5":
         c, _ = scan_out["r"]
         hit_rate = float(c.float().mean().item())  # mean values per scan
@@ -359,6 +372,7 @@ def main():
                 "tree_height": st["height"],
                 "pages": st["pages_used"],
                 "get_order": args.sort,
+                "streams": (len(outs) if args.workload == "c2" else 1),
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
                 "splits_in_timed_steps": st_end["splits"] - splits0,

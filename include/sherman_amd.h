@@ -99,8 +99,14 @@ int shm_abi_version(void);
 
 /* batched hot path (device pointers) ------------------------------------------ */
 /* vals_out[i] = value of keys[i] (0 if absent); found_out[i] = 1/0.
- * found_out may be NULL. Reads only; safe to call concurrently on distinct
- * streams with other searches. */
+ * found_out may be NULL. Reads only.
+ * Streams: searches issued on distinct streams may run concurrently on the
+ * device (an ordered batch uses one of two internal workspaces, alternating,
+ * so consecutive batches on two streams overlap one's ordering with the
+ * other's walk).  Every other call (insert, delete, range, routing, a
+ * directory rebuild) is ordered on the device after all calls issued before
+ * it on any stream, and before all calls issued after it: results follow
+ * the host's call order. */
 int shm_search_batch(shm_tree *t, const uint64_t *keys, uint64_t n,
                      uint64_t *vals_out, uint8_t *found_out, void *stream);
 /* Upsert keys[i] -> vals[i] in batch order (last writer in the batch wins).

@@ -112,6 +112,30 @@ struct shm_tree {
   ProfRec* prof_ins = nullptr;  // the insert chunk being timed
   std::vector<hipEvent_t> event_pool;
   shm_profile_t prof_acc{};
+  // ---- cross-stream ordering (Order below) --------------------------------
+  // Searches are "shared" calls: they may run concurrently on distinct
+  // streams.  An ordered search uses one of two get workspaces, alternating,
+  // so the partition of one batch can overlap the walk of the previous one
+  // on another stream.  Every other call that touches device state (inserts,
+  // deletes, range scans, routing, a directory rebuild) is "exclusive": its
+  // stream waits for every earlier call on the other streams.
+  struct GetWs {
+    uint64_t *keys1 = nullptr, *keys_out = nullptr;
+    uint32_t *pos1 = nullptr, *src = nullptr, *M = nullptr, *S = nullptr, *chunks = nullptr;
+  };
+  GetWs gws[2];           // gws[0] aliases the insert workspace (ka, kb, ia, ib, part_*)
+  int next_gws = 0;
+  struct StreamEv {
+    hipStream_t s;
+    hipEvent_t ev;
+  };
+  std::vector<StreamEv> shared_ev;  // last shared call per stream
+  hipEvent_t ex_ev = nullptr;       // last exclusive call
+  hipStream_t ex_s = nullptr;
+  bool ex_valid = false;
+  hipEvent_t gws_ev[2] = {nullptr, nullptr};  // last user of each get workspace
+  hipStream_t gws_s[2] = {nullptr, nullptr};
+  bool gws_valid[2] = {false, false};
 };
 
 namespace {
@@ -142,6 +166,83 @@ hipStream_t pick(shm_tree* t, void* s) {
   (void)t;
   return (hipStream_t)s;
 }
+
+hipEvent_t new_event() {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Cross-stream ordering of one API call (shm_tree: shared / exclusive calls).
+// Constructed under t->mu before the call's first launch; the destructor
+// records the call's completion event on its stream.  Waits are skipped for
+// events of the same stream (stream order already covers them).
+struct Order {
+  shm_tree* t;
+  hipStream_t s;
+  bool ex;
+  int ws = -1;  // get workspace used by a shared call (-1: none)
+  int rc = SHM_OK;
+  Order(shm_tree* tt, hipStream_t ss, bool exclusive) : t(tt), s(ss), ex(exclusive) {
+    if (t->ex_valid && t->ex_s != s) wait(t->ex_ev);
+    if (ex) {
+      for (const auto& r : t->shared_ev)
+        if (r.s != s) wait(r.ev);
+      for (int j = 0; j < 2; ++j)
+        if (t->gws_valid[j] && t->gws_s[j] != s) wait(t->gws_ev[j]);
+    }
+  }
+  // a shared call that turns exclusive (a directory rebuild)
+  void make_exclusive() {
+    if (ex) return;
+    ex = true;
+    for (const auto& r : t->shared_ev)
+      if (r.s != s) wait(r.ev);
+    for (int j = 0; j < 2; ++j)
+      if (t->gws_valid[j] && t->gws_s[j] != s) wait(t->gws_ev[j]);
+  }
+  // take the next get workspace; returns its index
+  int take_ws() {
+    ws = t->next_gws;
+    t->next_gws ^= 1;
+    if (!ex && t->gws_valid[ws] && t->gws_s[ws] != s) wait(t->gws_ev[ws]);
+    return ws;
+  }
+  void wait(hipEvent_t e) {
+    if (hipStreamWaitEvent(s, e, 0) != hipSuccess) rc = SHM_EIO;
+  }
+  ~Order() {
+    if (ex) {
+      if (!t->ex_ev) t->ex_ev = new_event();
+      if (t->ex_ev && hipEventRecord(t->ex_ev, s) == hipSuccess) {
+        t->ex_s = s;
+        t->ex_valid = true;
+        // the waits above ordered this call after every earlier one
+        for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
+        t->shared_ev.clear();
+        t->gws_valid[0] = t->gws_valid[1] = false;
+      }
+      return;
+    }
+    shm_tree::StreamEv* r = nullptr;
+    for (auto& x : t->shared_ev)
+      if (x.s == s) r = &x;
+    if (!r) {
+      hipEvent_t e = new_event();
+      if (!e) return;
+      t->shared_ev.push_back({s, e});
+      r = &t->shared_ev.back();
+    }
+    (void)hipEventRecord(r->ev, s);
+    if (ws >= 0) {
+      if (!t->gws_ev[ws]) t->gws_ev[ws] = new_event();
+      if (t->gws_ev[ws] && hipEventRecord(t->gws_ev[ws], s) == hipSuccess) {
+        t->gws_s[ws] = s;
+        t->gws_valid[ws] = true;
+      }
+    }
+  }
+};
 
 // SHM_GET_KERNEL=walk selects the page-at-a-time walk (k_walk) for gets
 // instead of the grouped one (k_get): an A/B switch for measurements.
@@ -245,8 +346,12 @@ bool use_leaf_dir(const shm_tree* t) {
 
 // (re)build the leaf directory when missing or the tree grew by > 1/32;
 // 2^bits entries with bits = ceil(log2(pages)) (~1 entry per leaf)
+bool dir_stale(const shm_tree* t) {
+  return !(t->dir_valid && t->next_page <= t->dir_np + t->dir_np / 32);
+}
+
 int refresh_dir(shm_tree* t, hipStream_t s) {
-  if (t->dir_valid && t->next_page <= t->dir_np + t->dir_np / 32) return SHM_OK;
+  if (!dir_stale(t)) return SHM_OK;
   uint32_t bits = 10;
   while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
   if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
@@ -671,6 +776,14 @@ void free_all(shm_tree* t) {
       if (e) t->event_pool.push_back(e);
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
   if (t->rstage) (void)hipFree(t->rstage);
+  {
+    shm_tree::GetWs& w = t->gws[1];
+    F(w.keys1); F(w.keys_out); F(w.pos1); F(w.src); F(w.M); F(w.S); F(w.chunks);
+  }
+  for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
+  if (t->ex_ev) (void)hipEventDestroy(t->ex_ev);
+  for (hipEvent_t e : t->gws_ev)
+    if (e) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
 }
@@ -850,6 +963,18 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->start, 1ull << start_bits());
   rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
   rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count), then (upserts, deletes)
+  // get workspaces: 0 shares the insert arrays, 1 is its own
+  t->gws[0] = {t->kb, t->ka, t->ia, t->ib, t->part_hist, t->part_S, t->part_chunks};
+  {
+    shm_tree::GetWs& w = t->gws[1];
+    rc |= dalloc(&w.keys1, n);
+    rc |= dalloc(&w.keys_out, n);
+    rc |= dalloc(&w.pos1, n);
+    rc |= dalloc(&w.src, n);
+    rc |= dalloc(&w.M, dev::kPartHistWords);
+    rc |= dalloc(&w.S, dev::kPartGroupWords);
+    rc |= dalloc(&w.chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
+  }
   if (rc) return fail(SHM_ENOMEM);
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
@@ -859,6 +984,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
       hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
+      hipMemsetAsync(t->gws[1].S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->arena, 0, kPageSize, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
@@ -896,10 +1022,13 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   const bool dense = (t->cfg.flags & SHM_FLAG_AUTO_SORT_GETS) && 5 * n >= 2 * t->next_page;
   const bool ordered = ((t->cfg.flags & SHM_FLAG_SORT_GETS) || dense) && n >= kSortMinGets;
   const bool dir = use_leaf_dir(t);
+  Order ord(t, s, false);
   if (dir) {
-    const int rc = refresh_dir(t, s);
+    if (dir_stale(t)) ord.make_exclusive();  // the rebuild rewrites what searches read
+    const int rc = ord.rc ? ord.rc : refresh_dir(t, s);
     if (rc) return rc;
   } else if (ordered && (t->start_np != t->next_page || t->start_root != t->root)) {
+    ord.make_exclusive();
     dev::launch_start_table(t->arena, t->arena_bytes, t->cfg.node_id, t->root, start_bits(),
                             t->start, t->d_err, s);
     t->start_np = t->next_page;
@@ -923,14 +1052,14 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       // (keys1 = kb, pos1 = ia, walk order = ka, src = ib); the walk stores
       // result p at vals1[src[p]] (kb, inside p's chunk), unpartition gathers
       const bool direct = get_direct();
-      dev::launch_partition(keys + off, m, t->cfg.key_lo, t->cfg.key_bits, t->part_hist,
-                            t->part_S, t->part_chunks,
-                            t->kb, t->ia,
-                            t->ka, t->ib, direct, s);
-      a.keys = t->ka;
-      a.perm = t->ib;
-      if (!direct) {  // else results go straight to input order (ib = input index)
-        a.out_val = t->kb;
+      const shm_tree::GetWs& w = t->gws[ord.ws >= 0 ? ord.ws : ord.take_ws()];
+      if (ord.rc) return ord.rc;
+      dev::launch_partition(keys + off, m, t->cfg.key_lo, t->cfg.key_bits, w.M, w.S, w.chunks,
+                            w.keys1, w.pos1, w.keys_out, w.src, direct, s);
+      a.keys = w.keys_out;
+      a.perm = w.src;
+      if (!direct) {  // else results go straight to input order (src = input index)
+        a.out_val = w.keys1;
         a.out_found = nullptr;
       }
       a.xcd_remap = getenv("SHM_XCD_REMAP") ? atoi(getenv("SHM_XCD_REMAP")) : 1;
@@ -976,7 +1105,8 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       t->prof_pending.push_back(pr);
     }
     if (gathered) {
-      dev::launch_unpartition(t->kb, t->ia, m, vals_out + off,
+      const shm_tree::GetWs& w = t->gws[ord.ws];
+      dev::launch_unpartition(w.keys1, w.pos1, m, vals_out + off,
                               found_out ? found_out + off : nullptr, s);
       DBG(s, "gather");
     }
@@ -989,6 +1119,8 @@ int shm_insert_batch(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
                      uint64_t n, void* stream) {
   if (!t || (n && (!keys || !vals))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
+  Order ord(t, pick(t, stream), true);
+  if (ord.rc) return ord.rc;
   hipStream_t s = pick(t, stream);
   int rc = SHM_OK;
   for (uint64_t off = 0; off < n && rc == SHM_OK; off += t->nmax) {
@@ -1072,6 +1204,8 @@ int shm_range_query(shm_tree* t, const uint64_t* from, const uint64_t* to,
   if (offsets && !vals_out) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
+  Order ord(t, s, true);  // range workspace (scan temp, staging)
+  if (ord.rc) return ord.rc;
   if (use_leaf_dir(t)) {
     const int rc = refresh_dir(t, s);
     if (rc) return rc;
@@ -1087,6 +1221,8 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
   if (vals_cap && !vals_out) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
+  Order ord(t, s, true);  // range workspace (scan temp, staging)
+  if (ord.rc) return ord.rc;
   *total_out = 0;
   if (n == 0) return SHM_OK;
   if (use_leaf_dir(t)) {
@@ -1202,6 +1338,7 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   t->next_page = pages;
   t->start_np = ~0ull;  // contents changed: rebuild the get start table
   t->dir_valid = false;  // and the leaf directory
+  Order ord(t, t->stream, true);
   return write_superblock(t, t->stream);
 }
 
@@ -1245,7 +1382,10 @@ int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
   if (!t || num_shards == 0 || num_shards > 64 || !counts_out) return SHM_EINVAL;
   if (n && (!keys || !keys_out || !perm_out)) return SHM_EINVAL;
   if (n > t->nmax) return SHM_E2BIG;
+  std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
+  Order ord(t, s, true);  // route_scratch
+  if (ord.rc) return ord.rc;
   dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out,
                            t->route_scratch, s);
   HIP_OK(hipGetLastError());

@@ -493,3 +493,48 @@ def test_insert_with_colliding_lock_words(lib_ok):
         orc.apply_batch(keys, vals)
     compare_contents(t, orc)
     t.close()
+
+
+def test_searches_on_two_streams_with_an_insert_between(lib_ok):
+    """Cross-stream ordering (tree.cpp Order): ordered searches alternate over
+    two streams and two get workspaces; an insert issued on a third stream is
+    seen by every search issued after it (host order), on either stream."""
+    n = 1 << 16
+    keys = hashed_keys(1, n + 1)
+    vals = np.arange(1, n + 1, dtype=U64) * U64(2)
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16)
+    orc = OracleTree(256 << 20)
+    gpu_insert(t, keys, vals)
+    orc.apply_batch(keys, vals)
+    t.synchronize()
+    rng = np.random.default_rng(5)
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    new_k = hashed_keys(n + 1, n + 20001)
+    new_v = np.arange(1, new_k.size + 1, dtype=U64) * U64(7)
+    pool = np.concatenate([keys, new_k])
+    plan = []
+    for i in range(8):
+        q = pool[rng.integers(0, pool.size, 1 << 15)]
+        plan.append(("get", q))
+        if i == 3:
+            plan.append(("put", None))
+    outs, want = [], []
+    for j, (kind, q) in enumerate(plan):
+        if kind == "put":
+            t.insert_batch(dev(new_k), dev(new_v), stream=s3)
+            orc.apply_batch(new_k, new_v)
+            continue
+        st = s1 if j % 2 else s2
+        with torch.cuda.stream(st):
+            k = dev(q)
+            v = torch.empty_like(k)
+            f = torch.empty(k.numel(), dtype=torch.uint8, device=k.device)
+        t.search_batch(k, v, f, stream=st)
+        outs.append((q, v, f, k))
+        want.append(orc.search_batch(q))
+    torch.cuda.synchronize()
+    for (q, v, f, _), (ov, of) in zip(outs, want):
+        assert_same(q, ov, of, host(v), f.cpu().numpy())
+    t.check()
+    t.close()
+    orc.close()
