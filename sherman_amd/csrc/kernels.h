@@ -169,10 +169,11 @@ void launch_compact_unique(const uint64_t* sk, const uint32_t* sidx,
                            const uint64_t* pos, uint64_t n, uint64_t* uk,
                            uint64_t* uv, uint64_t* dk, uint64_t* counts,
                            hipStream_t s);
-void launch_seg_heads(const uint64_t* page, uint64_t n, uint32_t* heads,
+// segments of a located op list (n_dev: device-side op count <= n, nullable)
+void launch_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* heads,
                       hipStream_t s);
 void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
-                     const uint32_t* pos, uint64_t n, uint32_t* seg_start,
+                     const uint32_t* pos, uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
@@ -219,6 +220,12 @@ void launch_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_
 // dst[i] = *s_i (one launch instead of four device-to-device copies)
 void launch_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
                         const uint32_t* s2, const uint32_t* s3, hipStream_t s);
+struct Gather8 {
+  const uint32_t* p[8];
+  int n;
+};
+// dst[i] = *g.p[i], i < g.n
+void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s);
 // x[i] += c for i < n
 void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 

@@ -131,6 +131,14 @@ void launch_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
   hipLaunchKernelGGL(k_gather4_u32, dim3(1), dim3(64), 0, s, dst, s0, s1, s2, s3);
 }
 
+__global__ void k_gather_u32(uint32_t* dst, Gather8 g) {
+  if ((int)threadIdx.x < g.n) dst[threadIdx.x] = *g.p[threadIdx.x];
+}
+
+void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_u32, dim3(1), dim3(64), 0, s, dst, g);
+}
+
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += c;

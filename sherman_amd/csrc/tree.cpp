@@ -38,6 +38,7 @@ uint32_t start_bits() {
   }();
   return b;
 }
+constexpr int kRedoOrder = -1000;          // internal: re-order with rocPRIM
 constexpr uint32_t kRangeStage = 160;      // staged values per range scan
 constexpr uint64_t kRangeStageBytes = 256ull << 20;  // staging budget
 constexpr int kWalkDepth = 4;             // (ring depth is fixed in walk.hip)
@@ -55,6 +56,7 @@ struct shm_tree {
   uint64_t* d_counts = nullptr;  // 16 words of device scratch
   uint32_t* route_scratch = nullptr;
   uint64_t* h_pin = nullptr;     // 16 words pinned host scratch
+  uint64_t rb_nup = 0, rb_ndel = 0;  // ordering counts of the last read-back
   uint64_t* rstage = nullptr;    // range-scan value staging (RangeArgs.stage)
   uint64_t rstage_words = 0;
   // host-authoritative tree metadata (superblock mirror)
@@ -265,6 +267,16 @@ int walk_nt() {
   return v;
 }
 
+// SHM_DEFER_COUNTS=0 reads the insert ordering's counts back before the
+// leaf level (one more host synchronisation per batch; A/B knob)
+bool deferred_counts() {
+  static const bool v = [] {
+    const char* e = getenv("SHM_DEFER_COUNTS");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return v;
+}
+
 // SHM_BIN_UNIQUE=0 orders insert batches with the per-bin bitonic sort and
 // the mark / scan / compact passes instead of k_bin_unique (A/B knob)
 bool bin_unique() {
@@ -466,10 +478,12 @@ int locate_kernel() {
 }
 
 int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
-                uint64_t n_ops, int level, bool sync = true) {
+                uint64_t n_ops, int level, bool sync = true,
+                const uint64_t* n_dev = nullptr) {
   dev::WalkArgs w = walk_args(t);
   w.keys = op_key;
   w.n = n_ops;
+  w.n_dev = n_dev;
   w.out_page = t->pages;
   w.target_level = level;
   if (locate_kernel() != 2 && (level > 0 || use_fast_insert())) {
@@ -490,10 +504,10 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
     dev::launch_walk(w, n_ops, 4, true, s);
   }
   DBG(s, "walk(locate)");
-  dev::launch_seg_heads(t->pages, n_ops, t->heads, s);
+  dev::launch_seg_heads(t->pages, n_ops, n_dev, t->heads, s);
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, t->seg_start,
+  dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
                        t->seg_page, d_ns, s);
   DBG(s, "seg_fill");
   if (!sync) return (int64_t)n_ops;  // an upper bound; the count stays on the device
@@ -519,16 +533,31 @@ int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
 int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t reserve) {
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
                                  a.num_seg, s));
-  // total = pbase[last] + np[last]
-  uint32_t* d_tot = reinterpret_cast<uint32_t*>(t->d_counts + 10);
-  dev::launch_gather4_u32(d_tot, t->seg_pbase + (a.num_seg - 1), t->seg_np + (a.num_seg - 1),
-                          t->d_err, reinterpret_cast<const uint32_t*>(t->d_counts + 8), s);
-  int rc = readback(t, s, d_tot, 4 * sizeof(uint32_t));
+  // total = pbase[last] + np[last]; with the error word, the device-side
+  // segment count and the ordering's (upserts, deletes) in one read-back
+  uint32_t* d_tot = reinterpret_cast<uint32_t*>(t->d_counts + 16);
+  dev::Gather8 g{};
+  g.p[0] = t->seg_pbase + (a.num_seg - 1);
+  g.p[1] = t->seg_np + (a.num_seg - 1);
+  g.p[2] = t->d_err;
+  g.p[3] = reinterpret_cast<const uint32_t*>(t->d_counts + 8);
+  g.p[4] = reinterpret_cast<const uint32_t*>(t->d_counts + 0);  // low words (n < 2^31)
+  g.p[5] = reinterpret_cast<const uint32_t*>(t->d_counts + 1);
+  g.n = 6;
+  dev::launch_gather_u32(d_tot, g, s);
+  int rc = readback(t, s, d_tot, 6 * sizeof(uint32_t));
   if (rc) return rc;
   t->err_pending = false;
   const uint32_t* h = reinterpret_cast<const uint32_t*>(t->h_pin);
   const uint64_t total = (uint64_t)h[0] + h[1];
+  t->rb_nup = h[4];
+  t->rb_ndel = h[5];
   if (a.num_seg_dev) a.num_seg = h[3];  // the device-side segment count, now known
+  if (h[2] & (dev::kErrKeyMax | dev::kErrSortOverflow)) {
+    // the deferred ordering check (insert_chunk_impl): nothing was written
+    HIP_OK(hipMemsetAsync(t->d_err, 0, 4, s));
+    return (h[2] & dev::kErrKeyMax) ? SHM_EINVAL : kRedoOrder;
+  }
   if (h[2]) return check_err(t, s);
   if (total > t->sep_cap) return SHM_ENOMEM;
   if (t->next_page + total + reserve > t->cap_pages) return SHM_ENOMEM;
@@ -539,9 +568,9 @@ int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t res
 // sep[out]) or a negative status.
 int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                     const uint64_t* op_val, uint64_t n_ops, int level,
-                    bool is_delete, int out) {
+                    bool is_delete, int out, const uint64_t* n_dev = nullptr) {
   const bool fast_leaf = level == 0 && !is_delete && use_fast_insert();
-  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf);
+  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf, n_dev);
   if (ns < 0) return ns;
   if (ns == 0) return 0;
   dev::SegArgs a = seg_args(t);
@@ -637,10 +666,71 @@ int order_and_dedup(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint
   return readback(t, s, t->d_counts, 3 * sizeof(uint64_t));
 }
 
+int insert_chunk_sync(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                      const uint64_t* vals, uint64_t n, bool fast);
+
+// the split levels above the leaves, after the leaf level produced nsep
+// separators into sep[cur]
+int apply_upper_levels(shm_tree* t, hipStream_t s, int64_t nsep, int cur) {
+  int level = 1;
+  while (nsep > 0) {
+    if (level > kMaxLevelOfTree) return SHM_EIO;
+    if ((uint32_t)(level - 1) == t->root_level) {
+      // the root split: new root above it (update_new_root, Tree.cpp:126-149)
+      if (t->next_page + 1 > t->cap_pages) return SHM_ENOMEM;
+      const uint64_t off = t->next_page * kPageSize;
+      dev::launch_new_root(t->arena, off, t->root, (uint32_t)level, s);
+      DBG(s, "new_root");
+      t->next_page += 1;
+      t->root = ga_make(t->cfg.node_id, off);
+      t->root_level = (uint32_t)level;
+    }
+    const int nxt = 1 - cur;
+    nsep = apply_level(t, s, t->sep_key[cur], t->sep_ptr[cur], (uint64_t)nsep,
+                       level, false, nxt);
+    cur = nxt;
+    ++level;
+  }
+  return nsep < 0 ? (int)nsep : SHM_OK;
+}
+
 int insert_chunk_impl(shm_tree* t, hipStream_t s, const uint64_t* keys,
                       const uint64_t* vals, uint64_t n) {
+  if (use_fast_insert() && bin_unique() && deferred_counts()) {
+    // Ordering with its counts left on the device: the leaf level runs over
+    // n (an upper bound) with the device-side upsert count, and the one
+    // read-back after the in-place upserts returns the counts with the
+    // split total.  An ordering error (kKeyMax, a bin too large) gates the
+    // upsert kernel off, so nothing is written before the host sees it.
+    dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, s);
+    dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
+                                 t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
+    dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
+                           t->bins + 2 * dev::kCoarse, t->uk, t->uv, t->dk, t->d_counts,
+                           t->part_S, t->d_err, s);
+    DBG(s, "bin_unique (deferred counts)");
+    const int64_t nsep = apply_level(t, s, t->uk, t->uv, n, 0, false, 0, t->d_counts);
+    if (nsep == kRedoOrder) return insert_chunk_sync(t, s, keys, vals, n, false);
+    if (nsep < 0) return (int)nsep;
+    const uint64_t n_del = t->rb_ndel;
+    int rc = apply_upper_levels(t, s, nsep, 0);
+    if (rc) return rc;
+    // deletes after the upserts: one op per key, so the order between them
+    // does not change the contents
+    if (n_del) {
+      const int64_t r = apply_level(t, s, t->dk, nullptr, n_del, 0, true, 0);
+      if (r < 0) return (int)r;
+    }
+    return SHM_OK;
+  }
+  return insert_chunk_sync(t, s, keys, vals, n, use_fast_insert());
+}
+
+// the ordering's counts read back before anything is applied
+int insert_chunk_sync(shm_tree* t, hipStream_t s, const uint64_t* keys,
+                      const uint64_t* vals, uint64_t n, bool fast) {
   // 1-2. order by key, one op per key (last writer in batch order)
-  int rc = order_and_dedup(t, s, keys, vals, n, use_fast_insert());
+  int rc = order_and_dedup(t, s, keys, vals, n, fast);
   if (rc) return rc;
   if ((uint32_t)t->h_pin[2] & dev::kErrSortOverflow) {
     // a coarse bin too large for the LDS sort (skewed keys): rocPRIM instead
@@ -661,29 +751,9 @@ int insert_chunk_impl(shm_tree* t, hipStream_t s, const uint64_t* keys,
     if (r < 0) return (int)r;
   }
   if (!n_up) return SHM_OK;
-  int cur = 0;
-  int64_t nsep = apply_level(t, s, t->uk, t->uv, n_up, 0, false, cur);
-  int level = 1;
-  while (nsep > 0) {
-    if (level > kMaxLevelOfTree) return SHM_EIO;
-    if ((uint32_t)(level - 1) == t->root_level) {
-      // the root split: new root above it (update_new_root, Tree.cpp:126-149)
-      if (t->next_page + 1 > t->cap_pages) return SHM_ENOMEM;
-      const uint64_t off = t->next_page * kPageSize;
-      dev::launch_new_root(t->arena, off, t->root, (uint32_t)level, s);
-      DBG(s, "new_root");
-      t->next_page += 1;
-      t->root = ga_make(t->cfg.node_id, off);
-      t->root_level = (uint32_t)level;
-    }
-    const int nxt = 1 - cur;
-    nsep = apply_level(t, s, t->sep_key[cur], t->sep_ptr[cur], (uint64_t)nsep,
-                       level, false, nxt);
-    cur = nxt;
-    ++level;
-  }
+  const int64_t nsep = apply_level(t, s, t->uk, t->uv, n_up, 0, false, 0);
   if (nsep < 0) return (int)nsep;
-  return SHM_OK;
+  return apply_upper_levels(t, s, nsep, 0);
 }
 
 hipEvent_t take_event(shm_tree* t);
@@ -932,7 +1002,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->arena, t->arena_bytes);
   rc |= dalloc(&t->locks, cfg->num_locks);
   rc |= dalloc(&t->d_err, 4);
-  rc |= dalloc(&t->d_counts, 16);
+  rc |= dalloc(&t->d_counts, 32);
   rc |= dalloc(&t->route_scratch, dev::route_scratch_words(n));
   rc |= dalloc(&t->ka, n);
   rc |= dalloc(&t->kb, n);

@@ -66,7 +66,11 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
   const uint64_t g0 = wid * G;
   // the grid may be sized for an upper bound of the segment count
-  const uint32_t num_seg = a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
+  // an ordering error flagged on the device (kKeyMax in the batch, a bin
+  // too large) rejects the batch before anything is written: the host sees
+  // it at its next read-back and re-orders or returns SHM_EINVAL
+  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
+  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
   if (g0 >= num_seg) {
     // past the last segment: zero the new-page counts the host scans
     if (lane < G && g0 + (uint64_t)lane < a.num_seg) a.seg_newpages[g0 + lane] = 0;

@@ -91,35 +91,46 @@ void launch_compact_unique(const uint64_t* sk, const uint32_t* sidx,
   if (n) hipLaunchKernelGGL(k_compact_unique, grid1(n), dim3(kT), 0, s, sk, sidx, vals, flags, pos, n, uk, uv, dk, counts);
 }
 
-__global__ void k_seg_heads(const uint64_t* page, uint64_t n, uint32_t* heads) {
+// n_dev (nullable): the device-side op count, n its upper bound
+__device__ __forceinline__ uint64_t dev_n(const uint64_t* n_dev, uint64_t n) {
+  return n_dev ? *n_dev : n;
+}
+
+__global__ void k_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev,
+                            uint32_t* heads) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  heads[i] = (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
+  const uint64_t nv = dev_n(n_dev, n);
+  heads[i] = i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
 }
-void launch_seg_heads(const uint64_t* page, uint64_t n, uint32_t* heads,
+void launch_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* heads,
                       hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_seg_heads, grid1(n), dim3(kT), 0, s, page, n, heads);
+  if (n) hipLaunchKernelGGL(k_seg_heads, grid1(n), dim3(kT), 0, s, page, n, n_dev, heads);
 }
 
 __global__ void k_seg_fill(const uint64_t* page, const uint32_t* heads,
-                           const uint32_t* pos, uint64_t n, uint32_t* seg_start,
-                           uint64_t* seg_page, uint32_t* num_seg) {
+                           const uint32_t* pos, uint64_t n, const uint64_t* n_dev,
+                           uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (heads[i]) {
+  const uint64_t nv = dev_n(n_dev, n);
+  if (i < nv && heads[i]) {
     seg_start[pos[i]] = (uint32_t)i;
     seg_page[pos[i]] = page[i];
   }
-  if (i + 1 == n) {
+  if (i + 1 == nv) {
     const uint32_t ns = pos[i] + heads[i];
     *num_seg = ns;
-    seg_start[ns] = (uint32_t)n;
+    seg_start[ns] = (uint32_t)nv;
+  } else if (nv == 0 && i == 0) {
+    *num_seg = 0;
+    seg_start[0] = 0;
   }
 }
 void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
-                     const uint32_t* pos, uint64_t n, uint32_t* seg_start,
+                     const uint32_t* pos, uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_seg_fill, grid1(n), dim3(kT), 0, s, page, heads, pos, n, seg_start, seg_page, num_seg);
+  if (n) hipLaunchKernelGGL(k_seg_fill, grid1(n), dim3(kT), 0, s, page, heads, pos, n, n_dev, seg_start, seg_page, num_seg);
 }
 
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
