@@ -195,13 +195,18 @@ def main():
                 k = torch.empty_like(ids)
                 tree.hash_keys(ids, k)
                 qs.append(k)
-        route = ShardRouter(tree, world, dist) if world > 1 else None
-        # N = 1: independent batches alternate over two streams (each with its
-        # own result buffers); the library orders them on the device
-        nstr = args.streams if route is None else 1
+        # independent batches alternate over two streams (each with its own
+        # result buffers; N > 1: its own router buffers and RCCL communicator,
+        # so one batch's exchange and ordering overlap the previous walk); the
+        # library orders the streams' calls on the device
+        nstr = args.streams
         streams = [torch.cuda.Stream() for _ in range(nstr)] if nstr > 1 else [None]
         outs = [(vals, found)] + [(torch.empty_like(vals), torch.empty_like(found))
                                   for _ in range(nstr - 1)]
+        routes = [None] * nstr
+        if world > 1:
+            groups = [None] + [dist.new_group(list(range(world))) for _ in range(nstr - 1)]
+            routes = [ShardRouter(tree, world, dist, group=gr) for gr in groups]
         for sx in streams:
             if sx is not None:
                 sx.wait_stream(torch.cuda.current_stream())
@@ -209,10 +214,12 @@ def main():
         def step(i):
             q = qs[i % N_BATCHES]
             v, f = outs[i % nstr]
-            if route is None:
-                tree.search_batch(q, v, f, stream=streams[i % nstr])
+            sx = streams[i % nstr]
+            if routes[0] is None:
+                tree.search_batch(q, v, f, stream=sx)
             else:
-                route.search(q, v, f)
+                with torch.cuda.stream(sx if sx is not None else torch.cuda.current_stream()):
+                    routes[i % nstr].search(q, v, f)
     elif args.workload == "c5":
         from sherman_amd.shard import umin
         assert not sim, "--sim-world is a C2 option"
@@ -373,6 +380,7 @@ def main():
                 "pages": st["pages_used"],
                 "get_order": args.sort,
                 "streams": (len(outs) if args.workload == "c2" else 1),
+                "rccl_groups": (len(outs) if args.workload == "c2" and world > 1 else None),
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
                 "splits_in_timed_steps": st_end["splits"] - splits0,

@@ -55,6 +55,9 @@ struct shm_tree {
   uint32_t* d_err = nullptr;
   uint64_t* d_counts = nullptr;  // 16 words of device scratch
   uint32_t* route_scratch = nullptr;
+  // route_bucket scratch per stream (route_scratch serves the first one), so
+  // routed batches on distinct streams bucket concurrently
+  std::vector<std::pair<hipStream_t, uint32_t*>> route_ws;
   uint64_t* h_pin = nullptr;     // 16 words pinned host scratch
   uint64_t rb_nup = 0, rb_ndel = 0;  // ordering counts of the last read-back
   uint64_t* rstage = nullptr;    // range-scan value staging (RangeArgs.stage)
@@ -835,6 +838,8 @@ void free_all(shm_tree* t) {
     if (p) (void)hipFree(p);
   };
   F(t->arena); F(t->locks); F(t->d_err); F(t->d_counts); F(t->route_scratch);
+  for (auto& r : t->route_ws)
+    if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
@@ -1454,10 +1459,20 @@ int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
   if (n > t->nmax) return SHM_E2BIG;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(t, stream);
-  Order ord(t, s, true);  // route_scratch
+  Order ord(t, s, false);  // reads only the caller's keys; scratch per stream
   if (ord.rc) return ord.rc;
-  dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out,
-                           t->route_scratch, s);
+  uint32_t* scratch = nullptr;
+  for (auto& r : t->route_ws)
+    if (r.first == s) scratch = r.second;
+  if (!scratch) {
+    if (t->route_ws.empty()) {
+      scratch = t->route_scratch;
+    } else if (dalloc(&scratch, dev::route_scratch_words(t->nmax))) {
+      return SHM_ENOMEM;
+    }
+    t->route_ws.push_back({s, scratch});
+  }
+  dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out, scratch, s);
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }
