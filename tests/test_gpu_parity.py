@@ -538,3 +538,27 @@ def test_searches_on_two_streams_with_an_insert_between(lib_ok):
     t.check()
     t.close()
     orc.close()
+
+
+def test_insert_bin_overflow_reorders(lib_ok):
+    """Clustered keys put > 6144 ops into one ordering bin: k_bin_unique flags
+    the overflow, the upsert kernel is gated off, and the batch is re-ordered
+    by the rocPRIM path (tree.cpp kRedoOrder) with the same result; a bin of
+    <= 6144 clustered keys takes the LDS bitonic fallback inside the bin."""
+    t = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 14)
+    orc = OracleTree(64 << 20)
+    rng = np.random.default_rng(11)
+    for n in (12000, 5000, 16000):
+        ks = (np.arange(1, n + 1, dtype=U64) * U64(3))[rng.permutation(n)]
+        ks = np.concatenate([ks, ks[: n // 10]])                 # duplicates
+        vs = np.arange(1, ks.size + 1, dtype=U64) + U64(n << 20)
+        vs[rng.random(ks.size) < 0.03] = 0                         # deletes
+        gpu_insert(t, ks, vs)
+        orc.apply_batch(ks, vs)
+        probe = np.arange(0, 3 * n + 10, dtype=U64)
+        ov, of = orc.search_batch(probe)
+        gv, gf = gpu_search(t, probe)
+        assert_same(probe, ov, of, gv, gf)
+    t.check()
+    t.close()
+    orc.close()
