@@ -288,6 +288,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    host_issue = time.perf_counter() - t_start  # host time to issue the steps
     barrier()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
@@ -367,6 +368,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "host_issue_ms_per_step": round(host_issue / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

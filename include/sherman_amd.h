@@ -185,6 +185,10 @@ int shm_route_permute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
 /* out[perm[i]] = in[i] (reverse of the bucket permutation). */
 int shm_route_unpermute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
                         uint64_t n, uint64_t *out, void *stream);
+/* the same for routed get replies, with found_out[perm[i]] = in[i] != 0
+ * (Tree::search's bool, Tree.cpp:445-448) in the same pass */
+int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *perm,
+                              uint64_t n, uint64_t *out, uint8_t *found_out, void *stream);
 
 /* workload generators on device (test/benchmark.cpp:43-46, zipf.h) ----------- */
 /* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */

@@ -119,6 +119,7 @@ _SIGNATURES = [
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
     ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
+    ("shm_route_unpermute_found", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     ("shm_hash_keys", ctypes.c_int, [vp, vp, u64, u64, vp, vp]),
 ]
@@ -334,7 +335,12 @@ class Tree:
         _check(lib().shm_route_permute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
                                        _ptr(out), _stream_ptr(stream)), "permute")
 
-    def route_unpermute(self, vals_in, perm, out, stream=None):
+    def route_unpermute(self, vals_in, perm, out, stream=None, found=None):
+        if found is not None:  # found[perm[i]] = vals_in[i] != 0 in the same pass
+            _check(lib().shm_route_unpermute_found(self.h, _ptr(vals_in), _ptr(perm),
+                                                   vals_in.numel(), _ptr(out), _ptr(found),
+                                                   _stream_ptr(stream)), "unpermute")
+            return
         _check(lib().shm_route_unpermute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
                                          _ptr(out), _stream_ptr(stream)), "unpermute")
 

@@ -188,7 +188,7 @@ void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
 void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64_t* out,
                     hipStream_t s);
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
-                      uint64_t* out, hipStream_t s);
+                      uint64_t* out, uint8_t* found, hipStream_t s);
 // batched range scans (range.hip)
 struct RangeArgs {
   const uint8_t* arena;

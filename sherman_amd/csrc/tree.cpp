@@ -1488,7 +1488,15 @@ int shm_route_permute(shm_tree* t, const uint64_t* in, const uint32_t* perm,
 int shm_route_unpermute(shm_tree* t, const uint64_t* in, const uint32_t* perm,
                         uint64_t n, uint64_t* out, void* stream) {
   if (!t || (n && (!in || !perm || !out))) return SHM_EINVAL;
-  dev::launch_unpermute(in, perm, n, out, pick(t, stream));
+  dev::launch_unpermute(in, perm, n, out, nullptr, pick(t, stream));
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_route_unpermute_found(shm_tree* t, const uint64_t* in, const uint32_t* perm,
+                              uint64_t n, uint64_t* out, uint8_t* found_out, void* stream) {
+  if (!t || (n && (!in || !perm || !out || !found_out))) return SHM_EINVAL;
+  dev::launch_unpermute(in, perm, n, out, found_out, pick(t, stream));
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }

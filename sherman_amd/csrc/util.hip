@@ -309,14 +309,20 @@ void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64
   if (n) hipLaunchKernelGGL(k_permute, grid1(n), dim3(kT), 0, s, in, perm, n, out);
 }
 
+// found (nullable): found[perm[i]] = in[i] != kValueNull (Tree.cpp:445-448)
 __global__ void k_unpermute(const uint64_t* in, const uint32_t* perm,
-                            uint64_t n, uint64_t* out) {
+                            uint64_t n, uint64_t* out, uint8_t* found) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[perm[i]] = in[i];
+  if (i < n) {
+    const uint64_t v = in[i];
+    const uint32_t p = perm[i];
+    out[p] = v;
+    if (found) found[p] = v != kValueNull ? 1 : 0;
+  }
 }
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
-                      uint64_t* out, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_unpermute, grid1(n), dim3(kT), 0, s, in, perm, n, out);
+                      uint64_t* out, uint8_t* found, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_unpermute, grid1(n), dim3(kT), 0, s, in, perm, n, out, found);
 }
 
 }  // namespace dev

@@ -105,9 +105,9 @@ class ShardRouter:
         self.local.search_batch(recv, rv, rf)
         back = self._buf("back", n, torch.int64, dev)
         self._a2a(back, rv, cnt, rcnt)
-        self.local.route_unpermute(back, perm, vals_out)
-        # value 0 is kValueNull: found <=> value != 0 (Tree.cpp:445-448)
-        torch.ne(vals_out, 0, out=found_out)
+        # value 0 is kValueNull: found <=> value != 0 (Tree.cpp:445-448),
+        # written by the same un-permute pass
+        self.local.route_unpermute(back, perm, vals_out, found=found_out)
 
     def insert(self, keys, vals):
         """Batched insert (value 0 deletes) of this rank's (key, value) pairs."""

@@ -48,8 +48,10 @@ class OracleShard:
     def route_permute(self, vals, perm, out):
         out.copy_(vals[perm.long()])
 
-    def route_unpermute(self, vals, perm, out):
+    def route_unpermute(self, vals, perm, out, found=None):
         out[perm.long()] = vals
+        if found is not None:
+            torch.ne(out, 0, out=found)
 
     def search_batch(self, keys, vals_out, found_out):
         v, f = self.t.search_batch(keys.numpy().view(U64))
