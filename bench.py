@@ -211,15 +211,35 @@ def main():
             if sx is not None:
                 sx.wait_stream(torch.cuda.current_stream())
 
-        def step(i):
-            q = qs[i % N_BATCHES]
-            v, f = outs[i % nstr]
+        pend = {}
+        seq = [0]  # routed batches issued so far (all step loops)
+
+        def on(i):
             sx = streams[i % nstr]
+            return torch.cuda.stream(sx if sx is not None else torch.cuda.current_stream())
+
+        def step(i):
             if routes[0] is None:
-                tree.search_batch(q, v, f, stream=sx)
-            else:
-                with torch.cuda.stream(sx if sx is not None else torch.cuda.current_stream()):
-                    routes[i % nstr].search(q, v, f)
+                v, f = outs[i % nstr]
+                tree.search_batch(qs[i % N_BATCHES], v, f, stream=streams[i % nstr])
+                return
+            c = seq[0]
+            seq[0] += 1
+            v, f = outs[c % nstr]
+            if nstr == 1:
+                with on(c):
+                    routes[0].search(qs[c % N_BATCHES], v, f)
+                return
+            # N > 1, two streams: batch c + 1's bucketing and count exchange
+            # are issued before batch c's exchange and walk
+            # (ShardRouter.search_begin); each router serves every other batch
+            if c not in pend:
+                with on(c):
+                    pend[c] = routes[c % nstr].search_begin(qs[c % N_BATCHES])
+            with on(c + 1):
+                pend[c + 1] = routes[(c + 1) % nstr].search_begin(qs[(c + 1) % N_BATCHES])
+            with on(c):
+                routes[c % nstr].search_end(pend.pop(c), v, f)
     elif args.workload == "c5":
         from sherman_amd.shard import umin
         assert not sim, "--sim-world is a C2 option"
@@ -300,7 +320,8 @@ def main():
     mops = total_ops / elapsed / 1e6
     torch.cuda.synchronize()
     if args.workload == "c2":
-        hit_rate = float(outs[(args.steps - 1) % len(outs)][1].float().mean().item())
+        last = (args.steps - 1) if world == 1 else seq[0] - 1  # last routed batch ended
+        hit_rate = float(outs[last % len(outs)][1].float().mean().item())
     elif args.workload == "c5":
         c, _ = scan_out["r"]
         hit_rate = float(c.float().mean().item())  # mean values per scan

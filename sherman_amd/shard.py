@@ -83,7 +83,8 @@ class ShardRouter:
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def _bucket(self, keys):
+    def _bucket_async(self, keys):
+        """Bucket by owner and exchange the counts; nothing waits for them."""
         n, dev = keys.numel(), keys.device
         kb = self._buf("kb", n, torch.int64, dev)
         perm = self._buf("perm", n, torch.int32, dev)
@@ -91,12 +92,31 @@ class ShardRouter:
         self.local.route_bucket(keys, self.world, kb, perm, cnt)
         rcnt = self._buf("rcnt", self.world, torch.int64, dev)
         self._a2a(rcnt, cnt)
+        return kb, perm, cnt, rcnt
+
+    def _bucket(self, keys):
+        kb, perm, cnt, rcnt = self._bucket_async(keys)
         return kb, perm, cnt.tolist(), rcnt.tolist()
 
     def search(self, keys, vals_out, found_out):
         """Batched get of this rank's keys; results land in input order."""
+        self.search_end(self.search_begin(keys), vals_out, found_out)
+
+    def search_begin(self, keys):
+        """First half of search(): bucketing and the count exchange, issued
+        without waiting for them.  A pipelined caller begins batch i + 1
+        before it ends batch i, so batch i + 1's counts are on the host by
+        the time they are needed instead of queueing behind batch i's walk
+        (bench.py, N > 1).  Every rank must begin and end the same batches
+        in the same order (collectives)."""
+        return (keys,) + self._bucket_async(keys)
+
+    def search_end(self, pending, vals_out, found_out):
+        """Second half: key exchange, local batched get, value exchange,
+        un-permute into vals_out / found_out (input order)."""
+        keys, kb, perm, cnt_t, rcnt_t = pending
         n, dev = keys.numel(), keys.device
-        kb, perm, cnt, rcnt = self._bucket(keys)
+        cnt, rcnt = cnt_t.tolist(), rcnt_t.tolist()
         nrecv = sum(rcnt)
         recv = self._buf("recv", nrecv, torch.int64, dev)
         self._a2a(recv, kb, rcnt, cnt)

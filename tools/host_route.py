@@ -66,6 +66,33 @@ total = time.perf_counter() - t0
 print(f"router.search, 2 streams: host issue {issue / 50 * 1e6:.1f} us/step, "
       f"wall {total / 50 * 1e6:.1f} us/step", flush=True)
 
+# pipelined: batch i + 1 begun before batch i ends (bench.py at N > 1)
+pend = {0: None}
+
+
+def step3(i):
+    if pend.get(i) is None:
+        with torch.cuda.stream(streams[i & 1]):
+            pend[i] = routers[i & 1].search_begin(q)
+    with torch.cuda.stream(streams[(i + 1) & 1]):
+        pend[i + 1] = routers[(i + 1) & 1].search_begin(q)
+    with torch.cuda.stream(streams[i & 1]):
+        routers[i & 1].search_end(pend.pop(i), *outs[i & 1])
+
+
+for i in range(6):
+    step3(i)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(6, 56):
+    step3(i)
+issue = time.perf_counter() - t0
+torch.cuda.synchronize()
+total = time.perf_counter() - t0
+print(f"router pipelined, 2 streams: host issue {issue / 50 * 1e6:.1f} us/step, "
+      f"wall {total / 50 * 1e6:.1f} us/step", flush=True)
+pend.clear()
+
 # per-piece host cost of router.search (no device waits except tolist)
 import collections
 acc = collections.defaultdict(float)
