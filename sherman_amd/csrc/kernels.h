@@ -89,6 +89,9 @@ struct SegArgs {
   uint64_t* locks;
   uint32_t num_locks;
   uint64_t tag_base;
+  // per segment: 1 = its page's lock word was taken ahead by k_seg_fill
+  // (nullable: k_leaf_upsert takes the words itself)
+  const uint32_t* seg_lk;
   int level;
   int is_delete;
   int split_only;             // k_leaf_update: skip segments with P == 1
@@ -175,6 +178,22 @@ void launch_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev, u
 void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
                      const uint32_t* pos, uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
+// the same, also taking each segment's lock word (lane per segment,
+// atomicCAS(0 -> tag) on lock[CityHash64(page) % num_locks], bounded spin):
+// seg_lk[s] = 1 when held.  launch_seg_unlock releases them.
+struct SegLock {
+  uint64_t* locks;
+  uint32_t num_locks;
+  uint64_t tag;
+  uint32_t* seg_lk;
+  uint32_t* err;
+};
+void launch_seg_fill_lock(const uint64_t* page, const uint32_t* heads, const uint32_t* pos,
+                          uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
+                          uint64_t* seg_page, uint32_t* num_seg, const SegLock& lk,
+                          hipStream_t s);
+void launch_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev, uint64_t n_max,
+                       const SegLock& lk, hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
 void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_t* out,

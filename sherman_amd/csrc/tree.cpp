@@ -81,6 +81,7 @@ struct shm_tree {
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr,
            *seg_pbase = nullptr, *seg_ver = nullptr;
+  uint32_t* seg_lk = nullptr;  // lock words taken ahead per segment (k_seg_fill)
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   void* temp = nullptr;
   size_t temp_bytes = 0;
@@ -480,9 +481,22 @@ int locate_kernel() {
   return v;
 }
 
+dev::SegLock seg_lock(shm_tree* t) {
+  return dev::SegLock{t->locks, t->cfg.num_locks, (t->batches + 1) << 32, t->seg_lk, t->d_err};
+}
+
+// SHM_LOCK_AHEAD=0: k_leaf_upsert takes its lock words itself (A/B knob)
+bool lock_ahead() {
+  static const bool v = [] {
+    const char* e = getenv("SHM_LOCK_AHEAD");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return v;
+}
+
 int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                 uint64_t n_ops, int level, bool sync = true,
-                const uint64_t* n_dev = nullptr) {
+                const uint64_t* n_dev = nullptr, bool lock = false) {
   dev::WalkArgs w = walk_args(t);
   w.keys = op_key;
   w.n = n_ops;
@@ -510,8 +524,12 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   dev::launch_seg_heads(t->pages, n_ops, n_dev, t->heads, s);
   HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
-                       t->seg_page, d_ns, s);
+  if (lock)
+    dev::launch_seg_fill_lock(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
+                              t->seg_page, d_ns, seg_lock(t), s);
+  else
+    dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
+                         t->seg_page, d_ns, s);
   DBG(s, "seg_fill");
   if (!sync) return (int64_t)n_ops;  // an upper bound; the count stays on the device
   int rc = readback(t, s, d_ns, sizeof(uint32_t));
@@ -573,7 +591,8 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                     const uint64_t* op_val, uint64_t n_ops, int level,
                     bool is_delete, int out, const uint64_t* n_dev = nullptr) {
   const bool fast_leaf = level == 0 && !is_delete && use_fast_insert();
-  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf, n_dev);
+  const bool ahead = fast_leaf && lock_ahead();
+  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf, n_dev, ahead);
   if (ns < 0) return ns;
   if (ns == 0) return 0;
   dev::SegArgs a = seg_args(t);
@@ -600,8 +619,13 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
     // in-place segments are applied here; the rest go the k-way split path
     shm_tree::ProfRec* pi = t->prof_ins;
     if (pi && !pi->upsert_done) HIP_OK(hipEventRecord(pi->e[1], s));
+    if (ahead) a.seg_lk = t->seg_lk;
     dev::launch_leaf_upsert(a, s);
     DBG(s, "leaf_upsert");
+    if (ahead) {
+      dev::launch_seg_unlock(t->seg_page, a.num_seg_dev, a.num_seg, seg_lock(t), s);
+      DBG(s, "seg_unlock");
+    }
     if (pi && !pi->upsert_done) {
       HIP_OK(hipEventRecord(pi->e[2], s));
       pi->upsert_done = true;
@@ -843,7 +867,7 @@ void free_all(shm_tree* t) {
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_pbase); F(t->seg_ver);
+  F(t->seg_pbase); F(t->seg_ver); F(t->seg_lk);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
   F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir); F(t->gcount); F(t->bins);
   for (auto& r : t->prof_pending)
@@ -1028,6 +1052,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->seg_np, segcap);
   rc |= dalloc(&t->seg_pbase, segcap);
   rc |= dalloc(&t->seg_ver, segcap);
+  rc |= dalloc(&t->seg_lk, segcap);
   for (int i = 0; i < 2; ++i) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);
     rc |= dalloc(&t->sep_ptr[i], t->sep_cap);

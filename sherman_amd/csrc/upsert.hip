@@ -84,8 +84,12 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   const bool sl = lane < G && g0 + (uint64_t)lane < num_seg;
   const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
   const uint64_t page = sl ? a.seg_page[gs] : 0;
-  const bool pok = sl && ptr_ok(page, a.node, a.arena_bytes);
-  if (ballot(sl && !pok)) err |= kErrBadPtr;
+  const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
+  if (ballot(sl && !pgok)) err |= kErrBadPtr;
+  // lock words taken ahead (k_seg_fill, SegArgs.seg_lk): a segment whose
+  // word could not be taken is skipped (kErrLock is already set)
+  const bool pre = a.seg_lk != nullptr;
+  const bool pok = pgok && (!pre || a.seg_lk[gs] != 0);
   const uint32_t st = sl ? a.seg_start[gs] : 0u;
   const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
   // prefetch: lane li of group q holds op li of segment q (ops >= L are read
@@ -103,8 +107,8 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
   const uint32_t lw = pok ? lock_word(page, a.num_locks) : 0u;
   const unsigned long long tag = (unsigned long long)(a.tag_base + wid + 1);
   const uint64_t wantm = ballot(pok);
-  bool own = false, have = !pok;
-  if (pok) {
+  bool own = false, have = !pok || pre;
+  if (pok && !pre) {
     // lanes sharing a word: the first takes it, the others see our tag
     const unsigned long long o = atomicCAS(lk + lw, 0ull, tag);
     own = o == 0ull;
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
     a.seg_newpages[gq] = P - 1;
     a.seg_ver[gq] = live ? fver : ~0u;
   }
-  if (locked) release_words(lk, lw, wantm);
+  if (locked && !pre) release_words(lk, lw, wantm);  // else k_seg_unlock
   if (err) atomicOr(a.err, err);
 }
 

@@ -110,13 +110,34 @@ void launch_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev, u
 
 __global__ void k_seg_fill(const uint64_t* page, const uint32_t* heads,
                            const uint32_t* pos, uint64_t n, const uint64_t* n_dev,
-                           uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg) {
+                           uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
+                           SegLock lk) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t nv = dev_n(n_dev, n);
   if (i < nv && heads[i]) {
+    const uint64_t pg = page[i];
     seg_start[pos[i]] = (uint32_t)i;
-    seg_page[pos[i]] = page[i];
+    seg_page[pos[i]] = pg;
+    if (lk.locks) {
+      // lock_and_read_page's lock half (Tree.cpp:205-242, 851): every
+      // segment of the batch takes its word with the batch's tag (segments
+      // sharing a word share the hold: their pages differ); a word held by
+      // another owner is waited for, bounded
+      unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
+                              cityhash64_u64(pg) % lk.num_locks;
+      uint32_t ok = 0;
+      for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+        const unsigned long long o = atomicCAS(w, 0ull, (unsigned long long)lk.tag);
+        if (o == 0ull || o == lk.tag) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) atomicOr(lk.err, kErrLock);
+      lk.seg_lk[pos[i]] = ok;
+    }
   }
   if (i + 1 == nv) {
     const uint32_t ns = pos[i] + heads[i];
@@ -130,7 +151,29 @@ __global__ void k_seg_fill(const uint64_t* page, const uint32_t* heads,
 void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
                      const uint32_t* pos, uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
                      uint64_t* seg_page, uint32_t* num_seg, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_seg_fill, grid1(n), dim3(kT), 0, s, page, heads, pos, n, n_dev, seg_start, seg_page, num_seg);
+  launch_seg_fill_lock(page, heads, pos, n, n_dev, seg_start, seg_page, num_seg, SegLock{},
+                       s);
+}
+void launch_seg_fill_lock(const uint64_t* page, const uint32_t* heads, const uint32_t* pos,
+                          uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
+                          uint64_t* seg_page, uint32_t* num_seg, const SegLock& lk,
+                          hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_seg_fill, grid1(n), dim3(kT), 0, s, page, heads, pos, n, n_dev, seg_start, seg_page, num_seg, lk);
+}
+
+// unlock_addr (Tree.cpp:244-264) for every segment holding its word, after
+// the page writes of the kernels before it (a kernel boundary orders them)
+__global__ void k_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev,
+                             uint64_t n_max, SegLock lk) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_max || i >= (uint64_t)*num_seg_dev || !lk.seg_lk[i]) return;
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
+                          cityhash64_u64(seg_page[i]) % lk.num_locks;
+  __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+void launch_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev, uint64_t n_max,
+                       const SegLock& lk, hipStream_t s) {
+  if (n_max) hipLaunchKernelGGL(k_seg_unlock, grid1(n_max), dim3(kT), 0, s, seg_page, num_seg_dev, n_max, lk);
 }
 
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
