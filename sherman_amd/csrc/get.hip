@@ -330,6 +330,7 @@ void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s) {
   switch (get_cfg()) {
     case 414: launch_cfg<4, 1, 4>(a, waves, s); break;
     case 411: launch_cfg<4, 1, 1>(a, waves, s); break;
+    case 412: launch_cfg<4, 1, 2>(a, waves, s); break;
     case 214: launch_cfg<2, 1, 4>(a, waves, s); break;
     case 221: launch_cfg<2, 2, 1>(a, waves, s); break;
     case 224: launch_cfg<2, 2, 4>(a, waves, s); break;

@@ -24,6 +24,10 @@
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
 // k-way split path of insert.hip; seg_T / seg_ver feed that path exactly as
 // the plan kernel's outputs did.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "device_common.h"
 #include "kernels.h"
 #include "lds_dma.h"
@@ -54,116 +58,25 @@ __device__ __forceinline__ void release_words(unsigned long long* lk, uint32_t l
 
 }  // namespace
 
+// Apply one group of G staged pages (buf: G x 1 KB in LDS; slot s = lanes
+// [s L, s L + L)): versions and fences, the segment's ops in key order with
+// the reference's slot rule, the changed entries written back, and the
+// segment's split plan (seg_T / seg_P / seg_newpages / seg_ver).  page / pok
+// are valid in lanes s < G; qst / qen / pk / pv per slot group.  Returns the
+// error bits.
 template <int G>
-__global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
+__device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t* buf,
+                                                uint64_t g0, uint32_t num_seg, uint64_t page,
+                                                bool pok, bool locked, uint32_t qst,
+                                                uint32_t qen, uint64_t pk, uint64_t pv) {
   constexpr int L = kWave / G;                       // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;  // entries per lane
   constexpr int CD = kLeafEntry * E / 4;             // dwords per lane chunk
   constexpr uint64_t kGroupMask = L == 64 ? ~0ull : ((1ull << (L & 63)) - 1);
-  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * G * kPageDwords];
   const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
-  const uint64_t g0 = wid * G;
-  // the grid may be sized for an upper bound of the segment count
-  // an ordering error flagged on the device (kKeyMax in the batch, a bin
-  // too large) rejects the batch before anything is written: the host sees
-  // it at its next read-back and re-orders or returns SHM_EINVAL
-  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
-  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
-  if (g0 >= num_seg) {
-    // past the last segment: zero the new-page counts the host scans
-    if (lane < G && g0 + (uint64_t)lane < a.num_seg) a.seg_newpages[g0 + lane] = 0;
-    return;  // wave-uniform
-  }
-  const uint32_t* buf = &s_pg[wv * G * kPageDwords];
-  const uint32_t buf_lds = lds_addr_of(buf);
-  uint32_t err = 0;
-
-  // ---- slot s (lane s < G) = segment g0 + s --------------------------------
-  const bool sl = lane < G && g0 + (uint64_t)lane < num_seg;
-  const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
-  const uint64_t page = sl ? a.seg_page[gs] : 0;
-  const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
-  if (ballot(sl && !pgok)) err |= kErrBadPtr;
-  // lock words taken ahead (k_seg_fill, SegArgs.seg_lk): a segment whose
-  // word could not be taken is skipped (kErrLock is already set)
-  const bool pre = a.seg_lk != nullptr;
-  const bool pok = pgok && (!pre || a.seg_lk[gs] != 0);
-  const uint32_t st = sl ? a.seg_start[gs] : 0u;
-  const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
-  // prefetch: lane li of group q holds op li of segment q (ops >= L are read
-  // in the apply loop), so the loop below makes no global round trip for the
-  // first L ops; the loads overlap the lock and the page staging
   const int q = lane / L;
   const int li = lane % L;
-  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
-  const bool pf = (uint32_t)li < qen - qst;
-  const uint64_t pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
-  const uint64_t pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
-
-  // ---- lock -------------------------------------------------------------------
-  unsigned long long* lk = reinterpret_cast<unsigned long long*>(a.locks);
-  const uint32_t lw = pok ? lock_word(page, a.num_locks) : 0u;
-  const unsigned long long tag = (unsigned long long)(a.tag_base + wid + 1);
-  const uint64_t wantm = ballot(pok);
-  bool own = false, have = !pok || pre;
-  if (pok && !pre) {
-    // lanes sharing a word: the first takes it, the others see our tag
-    const unsigned long long o = atomicCAS(lk + lw, 0ull, tag);
-    own = o == 0ull;
-    have = own || o == tag;
-  }
-  bool locked = true;
-  if (ballot(!have)) {
-    release_words(lk, lw, ballot(own));
-    // one at a time, increasing word order
-    bool first = true;
-    uint32_t prev = 0;
-    for (int it = 0; it < G && locked; ++it) {
-      uint32_t best = ~0u;
-      bool found = false;
-      for (uint64_t r = wantm; r; r &= r - 1) {
-        const uint32_t w = rl32(lw, ctz64(r));
-        if ((first || w > prev) && (!found || w < best)) {
-          best = w;
-          found = true;
-        }
-      }
-      if (!found) break;
-      uint32_t ok = 0;
-      if (lane == 0) {
-        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-          if (atomicCAS(lk + best, 0ull, tag) == 0ull) {
-            ok = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      if (rl32(ok, 0) == 0) {
-        // give up: release the words below `best` and fail the group
-        uint64_t held = 0;
-        for (uint64_t r = wantm; r; r &= r - 1) {
-          const int s = ctz64(r);
-          if (!first && rl32(lw, s) <= prev) held |= 1ull << s;
-        }
-        release_words(lk, lw, held);
-        err |= kErrLock;
-        locked = false;
-      }
-      prev = best;
-      first = false;
-    }
-  }
-
-  // ---- stage the pages under the locks ---------------------------------------
-#pragma unroll
-  for (int s = 0; s < G; ++s)
-    glds16(a.arena + ga_offset(rl64(pok && locked ? page : 0, s)),
-           buf_lds + (uint32_t)(s * kPageSize));
-  wait_vm<0>();
-
+  uint32_t err = 0;
   // ---- per slot q: header, entries ---------------------------------------------
   const uint32_t* hp = buf + q * kPageDwords;
   const uint32_t h2 = hp[2], h3 = hp[3], h4 = hp[4], h7 = hp[7], h8 = hp[8], h9 = hp[9],
@@ -287,13 +200,240 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
     a.seg_newpages[gq] = P - 1;
     a.seg_ver[gq] = live ? fver : ~0u;
   }
+  return err;
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
+  constexpr int L = kWave / G;                       // lanes per page
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * G * kPageDwords];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
+  const uint64_t g0 = wid * G;
+  // the grid may be sized for an upper bound of the segment count
+  // an ordering error flagged on the device (kKeyMax in the batch, a bin
+  // too large) rejects the batch before anything is written: the host sees
+  // it at its next read-back and re-orders or returns SHM_EINVAL
+  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
+  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
+  if (g0 >= num_seg) {
+    // past the last segment: zero the new-page counts the host scans
+    if (lane < G && g0 + (uint64_t)lane < a.num_seg) a.seg_newpages[g0 + lane] = 0;
+    return;  // wave-uniform
+  }
+  const uint32_t* buf = &s_pg[wv * G * kPageDwords];
+  const uint32_t buf_lds = lds_addr_of(buf);
+  uint32_t err = 0;
+
+  // ---- slot s (lane s < G) = segment g0 + s --------------------------------
+  const bool sl = lane < G && g0 + (uint64_t)lane < num_seg;
+  const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
+  const uint64_t page = sl ? a.seg_page[gs] : 0;
+  const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
+  if (ballot(sl && !pgok)) err |= kErrBadPtr;
+  // lock words taken ahead (k_seg_fill, SegArgs.seg_lk): a segment whose
+  // word could not be taken is skipped (kErrLock is already set)
+  const bool pre = a.seg_lk != nullptr;
+  const bool pok = pgok && (!pre || a.seg_lk[gs] != 0);
+  const uint32_t st = sl ? a.seg_start[gs] : 0u;
+  const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
+  // prefetch: lane li of group q holds op li of segment q (ops >= L are read
+  // in the apply loop), so the loop below makes no global round trip for the
+  // first L ops; the loads overlap the lock and the page staging
+  const int q = lane / L;
+  const int li = lane % L;
+  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
+  const bool pf = (uint32_t)li < qen - qst;
+  const uint64_t pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
+  const uint64_t pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
+
+  // ---- lock -------------------------------------------------------------------
+  unsigned long long* lk = reinterpret_cast<unsigned long long*>(a.locks);
+  const uint32_t lw = pok ? lock_word(page, a.num_locks) : 0u;
+  const unsigned long long tag = (unsigned long long)(a.tag_base + wid + 1);
+  const uint64_t wantm = ballot(pok);
+  bool own = false, have = !pok || pre;
+  if (pok && !pre) {
+    // lanes sharing a word: the first takes it, the others see our tag
+    const unsigned long long o = atomicCAS(lk + lw, 0ull, tag);
+    own = o == 0ull;
+    have = own || o == tag;
+  }
+  bool locked = true;
+  if (ballot(!have)) {
+    release_words(lk, lw, ballot(own));
+    // one at a time, increasing word order
+    bool first = true;
+    uint32_t prev = 0;
+    for (int it = 0; it < G && locked; ++it) {
+      uint32_t best = ~0u;
+      bool found = false;
+      for (uint64_t r = wantm; r; r &= r - 1) {
+        const uint32_t w = rl32(lw, ctz64(r));
+        if ((first || w > prev) && (!found || w < best)) {
+          best = w;
+          found = true;
+        }
+      }
+      if (!found) break;
+      uint32_t ok = 0;
+      if (lane == 0) {
+        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+          if (atomicCAS(lk + best, 0ull, tag) == 0ull) {
+            ok = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (rl32(ok, 0) == 0) {
+        // give up: release the words below `best` and fail the group
+        uint64_t held = 0;
+        for (uint64_t r = wantm; r; r &= r - 1) {
+          const int s = ctz64(r);
+          if (!first && rl32(lw, s) <= prev) held |= 1ull << s;
+        }
+        release_words(lk, lw, held);
+        err |= kErrLock;
+        locked = false;
+      }
+      prev = best;
+      first = false;
+    }
+  }
+
+  // ---- stage the pages under the locks ---------------------------------------
+#pragma unroll
+  for (int s = 0; s < G; ++s)
+    glds16(a.arena + ga_offset(rl64(pok && locked ? page : 0, s)),
+           buf_lds + (uint32_t)(s * kPageSize));
+  wait_vm<0>();
+
+  err |= apply_group<G>(a, buf, g0, num_seg, page, pok, locked, qst, qen, pk, pv);
   if (locked && !pre) release_words(lk, lw, wantm);  // else k_seg_unlock
+  if (err) atomicOr(a.err, err);
+}
+
+// Software-pipelined variant for lock words taken ahead (SegArgs.seg_lk): a
+// grid of about one resident wave set; each wave loops over groups
+// w, w + W, ... and, while it applies group g from one LDS buffer, the pages
+// of group g + W are already landing in the other (LDS-DMA) and the segment
+// records of g + 2W and the ops of g + W are in flight.  Per group the wave
+// then pays about the apply time instead of two dependent HBM round trips.
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
+  constexpr int L = kWave / G;
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * 2 * G * kPageDwords];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
+  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
+  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
+  // the host scans a.num_seg (an upper bound) new-page counts
+  for (uint64_t i = (uint64_t)num_seg + w * kWave + (uint64_t)lane; i < a.num_seg; i += W * kWave)
+    a.seg_newpages[i] = 0;
+  const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
+  uint64_t g = w;
+  if (g >= ngroups) return;  // wave-uniform
+  const uint32_t* bufs = &s_pg[wv * 2 * G * kPageDwords];
+  const uint32_t bufs_lds = lds_addr_of(bufs);
+  const int q = lane / L;
+  const int li = lane % L;
+  uint32_t err = 0;
+
+  // segment record of group gg for lane s < G (raw loads, used later)
+  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en, uint32_t& lk) {
+    const bool sl = gg < ngroups && lane < G && gg * G + (uint64_t)lane < num_seg;
+    const uint64_t gs = sl ? gg * G + (uint64_t)lane : 0;
+    page = sl ? a.seg_page[gs] : 0;
+    st = sl ? a.seg_start[gs] : 0u;
+    en = sl ? a.seg_start[gs + 1] : 0u;
+    lk = sl ? a.seg_lk[gs] : 0u;
+  };
+  // a loaded record -> page validity, slot ranges, op prefetch, page DMAs
+  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t lk,
+                   uint32_t b, bool& pok, uint32_t& qst, uint32_t& qen, uint64_t& pk,
+                   uint64_t& pv) {
+    const bool sl = lane < G && gg * G + (uint64_t)lane < num_seg;
+    const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
+    if (ballot(sl && !pgok)) err |= kErrBadPtr;
+    pok = pgok && lk != 0;
+    qst = shfl32(st, q);
+    qen = shfl32(en, q);
+    const bool pf = (uint32_t)li < qen - qst;
+    pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
+    pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer b's reads are done
+#pragma unroll
+    for (int s = 0; s < G; ++s)
+      glds16(a.arena + ga_offset(rl64(pok ? page : 0, s)),
+             bufs_lds + (uint32_t)((b * G + s) * kPageSize));
+  };
+
+  uint64_t c_page, n_page;
+  uint32_t c_st, c_en, c_lk, n_st, n_en, n_lk;
+  bool c_pok;
+  uint32_t c_qst, c_qen;
+  uint64_t c_pk, c_pv;
+  rec(g, c_page, c_st, c_en, c_lk);
+  stage(g, c_page, c_st, c_en, c_lk, 0, c_pok, c_qst, c_qen, c_pk, c_pv);
+  rec(g + W, n_page, n_st, n_en, n_lk);
+  for (uint32_t it = 0;; ++it) {
+    wait_vm<0>();  // group g's pages and ops, group g + W's records
+    const uint32_t b = it & 1u;
+    const uint64_t gn = g + W;
+    bool x_pok = false;
+    uint32_t x_qst = 0, x_qen = 0;
+    uint64_t x_pk = 0, x_pv = 0;
+    uint64_t m_page = 0;
+    uint32_t m_st = 0, m_en = 0, m_lk = 0;
+    if (gn < ngroups) {  // wave-uniform
+      stage(gn, n_page, n_st, n_en, n_lk, b ^ 1u, x_pok, x_qst, x_qen, x_pk, x_pv);
+      rec(gn + W, m_page, m_st, m_en, m_lk);
+    }
+    err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok, true,
+                          c_qst, c_qen, c_pk, c_pv);
+    if (gn >= ngroups) break;
+    g = gn;
+    c_page = n_page;
+    c_pok = x_pok;
+    c_qst = x_qst;
+    c_qen = x_qen;
+    c_pk = x_pk;
+    c_pv = x_pv;
+    n_page = m_page;
+    n_st = m_st;
+    n_en = m_en;
+    n_lk = m_lk;
+  }
   if (err) atomicOr(a.err, err);
 }
 
 void launch_leaf_upsert(const SegArgs& a, hipStream_t s) {
   constexpr int G = 4;
   if (!a.num_seg) return;
+  // SHM_UPSERT_PIPE=0: one group per wave even with the lock words taken ahead
+  static const bool pipe = [] {
+    const char* e = getenv("SHM_UPSERT_PIPE");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  if (pipe && a.seg_lk) {
+    static const unsigned blocks = [] {
+      int per_cu = 0, cus = 0, dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_leaf_upsert_pipe<G>,
+                                                          kBlock, 0);
+      return (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
+    }();
+    const uint64_t groups = (a.num_seg + G - 1) / G;
+    const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, blocks)),
+                       dim3(kBlock), 0, s, a);
+    return;
+  }
   const uint64_t waves = (a.num_seg + G - 1) / G;
   hipLaunchKernelGGL(k_leaf_upsert<G>, dim3((unsigned)((waves + kWavesPerBlock - 1) /
                                                        kWavesPerBlock)),
