@@ -87,6 +87,9 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   } else if (a.start) {
     ptr = a.start[k >> a.start_shift];
   }
+  // occupancy bound of my page (kLeafHwFull after a move: read it whole)
+  uint32_t hw = kLeafHwFull;
+  if (a.leaf_hw && ptr_ok(ptr, a.node, a.arena_bytes)) hw = a.leaf_hw[ga_offset(ptr) >> 10];
   // kKeyMax can never be stored (root highest is exclusive, Tree.h:150)
   bool done = !active || k == kKeyMax;
   uint64_t val = 0;
@@ -132,14 +135,21 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 #pragma unroll
       for (int s = 0; s < G; ++s) {
         uint64_t off = 0;
+        int nl = 1;  // padding: the superblock's first and last lanes
         if (hi) {
-          off = ga_offset(rl64(pload, ctz64(hi)));
+          const int h = ctz64(hi);
+          off = ga_offset(rl64(pload, h));
+          nl = hw_dma_lanes(rl32(hw, h));
           hi &= hi - 1;
         }
-        if (a.nt)
-          glds16_nt(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
-        else
-          glds16(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+        // lanes past the page's last occupied slot skip their 16 B (the
+        // last lane, rear_version, always loads: every DMA counts in vmcnt)
+        if (lane < nl || lane == 63) {
+          if (a.nt)
+            glds16_nt(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+          else
+            glds16(a.arena + off, ring_lds + (uint32_t)((b * G + s) * kPageSize));
+        }
       }
     };
 #pragma unroll
@@ -180,6 +190,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
       uint32_t D[CD];
       int hsrc = hq[0];
       uint64_t kq = 0;
+      uint32_t hwq = kLeafHwFull;  // slots of page q that were loaded
       if constexpr (!LOC) {
         const uint32_t* ep = buf + q * kPageDwords + chunk_dw;
 #pragma unroll
@@ -187,6 +198,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 #pragma unroll
         for (int s = 1; s < G; ++s) hsrc = q == s ? hq[s] : hsrc;
         kq = shfl64(k, hsrc < 63 ? hsrc : 63);
+        hwq = shfl32(hw, hsrc < 63 ? hsrc : 63);
       }
 
       const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
@@ -233,6 +245,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
         }
         const uint64_t child = lds_u64(lp, 13 + 4 * (pos > 0 ? pos - 1 : 0));
         ptr = qint ? (pos == 0 ? leftmost : child) : ptr;
+        hw = qint ? kLeafHwFull : hw;
       }
 
       // ---- leaf pages: lane groups hold the entries -----------------------
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 #pragma unroll
         for (int j = 0; j < E; ++j)
           eok[j] = evalue[j] != kValueNull && ((efr[j] ^ erv[j]) & 0xF) == 0 &&
-                   ebase + j >= li * E;
+                   ebase + j >= li * E && (uint32_t)(ebase + j) < hwq;
         const int tl = lane - myhead;  // my position in my run
         const int sl = slot & (G - 1);
         for (int t = 0;; ++t) {
@@ -272,6 +285,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
       }
 
       ptr = right ? sibling : ptr;
+      hw = right ? kLeafHwFull : hw;
       done = done || (inq && !pok) || low || (right && sibling == 0) || qleaf ||
              (qint && ptr == 0);
       if (!refilled && g + NB < ng) {

@@ -179,6 +179,7 @@ __device__ void build_leaf_page(const SegArgs& a, WaveLds& L, uint32_t g,
   if ((uint32_t)lane < c) put_leaf_entry(L.page, lane, key, val, ver & 0xFF, ver >> 8);
   if (lane == 0) L.page[kOffLeafRear / 4] = fver;  // rear_version, byte 1016
   store_page(a.arena, ga_offset(page_ga), L.page);
+  if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(page_ga) >> 10] = (uint8_t)c;  // slots [0, c)
   if (p > 0 && lane == 0) {
     const uint64_t o = a.seg_pbase[g] + (uint64_t)(p - 1);
     a.sep_key[o] = lowest;
@@ -366,6 +367,9 @@ __global__ __launch_bounds__(kBlock) void k_leaf_update(SegArgs a) {
     wave_lds_sync();
     if (dirty) put_leaf_entry(L.page, lane, e.key, e.val, e.fraw, e.rraw);
     store_page(a.arena, ga_offset(page), L.page);
+    const uint64_t vm = ballot(slot && e.val != kValueNull);
+    if (a.leaf_hw && lane == 0)
+      a.leaf_hw[ga_offset(page) >> 10] = (uint8_t)(vm ? 64 - __builtin_clzll(vm) : 0);
   } else {
     const int na = leaf_survivors(a, L, st, en);
     build_leaf_page(a, L, g, h, na, 0, P, a.seg_T[g], page);

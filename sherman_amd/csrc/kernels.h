@@ -38,6 +38,11 @@ struct WalkArgs {
   int nt;
   // diagnostics (nullable): per wave {start, end} s_memrealtime stamps
   uint64_t* stamps;
+  // GET: per-page occupancy bound (nullable -> whole pages are read).  For a
+  // leaf, every slot >= leaf_hw[page] is empty (value 0), so its page DMA
+  // stops after that slot; kLeafHwFull (internal pages, pages of a loaded
+  // image) reads the whole page
+  const uint8_t* leaf_hw;
 };
 
 void launch_walk(const WalkArgs& a, uint64_t n_upper, int depth, bool locate,
@@ -96,6 +101,8 @@ struct SegArgs {
   int is_delete;
   int split_only;             // k_leaf_update: skip segments with P == 1
   uint32_t* err;
+  // per-page occupancy bound kept by every leaf writer (see WalkArgs)
+  uint8_t* leaf_hw;
 };
 
 void launch_leaf_plan(const SegArgs& a, hipStream_t s);

@@ -53,6 +53,17 @@ static_assert(kOffRecords + kInternalCardinality * kInternalEntry ==
 static_assert(kOffRecords + kLeafCardinality * kLeafEntry == kOffLeafRear,
               "leaf layout");
 
+// Per-page occupancy bound (a side array, not part of the page bytes): for a
+// leaf, every slot >= hw holds value 0 (empty, Tree.cpp:881), so a reader may
+// stop its page read after slot hw - 1.  kLeafHwFull = unknown (internal
+// pages, pages of a loaded image): read the whole page.
+constexpr uint8_t kLeafHwFull = 0xFF;
+// 16 B lanes of a page DMA covering the header and slots [0, hw); the last
+// lane (rear_version, byte 1016) is loaded as well
+SHM_HD int hw_dma_lanes(uint32_t hw) {
+  return hw >= (uint32_t)kLeafCardinality ? 64 : (kOffRecords + kLeafEntry * (int)hw + 15) / 16;
+}
+
 // GlobalAddress{nodeID:16, offset:48} (include/GlobalAddress.h:7-16).
 // nodeID = GPU / shard id, offset = byte offset into that GPU's page arena.
 SHM_HD uint64_t ga_make(uint16_t node, uint64_t off) {

@@ -81,6 +81,7 @@ struct shm_tree {
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr,
            *seg_pbase = nullptr, *seg_ver = nullptr;
+  uint8_t* leaf_hw = nullptr;   // per-page occupancy bound (layout.h kLeafHwFull)
   uint32_t* seg_lk = nullptr;  // lock words taken ahead per segment (k_seg_fill)
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   void* temp = nullptr;
@@ -340,6 +341,15 @@ dev::WalkArgs walk_args(shm_tree* t) {
   return a;
 }
 
+// SHM_LEAF_HW=0: gets read whole leaves (A/B knob; the bound is kept anyway)
+bool use_leaf_hw() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_LEAF_HW");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // SHM_FAST_INSERT=0 selects the page-at-a-time locate walk and the
 // plan / update leaf kernels instead of the grouped locate + k_leaf_upsert
 bool use_fast_insert() {
@@ -403,6 +413,7 @@ dev::SegArgs seg_args(shm_tree* t) {
   a.num_locks = t->cfg.num_locks;
   a.tag_base = (t->batches + 1) << 32;
   a.err = t->d_err;
+  a.leaf_hw = t->leaf_hw;
   return a;
 }
 
@@ -867,7 +878,7 @@ void free_all(shm_tree* t) {
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_pbase); F(t->seg_ver); F(t->seg_lk);
+  F(t->seg_pbase); F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
   F(t->temp); F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->start); F(t->dir); F(t->gcount); F(t->bins);
   for (auto& r : t->prof_pending)
@@ -1053,6 +1064,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->seg_pbase, segcap);
   rc |= dalloc(&t->seg_ver, segcap);
   rc |= dalloc(&t->seg_lk, segcap);
+  rc |= dalloc(&t->leaf_hw, t->cap_pages);
   for (int i = 0; i < 2; ++i) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);
     rc |= dalloc(&t->sep_ptr[i], t->sep_cap);
@@ -1085,7 +1097,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->d_err, 0, 16, s) ||
       hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->gws[1].S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
-      hipMemsetAsync(t->arena, 0, kPageSize, s))
+      hipMemsetAsync(t->arena, 0, kPageSize, s) ||
+      hipMemsetAsync(t->leaf_hw, kLeafHwFull, t->cap_pages, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
   t->next_page = 1;
@@ -1192,6 +1205,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.perm = nullptr;
     }
     a.nt = walk_nt();
+    a.leaf_hw = use_leaf_hw() ? t->leaf_hw : nullptr;
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
     if (get_kernel_v4()) {
       dev::launch_walk(a, m, kWalkDepth, false, s);
@@ -1433,6 +1447,8 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   if (ro < kPageSize || ro + kPageSize > bytes) return SHM_EINVAL;
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemcpy(t->arena, host_buf, bytes, hipMemcpyHostToDevice));
+  // occupancy unknown for the loaded pages: whole-page reads until rewritten
+  HIP_OK(hipMemset(t->leaf_hw, kLeafHwFull, t->cap_pages));
   t->root = root_ptr;
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;

@@ -191,6 +191,19 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
       if (dirty[j])
         put_leaf_entry(reinterpret_cast<uint32_t*>(pg), ebase + j, ek[j], ev[j], ef[j], er[j]);
   }
+  if (a.leaf_hw) {
+    // the page's occupancy bound after the batch: 1 + its last valid slot
+    uint32_t hw = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (valid[j]) hw = (uint32_t)(ebase + j + 1);
+#pragma unroll
+    for (int m = L / 2; m > 0; m >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)hw, m);
+      hw = o > hw ? o : hw;
+    }
+    if (live && !over && li == 0) a.leaf_hw[ga_offset(qpage) >> 10] = (uint8_t)hw;
+  }
   const uint64_t gq = g0 + (uint64_t)q;
   if (li == 0 && q < G && gq >= num_seg && gq < a.num_seg) a.seg_newpages[gq] = 0;
   if (li == 0 && q < G && gq < num_seg) {
