@@ -562,3 +562,39 @@ def test_insert_bin_overflow_reorders(lib_ok):
     t.check()
     t.close()
     orc.close()
+
+
+@pytest.mark.parametrize("from_image", [False, True])
+def test_leaf_occupancy_bound_with_holes(lib_ok, from_image):
+    """Gets read a leaf only up to its occupancy bound (leaf_hw, layout.h):
+    leaves with deleted slots below and above the last valid one, slots
+    reused by later inserts, pages rewritten by splits, and pages of a loaded
+    image (bound unknown until first rewritten) all answer as the oracle."""
+    rng = np.random.default_rng(77 + int(from_image))
+    universe = hashed_keys(1, 40001)
+    orc = OracleTree(256 << 20)
+    orc.apply_batch(universe, universe + U64(3))
+    dels = universe[rng.random(universe.size) < 0.5]
+    orc.apply_batch(dels, np.zeros(dels.size, dtype=U64))
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16)
+    if from_image:
+        t.load_image(orc.image(), orc.root_ptr)
+    else:
+        gpu_insert(t, universe, universe + U64(3))
+        gpu_insert(t, dels, np.zeros(dels.size, dtype=U64))
+    probe = np.concatenate([universe, hashed_keys(50001, 52001)])
+    for r in range(6):
+        ov, of = orc.search_batch(probe)
+        gv, gf = gpu_search(t, probe)
+        assert_same(probe, ov, of, gv, gf)
+        # re-insert deleted keys (hole reuse), add new keys (slots past the
+        # old bound, splits), delete the highest-slot keys of some leaves
+        ks = np.concatenate([dels[rng.integers(0, dels.size, 3000)],
+                             hashed_keys(60001 + 4000 * r, 62001 + 4000 * r),
+                             universe[rng.integers(0, universe.size, 2000)]])
+        vs = rng.integers(1, 1 << 62, ks.size).astype(U64)
+        vs[-2000:][rng.random(2000) < 0.5] = 0
+        gpu_insert(t, ks, vs)
+        orc.apply_batch(ks, vs)
+    compare_contents(t, orc)
+    t.close()
