@@ -201,6 +201,18 @@ void launch_seg_fill_lock(const uint64_t* page, const uint32_t* heads, const uin
                           hipStream_t s);
 void launch_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev, uint64_t n_max,
                        const SegLock& lk, hipStream_t s);
+// Segmentation in two launches instead of heads + library scan + fill: per
+// 1024-op tile a head count (bsum), then each tile sums the counts before it
+// and fills its segments (lock words as launch_seg_fill_lock when lk.locks).
+// bsum holds seg_tiles(n) words.
+constexpr uint32_t kSegTile = 1024;
+inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
+void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
+                    const SegLock& lk, hipStream_t s);
+// out = exclusive scan of in[0, n) in the same two-launch form
+void launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* bsum,
+                     hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
 void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_t* out,

@@ -77,6 +77,7 @@ struct shm_tree {
   uint64_t *uk = nullptr, *uv = nullptr, *dk = nullptr;
   uint64_t* pages = nullptr;
   uint32_t *heads = nullptr, *hpos = nullptr;
+  uint32_t* bsum = nullptr;  // per-tile sums of the two-launch scans
   uint32_t* seg_start = nullptr;
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr,
@@ -350,6 +351,15 @@ bool use_leaf_hw() {
   return on;
 }
 
+// SHM_TILE_SCAN=0: segmentation and the new-page scan through rocPRIM
+bool use_tile_scan() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_TILE_SCAN");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // SHM_FAST_INSERT=0 selects the page-at-a-time locate walk and the
 // plan / update leaf kernels instead of the grouped locate + k_leaf_upsert
 bool use_fast_insert() {
@@ -532,15 +542,20 @@ int64_t segment(shm_tree* t, hipStream_t s, const uint64_t* op_key,
     dev::launch_walk(w, n_ops, 4, true, s);
   }
   DBG(s, "walk(locate)");
-  dev::launch_seg_heads(t->pages, n_ops, n_dev, t->heads, s);
-  HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  if (lock)
-    dev::launch_seg_fill_lock(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
-                              t->seg_page, d_ns, seg_lock(t), s);
-  else
-    dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
-                         t->seg_page, d_ns, s);
+  if (use_tile_scan()) {
+    dev::launch_segment(t->pages, n_ops, n_dev, t->bsum, t->seg_start, t->seg_page, d_ns,
+                        lock ? seg_lock(t) : dev::SegLock{}, s);
+  } else {
+    dev::launch_seg_heads(t->pages, n_ops, n_dev, t->heads, s);
+    HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->heads, t->hpos, n_ops, s));
+    if (lock)
+      dev::launch_seg_fill_lock(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
+                                t->seg_page, d_ns, seg_lock(t), s);
+    else
+      dev::launch_seg_fill(t->pages, t->heads, t->hpos, n_ops, n_dev, t->seg_start,
+                           t->seg_page, d_ns, s);
+  }
   DBG(s, "seg_fill");
   if (!sync) return (int64_t)n_ops;  // an upper bound; the count stays on the device
   int rc = readback(t, s, d_ns, sizeof(uint32_t));
@@ -563,8 +578,11 @@ int64_t plan_level(shm_tree* t, hipStream_t s, dev::SegArgs& a, bool leaf,
 
 // scan seg_newpages into seg_pbase and read back the level's new-page total
 int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t reserve) {
-  HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
-                                 a.num_seg, s));
+  if (use_tile_scan())
+    dev::launch_scan_u32(t->seg_np, t->seg_pbase, a.num_seg, t->bsum, s);
+  else
+    HIP_OK(dev::exclusive_scan_u32(t->temp, t->temp_bytes, t->seg_np, t->seg_pbase,
+                                   a.num_seg, s));
   // total = pbase[last] + np[last]; with the error word, the device-side
   // segment count and the ordering's (upserts, deletes) in one read-back
   uint32_t* d_tot = reinterpret_cast<uint32_t*>(t->d_counts + 16);
@@ -876,7 +894,7 @@ void free_all(shm_tree* t) {
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
-  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos);
+  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos); F(t->bsum);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
@@ -1056,6 +1074,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->pages, segcap);
   rc |= dalloc(&t->heads, segcap);
   rc |= dalloc(&t->hpos, segcap);
+  rc |= dalloc(&t->bsum, dev::seg_tiles(segcap) + 1);
   rc |= dalloc(&t->seg_start, segcap + 1);
   rc |= dalloc(&t->seg_page, segcap);
   rc |= dalloc(&t->seg_T, segcap);

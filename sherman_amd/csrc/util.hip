@@ -176,6 +176,164 @@ void launch_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev, ui
   if (n_max) hipLaunchKernelGGL(k_seg_unlock, grid1(n_max), dim3(kT), 0, s, seg_page, num_seg_dev, n_max, lk);
 }
 
+// ---- two-launch tile scans ---------------------------------------------------
+// A tile is kSegTile = 1024 elements, 4 consecutive per thread of a 256-thread
+// block.  Pass 1 stores each tile's sum; pass 2 adds the sums of the tiles
+// before it (<= n / 1024 words, read by the whole block) to a block scan.  No
+// look-back state to initialise, no temp storage, two launches in all.
+namespace {
+constexpr int kScanPer = (int)kSegTile / kT;
+static_assert(kScanPer * kT == (int)kSegTile, "tile shape");
+
+// exclusive scan of v over the block's 256 threads; *total = the block sum
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t ws[kT / kWave];
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+    if (lane_id() >= off) incl += y;
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == kWave - 1) ws[w] = incl;
+  __syncthreads();
+  uint32_t base = 0, sum = 0;
+#pragma unroll
+  for (int i = 0; i < kT / kWave; ++i) {
+    base += i < w ? ws[i] : 0u;
+    sum += ws[i];
+  }
+  __syncthreads();
+  *total = sum;
+  return base + incl - v;
+}
+
+// sum of bsum[0, b) by the whole block
+__device__ __forceinline__ uint32_t tiles_before(const uint32_t* bsum, uint32_t b) {
+  uint32_t v = 0;
+  for (uint32_t j = threadIdx.x; j < b; j += kT) v += bsum[j];
+  uint32_t total;
+  (void)block_scan(v, &total);
+  return total;
+}
+
+__device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, uint64_t nv) {
+  return i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
+}
+}  // namespace
+
+__global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t n,
+                                                  const uint64_t* n_dev, uint32_t* bsum) {
+  const uint64_t nv = dev_n(n_dev, n);
+  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) c += seg_head(page, i0 + j, nv);
+  uint32_t total;
+  (void)block_scan(c, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// seg_start / seg_page of every head; lock words as k_seg_fill
+__global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint64_t n,
+                                                      const uint64_t* n_dev,
+                                                      const uint32_t* bsum, uint32_t* seg_start,
+                                                      uint64_t* seg_page, uint32_t* num_seg,
+                                                      SegLock lk) {
+  const uint64_t nv = dev_n(n_dev, n);
+  const uint32_t prefix = tiles_before(bsum, blockIdx.x);
+  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t h[kScanPer], c = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    h[j] = seg_head(page, i0 + j, nv);
+    c += h[j];
+  }
+  uint32_t total;
+  uint32_t pos = prefix + block_scan(c, &total);
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    const uint64_t i = i0 + j;
+    if (h[j]) {
+      const uint64_t pg = page[i];
+      seg_start[pos] = (uint32_t)i;
+      seg_page[pos] = pg;
+      if (lk.locks) {
+        // lock_and_read_page's lock half (Tree.cpp:205-242, 851), as k_seg_fill
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
+                                cityhash64_u64(pg) % lk.num_locks;
+        uint32_t ok = 0;
+        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+          const unsigned long long o = atomicCAS(w, 0ull, (unsigned long long)lk.tag);
+          if (o == 0ull || o == lk.tag) {
+            ok = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) atomicOr(lk.err, kErrLock);
+        lk.seg_lk[pos] = ok;
+      }
+    }
+    pos += h[j];
+    if (i + 1 == nv) {
+      *num_seg = pos;
+      seg_start[pos] = (uint32_t)nv;
+    }
+  }
+  if (nv == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    *num_seg = 0;
+    seg_start[0] = 0;
+  }
+}
+
+void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
+                    const SegLock& lk, hipStream_t s) {
+  if (!n) return;
+  const dim3 g((unsigned)seg_tiles(n));
+  hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum);
+  hipLaunchKernelGGL(k_seg_fill_scan, g, dim3(kT), 0, s, page, n, n_dev, (const uint32_t*)bsum,
+                     seg_start, seg_page, num_seg, lk);
+}
+
+__global__ __launch_bounds__(kT) void k_tile_sum(const uint32_t* in, uint64_t n, uint32_t* bsum) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) c += i0 + j < n ? in[i0 + j] : 0u;
+  uint32_t total;
+  (void)block_scan(c, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kT) void k_tile_scan(const uint32_t* in, uint64_t n,
+                                                  const uint32_t* bsum, uint32_t* out) {
+  const uint32_t prefix = tiles_before(bsum, blockIdx.x);
+  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t v[kScanPer], c = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    v[j] = i0 + j < n ? in[i0 + j] : 0u;
+    c += v[j];
+  }
+  uint32_t total;
+  uint32_t pos = prefix + block_scan(c, &total);
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    if (i0 + j < n) out[i0 + j] = pos;
+    pos += v[j];
+  }
+}
+
+void launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* bsum,
+                     hipStream_t s) {
+  if (!n) return;
+  const dim3 g((unsigned)seg_tiles(n));
+  hipLaunchKernelGGL(k_tile_sum, g, dim3(kT), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_tile_scan, g, dim3(kT), 0, s, in, n, (const uint32_t*)bsum, out);
+}
+
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
 __global__ void k_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                            uint64_t* out) {
