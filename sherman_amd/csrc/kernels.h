@@ -213,6 +213,10 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
 // out = exclusive scan of in[0, n) in the same two-launch form
 void launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* bsum,
                      hipStream_t s);
+// the same over u64 (bsum: seg_tiles(n) words); tot = {total, *err} for the
+// range scan's one read-back
+void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,
+                           const uint32_t* err, uint64_t* tot, hipStream_t s);
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,
                      uint64_t* out, hipStream_t s);
 void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_t* out,

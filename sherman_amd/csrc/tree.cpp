@@ -78,6 +78,7 @@ struct shm_tree {
   uint64_t* pages = nullptr;
   uint32_t *heads = nullptr, *hpos = nullptr;
   uint32_t* bsum = nullptr;  // per-tile sums of the two-launch scans
+  uint64_t* bsum64 = nullptr;
   uint32_t* seg_start = nullptr;
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr,
@@ -894,7 +895,7 @@ void free_all(shm_tree* t) {
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->flags); F(t->pos);
-  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos); F(t->bsum);
+  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->heads); F(t->hpos); F(t->bsum); F(t->bsum64);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_pbase); F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); }
@@ -1075,6 +1076,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->heads, segcap);
   rc |= dalloc(&t->hpos, segcap);
   rc |= dalloc(&t->bsum, dev::seg_tiles(segcap) + 1);
+  rc |= dalloc(&t->bsum64, dev::seg_tiles(n) + 1);
   rc |= dalloc(&t->seg_start, segcap + 1);
   rc |= dalloc(&t->seg_page, segcap);
   rc |= dalloc(&t->seg_T, segcap);
@@ -1391,10 +1393,15 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
     const uint64_t m = std::min(t->nmax, n - off);
     int rc = range_launch(t, s, rargs(off, m, nullptr, nullptr));
     if (rc) return rc;
-    HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, counts_out + off,
-                                   offsets_out + off, m, s));
-    dev::launch_range_total(offsets_out + off, counts_out + off, m, t->d_err,
-                            t->d_counts + 12, s);
+    if (use_tile_scan()) {
+      dev::launch_scan_u64_total(counts_out + off, offsets_out + off, m, t->bsum64, t->d_err,
+                                 t->d_counts + 12, s);
+    } else {
+      HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, counts_out + off,
+                                     offsets_out + off, m, s));
+      dev::launch_range_total(offsets_out + off, counts_out + off, m, t->d_err,
+                              t->d_counts + 12, s);
+    }
     rc = readback(t, s, t->d_counts + 12, 2 * sizeof(uint64_t));
     if (rc) return rc;
     if (t->h_pin[1]) return check_err(t, s);

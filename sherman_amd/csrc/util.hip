@@ -186,21 +186,22 @@ constexpr int kScanPer = (int)kSegTile / kT;
 static_assert(kScanPer * kT == (int)kSegTile, "tile shape");
 
 // exclusive scan of v over the block's 256 threads; *total = the block sum
-__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* total) {
-  __shared__ uint32_t ws[kT / kWave];
-  uint32_t incl = v;
+template <class T>
+__device__ __forceinline__ T block_scan(T v, T* total) {
+  __shared__ T ws[kT / kWave];
+  T incl = v;
 #pragma unroll
   for (int off = 1; off < kWave; off <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+    const T y = __shfl_up(incl, off);
     if (lane_id() >= off) incl += y;
   }
   const int w = threadIdx.x / kWave;
   if (lane_id() == kWave - 1) ws[w] = incl;
   __syncthreads();
-  uint32_t base = 0, sum = 0;
+  T base = 0, sum = 0;
 #pragma unroll
   for (int i = 0; i < kT / kWave; ++i) {
-    base += i < w ? ws[i] : 0u;
+    base += i < w ? ws[i] : T(0);
     sum += ws[i];
   }
   __syncthreads();
@@ -209,10 +210,11 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* total) {
 }
 
 // sum of bsum[0, b) by the whole block
-__device__ __forceinline__ uint32_t tiles_before(const uint32_t* bsum, uint32_t b) {
-  uint32_t v = 0;
+template <class T>
+__device__ __forceinline__ T tiles_before(const T* bsum, uint32_t b) {
+  T v = 0;
   for (uint32_t j = threadIdx.x; j < b; j += kT) v += bsum[j];
-  uint32_t total;
+  T total;
   (void)block_scan(v, &total);
   return total;
 }
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) c += seg_head(page, i0 + j, nv);
   uint32_t total;
-  (void)block_scan(c, &total);
+  (void)block_scan<uint32_t>(c, &total);
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
                                                       uint64_t* seg_page, uint32_t* num_seg,
                                                       SegLock lk) {
   const uint64_t nv = dev_n(n_dev, n);
-  const uint32_t prefix = tiles_before(bsum, blockIdx.x);
+  const uint32_t prefix = tiles_before<uint32_t>(bsum, blockIdx.x);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint32_t h[kScanPer], c = 0;
 #pragma unroll
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
     c += h[j];
   }
   uint32_t total;
-  uint32_t pos = prefix + block_scan(c, &total);
+  uint32_t pos = prefix + block_scan<uint32_t>(c, &total);
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = i0 + j;
@@ -297,32 +299,39 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                      seg_start, seg_page, num_seg, lk);
 }
 
-__global__ __launch_bounds__(kT) void k_tile_sum(const uint32_t* in, uint64_t n, uint32_t* bsum) {
+template <class T>
+__global__ __launch_bounds__(kT) void k_tile_sum(const T* in, uint64_t n, T* bsum) {
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  uint32_t c = 0;
+  T c = 0;
 #pragma unroll
-  for (int j = 0; j < kScanPer; ++j) c += i0 + j < n ? in[i0 + j] : 0u;
-  uint32_t total;
+  for (int j = 0; j < kScanPer; ++j) c += i0 + j < n ? in[i0 + j] : T(0);
+  T total;
   (void)block_scan(c, &total);
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kT) void k_tile_scan(const uint32_t* in, uint64_t n,
-                                                  const uint32_t* bsum, uint32_t* out) {
-  const uint32_t prefix = tiles_before(bsum, blockIdx.x);
+// tot (nullable): {out[n-1] + in[n-1], *err} from the thread holding n - 1
+template <class T>
+__global__ __launch_bounds__(kT) void k_tile_scan(const T* in, uint64_t n, const T* bsum, T* out,
+                                                  const uint32_t* err, uint64_t* tot) {
+  const T prefix = tiles_before(bsum, blockIdx.x);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  uint32_t v[kScanPer], c = 0;
+  T v[kScanPer], c = 0;
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
-    v[j] = i0 + j < n ? in[i0 + j] : 0u;
+    v[j] = i0 + j < n ? in[i0 + j] : T(0);
     c += v[j];
   }
-  uint32_t total;
-  uint32_t pos = prefix + block_scan(c, &total);
+  T total;
+  T pos = prefix + block_scan(c, &total);
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     if (i0 + j < n) out[i0 + j] = pos;
     pos += v[j];
+    if (tot && i0 + j + 1 == n) {
+      tot[0] = (uint64_t)pos;
+      tot[1] = *err;
+    }
   }
 }
 
@@ -330,8 +339,19 @@ void launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* bs
                      hipStream_t s) {
   if (!n) return;
   const dim3 g((unsigned)seg_tiles(n));
-  hipLaunchKernelGGL(k_tile_sum, g, dim3(kT), 0, s, in, n, bsum);
-  hipLaunchKernelGGL(k_tile_scan, g, dim3(kT), 0, s, in, n, (const uint32_t*)bsum, out);
+  hipLaunchKernelGGL(k_tile_sum<uint32_t>, g, dim3(kT), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_tile_scan<uint32_t>, g, dim3(kT), 0, s, in, n, (const uint32_t*)bsum, out,
+                     (const uint32_t*)nullptr, (uint64_t*)nullptr);
+}
+
+void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,
+                           const uint32_t* err, uint64_t* tot, hipStream_t s) {
+  if (!n) return;
+  const dim3 g((unsigned)seg_tiles(n));
+  using U = unsigned long long;
+  hipLaunchKernelGGL(k_tile_sum<U>, g, dim3(kT), 0, s, (const U*)in, n, (U*)bsum);
+  hipLaunchKernelGGL(k_tile_scan<U>, g, dim3(kT), 0, s, (const U*)in, n, (const U*)bsum,
+                     (U*)out, err, tot);
 }
 
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
