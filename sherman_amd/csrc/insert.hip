@@ -424,6 +424,12 @@ __global__ __launch_bounds__(kBlock) void k_int_plan(SegArgs a) {
   const int lane = lane_id();
   const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (g >= a.num_seg) return;
+  // a.num_seg may be an upper bound (num_seg_dev): zero the new-page counts
+  // past the device-side count, which the scan after this kernel covers
+  if (a.num_seg_dev && g >= *a.num_seg_dev) {
+    if (lane == 0) a.seg_newpages[g] = 0;
+    return;
+  }
   const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
   const uint64_t page = a.seg_page[g];
   if (!ptr_ok(page, a.node, a.arena_bytes)) {

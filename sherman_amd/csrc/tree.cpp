@@ -361,6 +361,15 @@ bool use_tile_scan() {
   return on;
 }
 
+// SHM_INT_DEV_COUNT=0: internal levels read their segment count back
+bool int_dev_count() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_INT_DEV_COUNT");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // SHM_FAST_INSERT=0 selects the page-at-a-time locate walk and the
 // plan / update leaf kernels instead of the grouped locate + k_leaf_upsert
 bool use_fast_insert() {
@@ -622,7 +631,11 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
                     bool is_delete, int out, const uint64_t* n_dev = nullptr) {
   const bool fast_leaf = level == 0 && !is_delete && use_fast_insert();
   const bool ahead = fast_leaf && lock_ahead();
-  const int64_t ns = segment(t, s, op_key, n_ops, level, !fast_leaf, n_dev, ahead);
+  // internal levels keep the segment count on the device too: the plan
+  // kernel checks it and the new-page read-back returns it (one read-back
+  // per level instead of two)
+  const bool fast_int = level > 0 && use_fast_insert() && int_dev_count();
+  const int64_t ns = segment(t, s, op_key, n_ops, level, !(fast_leaf || fast_int), n_dev, ahead);
   if (ns < 0) return ns;
   if (ns == 0) return 0;
   dev::SegArgs a = seg_args(t);
@@ -630,7 +643,7 @@ int64_t apply_level(shm_tree* t, hipStream_t s, const uint64_t* op_key,
   a.op_val = op_val;
   a.n_ops = n_ops;
   a.num_seg = (uint32_t)ns;
-  if (fast_leaf) a.num_seg_dev = reinterpret_cast<const uint32_t*>(t->d_counts + 8);
+  if (fast_leaf || fast_int) a.num_seg_dev = reinterpret_cast<const uint32_t*>(t->d_counts + 8);
   t->err_pending = true;
   a.level = level;
   a.is_delete = is_delete ? 1 : 0;
