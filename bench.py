@@ -421,6 +421,14 @@ def main():
                 "walk_ms_per_launch": round(walk_ms, 4),
                 "order_ms_per_launch": round(order_ms, 4),
                 "queries_per_launch": int(q_per_launch),
+                # measured HBM bytes (PMC, profiles/pmc_walk.json) per get and
+                # as a rate over the walk; the reference's root-to-leaf path
+                # reads 5 x 1024 B + 16 B per get, for context
+                "traffic_per_get": (round(traffic / q_per_launch, 1)
+                                    if traffic and q_per_launch else None),
+                "traffic_GBps": (round(traffic / (walk_ms * 1e-3) / 1e9, 1)
+                                 if traffic and walk_ms else None),
+                "full_path_bytes_per_get": 5136,
             },
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
