@@ -266,12 +266,17 @@ bool get_kernel_v4() {
 // SHM_WALK_NT=0/1: leaf-page DMAs of the get walk with the default or the
 // non-temporal cache policy (A/B knob; default 1: a leaf is read once per
 // batch, and nt keeps it from displacing the directory: C2 +5 %)
-int walk_nt() {
+// leaf DMA policy: ordered walks read each leaf once per batch (queries
+// sharing it sit in one wave), so non-temporal loads keep the directory in
+// L2 (C2 +5 %); an unordered walk reads a leaf once per wave that needs it,
+// and under skew (C3, zipf 0.99) the cached policy serves the repeats from
+// L2 (walk -9 %).  SHM_WALK_NT=0/1 forces either.
+int walk_nt(bool ordered) {
   static const int v = [] {
     const char* e = getenv("SHM_WALK_NT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : -1;
   }();
-  return v;
+  return v >= 0 ? v : (ordered ? 1 : 0);
 }
 
 // SHM_DEFER_COUNTS=0 reads the insert ordering's counts back before the
@@ -1238,7 +1243,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
       a.keys = keys + off;
       a.perm = nullptr;
     }
-    a.nt = walk_nt();
+    a.nt = walk_nt(gathered || a.perm != nullptr);
     a.leaf_hw = use_leaf_hw() ? t->leaf_hw : nullptr;
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
     if (get_kernel_v4()) {
