@@ -37,7 +37,11 @@ for f in ("bench_c2.json", "bench_c3.json", "bench_c5.json", "pytest_gpu.log", "
         continue
     if f == "bench_c2.json":
         d = json.loads(open(src).read())
-        d["roofline"]["traffic"] = pmc["hbm_bytes_per_launch"]
+        r = d["roofline"]
+        r["traffic"] = pmc["hbm_bytes_per_launch"]
+        if r.get("queries_per_launch") and r.get("walk_ms_per_launch"):
+            r["traffic_per_get"] = round(r["traffic"] / r["queries_per_launch"], 1)
+            r["traffic_GBps"] = round(r["traffic"] / (r["walk_ms_per_launch"] * 1e-3) / 1e9, 1)
         open(os.path.join(dst, f), "w").write(json.dumps(d) + "\n")
     else:
         shutil.copy(src, os.path.join(dst, f))
