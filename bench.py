@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--sort", choices=("auto", "on", "off"), default="auto",
                    help="order get batches by key before the walk: always "
                         "(SHM_FLAG_SORT_GETS), never, or when dense (default)")
+    p.add_argument("--sync-scans", dest="async_scans", action="store_false",
+                   help="c5, N=1: range scans read their total back before the "
+                        "batch's inserts are queued (default: async, checked after)")
     p.add_argument("--profile-steps", type=int, default=10)
     p.add_argument("--streams", type=int, default=2, choices=(1, 2),
                    help="c2, N=1: consecutive batches alternate over this many HIP "
@@ -241,6 +244,7 @@ def main():
             with on(c):
                 routes[c % nstr].search_end(pend.pop(c), v, f)
     elif args.workload == "c5":
+        from sherman_amd import PendingRange
         from sherman_amd.shard import umin
         assert not sim, "--sim-world is a C2 option"
         n_glob = n_keys * world
@@ -266,11 +270,18 @@ def main():
 
         def step(i):
             lo, hi, pk, pv = mixed[i % N_BATCHES]
-            if route is None:
-                scan_out["r"] = tree.range_query_batch(lo, hi)
+            if route is None and args.async_scans:
+                # scans queued without a host wait; the batch's inserts queue
+                # behind them; every step's total is checked after the run
+                scan_out["r"] = pr = tree.range_query_batch_async(lo, hi)
+                if pr.tot is not None:  # only the (total, error) words stay alive
+                    scan_out.setdefault("all", []).append((pr.tot, pr.vals.numel()))
+                tree.insert_batch(pk, pv)
+            elif route is None:
+                scan_out["r"] = PendingRange(None, *tree.range_query_batch(lo, hi))
                 tree.insert_batch(pk, pv)
             else:
-                scan_out["r"] = route.range_query(lo, hi)
+                scan_out["r"] = PendingRange(None, *route.range_query(lo, hi))
                 route.insert(pk, pv)
     else:
         zipf = Zipf(n_keys, args.theta, dev)
@@ -323,7 +334,11 @@ def main():
         last = (args.steps - 1) if world == 1 else seq[0] - 1  # last routed batch ended
         hit_rate = float(outs[last % len(outs)][1].float().mean().item())
     elif args.workload == "c5":
-        c, _ = scan_out["r"]
+        for tot, cap in scan_out.pop("all", []):
+            total, err = (int(x) for x in tot.cpu().tolist())
+            # every timed step's values fit its buffer, with no device error
+            assert err == 0 and total <= cap, (total, cap, err)
+        c, _ = scan_out["r"].result()
         hit_rate = float(c.float().mean().item())  # mean values per scan
     else:
         n_get = mixed[(args.steps - 1) % N_BATCHES][0].numel()
@@ -527,7 +542,7 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
         if b < 2:
             step(b)
             torch.cuda.synchronize()
-            gc, gv = scan_out["r"]
+            gc, gv = scan_out["r"].result()
             gc = gc.cpu().numpy()
             gv = gv.cpu().numpy().view(np.uint64)
             goff = np.concatenate([[0], np.cumsum(gc)])

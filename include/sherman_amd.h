@@ -132,6 +132,17 @@ int shm_range_query_batch(shm_tree *t, const uint64_t *from, const uint64_t *to,
                           uint64_t n, uint64_t *counts_out, uint64_t *offsets_out,
                           uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_out,
                           void *stream);
+/* The same scans without a host synchronisation, for one chunk (n <=
+ * cfg.max_batch): total_dev (device, 2 words) receives the total and the
+ * device error bits when the call completes on `stream`; values at output
+ * index >= vals_cap are dropped, so the caller compares total_dev[0] with
+ * vals_cap when it reads the result (the reference leaves sizing the buffer
+ * to the caller too, Tree.cpp:513, 532).  Lets a caller queue further work
+ * (e.g. the batch's inserts) behind the scans without waiting for them. */
+int shm_range_query_batch_async(shm_tree *t, const uint64_t *from, const uint64_t *to,
+                                uint64_t n, uint64_t *counts_out, uint64_t *offsets_out,
+                                uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_dev,
+                                void *stream);
 
 /* introspection / images (host pointers) ------------------------------------- */
 int shm_stats(shm_tree *t, shm_stats_t *out);

@@ -109,6 +109,8 @@ _SIGNATURES = [
     ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
     ("shm_range_query_batch", ctypes.c_int,
      [vp, vp, vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
+    ("shm_range_query_batch_async", ctypes.c_int,
+     [vp, vp, vp, u64, vp, vp, vp, u64, vp, vp]),
     ("shm_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmStats)]),
     ("shm_dump_image", ctypes.c_int, [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
@@ -173,6 +175,37 @@ def _stream_ptr(stream):
     if isinstance(stream, int):
         return stream or None
     return stream.cuda_stream or None
+
+
+class PendingRange:
+    """Result of Tree.range_query_batch_async: (counts, values) once the
+    scans have run.  tot = device (total, error bits)."""
+
+    def __init__(self, tree, counts, vals, tot=None, stream=None):
+        self.tree, self.counts, self.vals, self.tot, self.stream = tree, counts, vals, tot, stream
+
+    def result(self):
+        if self.tot is None:  # ran synchronously
+            return self.counts, self.vals
+        import torch
+        s = self.stream
+        if s is None:
+            torch.cuda.current_stream().synchronize()
+        elif hasattr(s, "synchronize"):
+            s.synchronize()
+        else:  # a raw hipStream_t
+            torch.cuda.synchronize()
+        total, err = (int(x) for x in self.tot.cpu().tolist())
+        if err:
+            self.tree.synchronize()  # raises the device error
+            raise ShermanError(SHM_EIO, "range_query_batch_async")
+        if total > self.vals.numel():
+            raise ShermanError(SHM_ENOSPC, "range_query_batch_async: %d values, buffer %d"
+                               % (total, self.vals.numel()))
+        self.tree._rq_cap = max(self.tree._rq_cap, total + total // 4)
+        self.tot = None
+        self.vals = self.vals[:total]
+        return self.counts, self.vals
 
 
 class Tree:
@@ -255,6 +288,29 @@ class Tree:
         _check(rc, "range_query_batch")
         self._rq_cap = max(cap, total + total // 4)
         return counts, vals[:total]
+
+    def range_query_batch_async(self, lo, hi, stream=None):
+        """range_query_batch without the host synchronisation (n <= max_batch):
+        the scans are queued on `stream` and the returned PendingRange gives
+        (counts, values) on .result().  The value buffer is sized from earlier
+        totals (the first call on a handle runs synchronously to learn one);
+        .result() raises SHM_ENOSPC if this batch's total outgrew it, which
+        cannot be redone after later mutating calls."""
+        import torch
+        cap = getattr(self, "_rq_cap", None)
+        if cap is None:
+            return PendingRange(None, *self.range_query_batch(lo, hi, stream))
+        n = lo.numel()
+        dev = lo.device
+        counts = torch.empty(n, dtype=torch.int64, device=dev)
+        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        vals = torch.empty(cap, dtype=torch.int64, device=dev)
+        tot = torch.empty(2, dtype=torch.int64, device=dev)
+        _check(lib().shm_range_query_batch_async(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
+                                                 _ptr(offs), _ptr(vals), cap, _ptr(tot),
+                                                 _stream_ptr(stream)),
+               "range_query_batch_async")
+        return PendingRange(self, counts, vals, tot, stream)
 
     # -- reference single-op API (Tree.h:47-54) -------------------------------
     def _dev(self, name, n):

@@ -254,6 +254,9 @@ struct RangeArgs {
   // there instead of walking their leaves again
   uint64_t* stage;
   uint32_t stage_cap;
+  // fill pass: values at output index >= vals_cap are dropped (the async
+  // batch call writes before the host knows the total; it reports the total)
+  uint64_t vals_cap;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // out[0] = offsets[n-1] + counts[n-1], out[1] = *err  (n >= 1)

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
   if (a.offsets && stq && a.counts[q] <= a.stage_cap) {
     // fill pass, staged scan: copy its values out, no second walk
     const uint64_t c = a.counts[q];
-    for (uint64_t i = (uint64_t)lane; i < c; i += kWave) a.vals[out + i] = stq[i];
+    for (uint64_t i = (uint64_t)lane; i < c && out + i < a.vals_cap; i += kWave)
+      a.vals[out + i] = stq[i];
     return;
   }
   if (lo <= hi) {
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
                        (e.fraw & 0xF) == (e.rraw & 0xF) && e.key >= lo && e.key <= hi;
       const uint64_t m = ballot(hit);
       const uint64_t slot = cnt + popc64(m & lanemask_lt());
-      if (a.offsets && hit) a.vals[out + slot] = e.val;
+      if (a.offsets && hit && out + slot < a.vals_cap) a.vals[out + slot] = e.val;
       if (!a.offsets && stq && hit && slot < a.stage_cap) stq[slot] = e.val;
       cnt += popc64(m);
       wave_lds_sync();  // LDS reads done before the next stage

@@ -1323,6 +1323,7 @@ dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to,
   a.offsets = offsets;
   a.vals = vals;
   a.err = t->d_err;
+  a.vals_cap = ~0ull;
   if (use_leaf_dir(t)) {
     a.dir = t->dir;
     a.dir_lo = t->cfg.key_lo;
@@ -1344,6 +1345,24 @@ int range_launch(shm_tree* t, hipStream_t s, const dev::RangeArgs& a) {
   if (t->prof_on) {
     HIP_OK(hipEventRecord(pr.e[1], s));
     t->prof_pending.push_back(pr);
+  }
+  return SHM_OK;
+}
+
+// one-chunk batches whose staging fits kRangeStageBytes keep up to
+// kRangeStage values per scan from the count pass for the fill pass
+int range_stage(shm_tree* t, hipStream_t s, uint64_t n, bool* staged) {
+  *staged = n <= t->nmax && n * kRangeStage * 8 <= kRangeStageBytes;
+  if (*staged && t->rstage_words < n * kRangeStage) {
+    if (t->rstage) {
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipFree(t->rstage));
+      t->rstage = nullptr;
+      t->rstage_words = 0;
+    }
+    const uint64_t words = std::max<uint64_t>(n, 1u << 14) * kRangeStage;
+    if (dalloc(&t->rstage, words)) return SHM_ENOMEM;
+    t->rstage_words = words;
   }
   return SHM_OK;
 }
@@ -1387,18 +1406,8 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
   // staging fits kRangeStageBytes keeps its values for pass 2.
   uint64_t total = 0;
   std::vector<uint64_t> base;
-  const bool staged = n <= t->nmax && n * kRangeStage * 8 <= kRangeStageBytes;
-  if (staged && t->rstage_words < n * kRangeStage) {
-    if (t->rstage) {
-      HIP_OK(hipStreamSynchronize(s));
-      HIP_OK(hipFree(t->rstage));
-      t->rstage = nullptr;
-      t->rstage_words = 0;
-    }
-    const uint64_t words = std::max<uint64_t>(n, 1u << 14) * kRangeStage;
-    if (dalloc(&t->rstage, words)) return SHM_ENOMEM;
-    t->rstage_words = words;
-  }
+  bool staged = false;
+  if (const int rc = range_stage(t, s, n, &staged)) return rc;
   auto rargs = [&](uint64_t off, uint64_t m, const uint64_t* offs, uint64_t* vals) {
     dev::RangeArgs a = range_args(t, from + off, to + off, m, counts_out + off, offs, vals);
     if (staged) {
@@ -1442,6 +1451,51 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
   }
   t->err_pending = true;
   return SHM_OK;
+}
+
+int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_t* to,
+                                uint64_t n, uint64_t* counts_out, uint64_t* offsets_out,
+                                uint64_t* vals_out, uint64_t vals_cap, uint64_t* total_dev,
+                                void* stream) {
+  if (!t || !total_dev || (n && (!from || !to || !counts_out || !offsets_out)))
+    return SHM_EINVAL;
+  if (vals_cap && !vals_out) return SHM_EINVAL;
+  if (n > t->nmax) return SHM_EINVAL;  // one chunk: offsets need no host-side base
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(t, stream);
+  Order ord(t, s, true);
+  if (ord.rc) return ord.rc;
+  if (n == 0) {
+    HIP_OK(hipMemsetAsync(total_dev, 0, 2 * sizeof(uint64_t), s));
+    return SHM_OK;
+  }
+  if (use_leaf_dir(t)) {
+    const int rc = refresh_dir(t, s);
+    if (rc) return rc;
+  }
+  bool staged = false;
+  if (const int rc = range_stage(t, s, n, &staged)) return rc;
+  dev::RangeArgs a = range_args(t, from, to, n, counts_out, nullptr, nullptr);
+  if (staged) {
+    a.stage = t->rstage;
+    a.stage_cap = kRangeStage;
+  }
+  t->err_pending = true;
+  int rc = range_launch(t, s, a);
+  if (rc) return rc;
+  // count pass -> offsets and (total, error word) into total_dev, then the
+  // fill pass bounded by vals_cap; no host synchronisation
+  if (use_tile_scan()) {
+    dev::launch_scan_u64_total(counts_out, offsets_out, n, t->bsum64, t->d_err, total_dev, s);
+  } else {
+    HIP_OK(dev::exclusive_scan_u64(t->temp, t->temp_bytes, counts_out, offsets_out, n, s));
+    dev::launch_range_total(offsets_out, counts_out, n, t->d_err, total_dev, s);
+  }
+  if (!vals_cap) return SHM_OK;
+  a.offsets = offsets_out;
+  a.vals = vals_out;
+  a.vals_cap = vals_cap;
+  return range_launch(t, s, a);
 }
 
 int shm_stats(shm_tree* t, shm_stats_t* o) {

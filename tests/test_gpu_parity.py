@@ -243,6 +243,59 @@ def test_range_query_vs_oracle(lib_ok, max_batch, cap, leaf_dir):
     t.close()
 
 
+def test_range_query_async_matches_sync_and_reports_overflow(lib_ok):
+    """shm_range_query_batch_async: the scans queued before an insert see the
+    pre-insert tree and equal the synchronous call's (counts and values in the
+    same order); a buffer smaller than the total drops the values past it
+    (nothing is written out of bounds) and .result() raises SHM_ENOSPC."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 14)
+    ks = hashed_keys(1, 40001)
+    gpu_insert(t, ks, ks + U64(3))
+    rng = np.random.default_rng(11)
+    lo = rng.integers(0, 1 << 63, 500, dtype=np.uint64) * U64(2)
+    hi = lo + (U64(1) << U64(52)) * rng.integers(0, 8, 500).astype(U64)
+    hi[hi < lo] = U64((1 << 64) - 1)
+    lo[1], hi[1] = U64(5), U64(4)  # empty (from > to)
+    sc, sv = t.range_query_batch(dev(lo), dev(hi))
+    alo, ahi = dev(lo), dev(hi)
+    pend = t.range_query_batch_async(alo, ahi)
+    assert pend.tot is not None  # the handle knows a buffer size: really async
+    # an insert queued behind the scans (new keys inside their ranges)
+    newk = lo[2:200] + U64(1)
+    gpu_insert(t, newk, newk + U64(3))
+    ac, av = pend.result()
+    assert np.array_equal(ac.cpu().numpy(), sc.cpu().numpy())
+    assert np.array_equal(host(av), host(sv))
+    total = int(sc.sum().item())
+    assert total > 64
+    # overflow: a 64-value buffer inside a larger allocation, guard words intact
+    t._rq_cap = 64
+    n = lo.size
+    guard = torch.full((total + 64,), 0x5A5A, dtype=torch.int64, device="cuda")
+    counts = torch.empty(n, dtype=torch.int64, device="cuda")
+    offs = torch.empty(n, dtype=torch.int64, device="cuda")
+    tot = torch.empty(2, dtype=torch.int64, device="cuda")
+    dlo, dhi = dev(lo), dev(hi)  # kept alive while the scans run
+    rc = shm.lib().shm_range_query_batch_async(t.h, dlo.data_ptr(), dhi.data_ptr(), n,
+                                               counts.data_ptr(), offs.data_ptr(),
+                                               guard.data_ptr(), 64, tot.data_ptr(), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(tot[1].item()) == 0 and int(tot[0].item()) >= total
+    assert bool((guard[64:] == 0x5A5A).all().item())
+    pend = shm.PendingRange(t, counts, guard[:64], tot)
+    with pytest.raises(shm.ShermanError):
+        pend.result()
+    # more scans than one chunk is refused
+    big = torch.zeros((1 << 14) + 1, dtype=torch.int64, device="cuda")
+    rc = shm.lib().shm_range_query_batch_async(t.h, big.data_ptr(), big.data_ptr(), big.numel(),
+                                               big.data_ptr(), big.data_ptr(), None, 0,
+                                               tot.data_ptr(), None)
+    assert rc == shm.SHM_EINVAL
+    t.check()
+    t.close()
+
+
 def test_edge_cases(lib_ok):
     t = shm.Tree(arena_bytes=32 << 20, max_batch=4096)
     # empty batches
