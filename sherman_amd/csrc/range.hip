@@ -140,6 +140,23 @@ void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s) {
   hipLaunchKernelGGL(k_gather_u32, dim3(1), dim3(64), 0, s, dst, g);
 }
 
+// zero-copy read-back (tree.cpp readback): one wave copies the words into
+// mapped host memory with vector stores, fences at system scope, then lane 0
+// publishes the sequence number the host spins on
+__global__ void k_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
+                           uint32_t seq) {
+  const uint32_t l = threadIdx.x;
+  if (l < nw) dst[l] = src[l];
+  __threadfence_system();
+  __syncthreads();
+  if (l == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
+                     uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, dst, src, nw, flag, seq);
+}
+
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += c;

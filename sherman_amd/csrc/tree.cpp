@@ -58,7 +58,9 @@ struct shm_tree {
   // route_bucket scratch per stream (route_scratch serves the first one), so
   // routed batches on distinct streams bucket concurrently
   std::vector<std::pair<hipStream_t, uint32_t*>> route_ws;
-  uint64_t* h_pin = nullptr;     // 16 words pinned host scratch
+  uint64_t* h_pin = nullptr;     // 16 words pinned host scratch (coherent, mapped)
+  uint32_t* h_pin_dev = nullptr; // its device address (zero-copy read-backs)
+  uint32_t rb_seq = 0;           // last zero-copy read-back sequence number
   uint64_t rb_nup = 0, rb_ndel = 0;  // ordering counts of the last read-back
   uint64_t* rstage = nullptr;    // range-scan value staging (RangeArgs.stage)
   uint64_t rstage_words = 0;
@@ -466,11 +468,43 @@ int dbg(hipStream_t s, const char* what) {
     if (_r) return _r;                 \
   } while (0)
 
-// read `n` device words into pinned host scratch and wait
+// SHM_ZC_READBACK=0: read-backs as a D2H copy + stream synchronisation
+bool use_zc_readback() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_ZC_READBACK");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+// read `bytes` (<= 128) of device words into pinned host scratch and wait.
+// Zero-copy: a one-wave kernel stores the words straight into the mapped,
+// coherent host page, then a sequence number after a system-scope fence;
+// the host spins on that word instead of a D2H copy (an SDMA/blit round
+// trip) and a stream synchronisation.  While spinning it polls the stream,
+// so a fault in an earlier kernel (which would keep the word from ever
+// arriving) still returns SHM_EIO.
 int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
-  HIP_OK(hipMemcpyAsync(t->h_pin, src, bytes, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-  return SHM_OK;
+  if (!use_zc_readback()) {
+    HIP_OK(hipMemcpyAsync(t->h_pin, src, bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return SHM_OK;
+  }
+  const uint32_t seq = ++t->rb_seq;
+  constexpr uint32_t kFlagWord = 512;  // byte 2048 of the 4 KB page
+  dev::launch_readback(t->h_pin_dev, static_cast<const uint32_t*>(src),
+                       (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, s);
+  HIP_OK(hipGetLastError());
+  const uint32_t* flag = reinterpret_cast<const uint32_t*>(t->h_pin) + kFlagWord;
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return SHM_OK;
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e != hipSuccess && e != hipErrorNotReady) return SHM_EIO;
+      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) return SHM_EIO;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // superblock mirror (layout.h), written by a one-wave kernel: stream-ordered,
@@ -1130,7 +1164,11 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   t->temp_bytes = std::max(dev::sort_pairs_temp_bytes(n),
                            dev::scan_temp_bytes_max(segcap));
   if (hipMalloc(&t->temp, t->temp_bytes) != hipSuccess) return fail(SHM_ENOMEM);
-  if (hipHostMalloc((void**)&t->h_pin, 4096, 0) != hipSuccess) return fail(SHM_ENOMEM);
+  if (hipHostMalloc((void**)&t->h_pin, 4096, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&t->h_pin_dev, t->h_pin, 0) != hipSuccess)
+    return fail(SHM_ENOMEM);
+  memset(t->h_pin, 0, 4096);
   hipStream_t s = t->stream;
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
