@@ -158,6 +158,13 @@ int shm_load_image(shm_tree *t, const void *host_buf, uint64_t bytes,
 int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
               uint64_t *n_keys);
 int shm_synchronize(shm_tree *t);
+/* Copy `bytes` (a multiple of 4, <= 256) of device memory at `src` to
+ * host_out once the work queued on `stream` before it has produced them,
+ * through the library's zero-copy read-back (one-wave kernel into mapped
+ * host memory + a spin on a sequence word) instead of a D2H copy and a stream
+ * synchronisation.  Used by the shard router for the RCCL split sizes. */
+int shm_read_words(shm_tree *t, const void *src, uint64_t bytes, void *host_out,
+                   void *stream);
 
 /* per-kernel timing with HIP events recorded on the launch stream around the
  * hot path's phases (get: order = top-bits sort, walk = the page walk kernel;

@@ -116,6 +116,7 @@ _SIGNATURES = [
     ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
     ("shm_check", ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_synchronize", ctypes.c_int, [vp]),
+    ("shm_read_words", ctypes.c_int, [vp, vp, u64, vp, vp]),
     ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
@@ -382,6 +383,17 @@ class Tree:
         return {f: getattr(p, f) for f, _ in ShmProfile._fields_}
 
     # -- routing / generators ---------------------------------------------------
+    def read_i64(self, t, stream=None):
+        """A small device int64 tensor (<= 32 words) as a list of ints, via
+        the zero-copy read-back (shm_read_words); CPU tensors via tolist()."""
+        if t.device.type != "cuda":
+            return t.tolist()
+        n = t.numel()
+        buf = (ctypes.c_int64 * n)()
+        _check(lib().shm_read_words(self.h, _ptr(t), 8 * n, buf, _stream_ptr(stream)),
+               "read_words")
+        return list(buf)
+
     def route_bucket(self, keys, num_shards, keys_out, perm_out, counts_out, stream=None):
         _check(lib().shm_route_bucket(self.h, _ptr(keys), keys.numel(), num_shards,
                                       _ptr(counts_out), _ptr(keys_out), _ptr(perm_out),

@@ -271,7 +271,7 @@ struct Gather8 {
 };
 // dst[i] = *g.p[i], i < g.n
 void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s);
-// dst[i] = src[i] for i < nw (<= 32, dst in mapped host memory), then a
+// dst[i] = src[i] for i < nw (<= 64, dst in mapped host memory), then a
 // system-scope release store of seq to *flag
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
                      uint32_t seq, hipStream_t s);

@@ -477,7 +477,7 @@ bool use_zc_readback() {
   return on;
 }
 
-// read `bytes` (<= 128) of device words into pinned host scratch and wait.
+// read `bytes` (<= 256) of device words into pinned host scratch and wait.
 // Zero-copy: a one-wave kernel stores the words straight into the mapped,
 // coherent host page, then a sequence number after a system-scope fence;
 // the host spins on that word instead of a D2H copy (an SDMA/blit round
@@ -493,7 +493,7 @@ int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
   const uint32_t seq = ++t->rb_seq;
   constexpr uint32_t kFlagWord = 512;  // byte 2048 of the 4 KB page
   dev::launch_readback(t->h_pin_dev, static_cast<const uint32_t*>(src),
-                       (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, s);
+                       (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, s);  // <= 64
   HIP_OK(hipGetLastError());
   const uint32_t* flag = reinterpret_cast<const uint32_t*>(t->h_pin) + kFlagWord;
   for (uint32_t spin = 1;; ++spin) {
@@ -1549,6 +1549,16 @@ int shm_stats(shm_tree* t, shm_stats_t* o) {
   o->batches = t->batches;
   o->splits = t->splits;
   o->last_error = t->sticky_err;
+  return SHM_OK;
+}
+
+int shm_read_words(shm_tree* t, const void* src, uint64_t bytes, void* host_out,
+                   void* stream) {
+  if (!t || !src || !host_out || bytes == 0 || bytes > 256 || (bytes & 3)) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  const int rc = readback(t, pick(t, stream), src, bytes);
+  if (rc) return rc;
+  memcpy(host_out, t->h_pin, bytes);
   return SHM_OK;
 }
 

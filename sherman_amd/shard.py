@@ -88,15 +88,26 @@ class ShardRouter:
         n, dev = keys.numel(), keys.device
         kb = self._buf("kb", n, torch.int64, dev)
         perm = self._buf("perm", n, torch.int32, dev)
-        cnt = self._buf("cnt", self.world, torch.int64, dev)
+        # send and receive counts side by side: one read-back fetches both
+        cnts = self._buf("cnts", 2 * self.world, torch.int64, dev)
+        cnt, rcnt = cnts[:self.world], cnts[self.world:2 * self.world]
         self.local.route_bucket(keys, self.world, kb, perm, cnt)
-        rcnt = self._buf("rcnt", self.world, torch.int64, dev)
         self._a2a(rcnt, cnt)
         return kb, perm, cnt, rcnt
 
+    def _counts(self, cnt_t, rcnt_t):
+        """Both count vectors on the host (the RCCL split sizes): one
+        zero-copy read-back of the shared buffer (Tree.read_i64) on a GPU."""
+        w = self.world
+        rd = getattr(self.local, "read_i64", None)
+        if rd is not None and cnt_t.device.type == "cuda" and w <= 16:
+            both = rd(self._bufs["cnts"][:2 * w])
+            return both[:w], both[w:]
+        return cnt_t.tolist(), rcnt_t.tolist()
+
     def _bucket(self, keys):
         kb, perm, cnt, rcnt = self._bucket_async(keys)
-        return kb, perm, cnt.tolist(), rcnt.tolist()
+        return (kb, perm) + self._counts(cnt, rcnt)
 
     def search(self, keys, vals_out, found_out):
         """Batched get of this rank's keys; results land in input order."""
@@ -116,7 +127,7 @@ class ShardRouter:
         un-permute into vals_out / found_out (input order)."""
         keys, kb, perm, cnt_t, rcnt_t = pending
         n, dev = keys.numel(), keys.device
-        cnt, rcnt = cnt_t.tolist(), rcnt_t.tolist()
+        cnt, rcnt = self._counts(cnt_t, rcnt_t)
         nrecv = sum(rcnt)
         recv = self._buf("recv", nrecv, torch.int64, dev)
         self._a2a(recv, kb, rcnt, cnt)
