@@ -8,6 +8,8 @@ B-link invariants; and each side's page image is searchable by the other
 
 All GPU work runs in this one process.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -293,6 +295,25 @@ def test_range_query_async_matches_sync_and_reports_overflow(lib_ok):
                                                tot.data_ptr(), None)
     assert rc == shm.SHM_EINVAL
     t.check()
+    t.close()
+
+
+def test_read_words_zero_copy(lib_ok):
+    """shm_read_words (the router's count read-back) returns what the stream
+    wrote before it, on the default and on a side stream; bad sizes are
+    refused."""
+    t = shm.Tree(arena_bytes=32 << 20, max_batch=4096)
+    for it in range(3):
+        x = torch.arange(32, dtype=torch.int64, device="cuda") * (it + 7) - (1 << 40)
+        assert t.read_i64(x) == x.cpu().tolist()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        y = torch.full((5,), -3, dtype=torch.int64, device="cuda")
+        y += 1
+        assert t.read_i64(y) == [-2] * 5
+    buf = (ctypes.c_int64 * 64)()
+    assert shm.lib().shm_read_words(t.h, x.data_ptr(), 260, buf, None) == shm.SHM_EINVAL
+    assert shm.lib().shm_read_words(t.h, x.data_ptr(), 6, buf, None) == shm.SHM_EINVAL
     t.close()
 
 
