@@ -275,6 +275,8 @@ void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s);
 // system-scope release store of seq to *flag
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
                      uint32_t seq, hipStream_t s);
+void launch_readback_gather(uint32_t* dst, const Gather8& g, uint32_t* flag, uint32_t seq,
+                            hipStream_t s);
 // x[i] += c for i < n
 void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 

@@ -157,6 +157,20 @@ void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* 
   hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, dst, src, nw, flag, seq);
 }
 
+// the same for scattered words: dst[i] = *g.p[i]
+__global__ void k_readback_gather(uint32_t* dst, Gather8 g, uint32_t* flag, uint32_t seq) {
+  const int l = (int)threadIdx.x;
+  if (l < g.n) dst[l] = *g.p[l];
+  __threadfence_system();
+  __syncthreads();
+  if (l == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_readback_gather(uint32_t* dst, const Gather8& g, uint32_t* flag, uint32_t seq,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_readback_gather, dim3(1), dim3(64), 0, s, dst, g, flag, seq);
+}
+
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += c;

@@ -468,6 +468,9 @@ int dbg(hipStream_t s, const char* what) {
     if (_r) return _r;                 \
   } while (0)
 
+constexpr uint32_t kFlagWord = 512;  // read-back sequence word: byte 2048 of h_pin
+int readback_wait(shm_tree* t, hipStream_t s, uint32_t seq);
+
 // SHM_ZC_READBACK=0: read-backs as a D2H copy + stream synchronisation
 bool use_zc_readback() {
   static const bool on = [] {
@@ -491,9 +494,25 @@ int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
     return SHM_OK;
   }
   const uint32_t seq = ++t->rb_seq;
-  constexpr uint32_t kFlagWord = 512;  // byte 2048 of the 4 KB page
   dev::launch_readback(t->h_pin_dev, static_cast<const uint32_t*>(src),
                        (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, s);  // <= 64
+  return readback_wait(t, s, seq);
+}
+
+// the words *g.p[i] (scattered device u32s) into h_pin[0 ..] as u32s; with
+// zero-copy read-backs one fused kernel, else a gather into `staging` + copy
+int readback_gather(shm_tree* t, hipStream_t s, const dev::Gather8& g, uint32_t* staging) {
+  if (!use_zc_readback()) {
+    dev::launch_gather_u32(staging, g, s);
+    return readback(t, s, staging, (size_t)g.n * sizeof(uint32_t));
+  }
+  const uint32_t seq = ++t->rb_seq;
+  dev::launch_readback_gather(t->h_pin_dev, g, t->h_pin_dev + kFlagWord, seq, s);
+  return readback_wait(t, s, seq);
+}
+
+// spin until the read-back kernel has published `seq`
+int readback_wait(shm_tree* t, hipStream_t s, uint32_t seq) {
   HIP_OK(hipGetLastError());
   const uint32_t* flag = reinterpret_cast<const uint32_t*>(t->h_pin) + kFlagWord;
   for (uint32_t spin = 1;; ++spin) {
@@ -643,8 +662,7 @@ int64_t new_page_total(shm_tree* t, hipStream_t s, dev::SegArgs& a, uint64_t res
   g.p[4] = reinterpret_cast<const uint32_t*>(t->d_counts + 0);  // low words (n < 2^31)
   g.p[5] = reinterpret_cast<const uint32_t*>(t->d_counts + 1);
   g.n = 6;
-  dev::launch_gather_u32(d_tot, g, s);
-  int rc = readback(t, s, d_tot, 6 * sizeof(uint32_t));
+  int rc = readback_gather(t, s, g, d_tot);
   if (rc) return rc;
   t->err_pending = false;
   const uint32_t* h = reinterpret_cast<const uint32_t*>(t->h_pin);
