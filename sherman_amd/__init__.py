@@ -178,32 +178,44 @@ def _stream_ptr(stream):
     return stream.cuda_stream or None
 
 
+def _record_on(stream_ptr, device):
+    """A torch event recorded on the raw hipStream_t `stream_ptr` (None = the
+    null stream) of `device`: completion of the work queued there so far."""
+    import torch
+    ev = torch.cuda.Event()
+    s = (torch.cuda.ExternalStream(stream_ptr, device=device) if stream_ptr
+         else torch.cuda.default_stream(device))
+    ev.record(s)
+    return ev
+
+
 class PendingRange:
     """Result of Tree.range_query_batch_async: (counts, values) once the
-    scans have run.  tot = device (total, error bits)."""
+    scans have run.  tot = device (total, error bits); done = a torch event
+    recorded on the stream the scans were queued on (resolved when they were
+    issued, so .result() waits for them whatever stream is current then)."""
 
-    def __init__(self, tree, counts, vals, tot=None, stream=None):
-        self.tree, self.counts, self.vals, self.tot, self.stream = tree, counts, vals, tot, stream
+    def __init__(self, tree, counts, vals, tot=None, done=None):
+        self.tree, self.counts, self.vals, self.tot, self.done = tree, counts, vals, tot, done
 
     def result(self):
         if self.tot is None:  # ran synchronously
             return self.counts, self.vals
         import torch
-        s = self.stream
-        if s is None:
-            torch.cuda.current_stream().synchronize()
-        elif hasattr(s, "synchronize"):
-            s.synchronize()
-        else:  # a raw hipStream_t
+        if self.done is not None:
+            self.done.synchronize()
+        else:
             torch.cuda.synchronize()
         total, err = (int(x) for x in self.tot.cpu().tolist())
         if err:
             self.tree.synchronize()  # raises the device error
             raise ShermanError(SHM_EIO, "range_query_batch_async")
+        # learn the size even when this batch overflowed, so the next async
+        # batch gets a buffer that fits
+        self.tree._rq_cap = max(self.tree._rq_cap, total + total // 4)
         if total > self.vals.numel():
             raise ShermanError(SHM_ENOSPC, "range_query_batch_async: %d values, buffer %d"
                                % (total, self.vals.numel()))
-        self.tree._rq_cap = max(self.tree._rq_cap, total + total // 4)
         self.tot = None
         self.vals = self.vals[:total]
         return self.counts, self.vals
@@ -307,11 +319,11 @@ class Tree:
         offs = torch.empty(n, dtype=torch.int64, device=dev)
         vals = torch.empty(cap, dtype=torch.int64, device=dev)
         tot = torch.empty(2, dtype=torch.int64, device=dev)
+        sp = _stream_ptr(stream)
         _check(lib().shm_range_query_batch_async(self.h, _ptr(lo), _ptr(hi), n, _ptr(counts),
-                                                 _ptr(offs), _ptr(vals), cap, _ptr(tot),
-                                                 _stream_ptr(stream)),
+                                                 _ptr(offs), _ptr(vals), cap, _ptr(tot), sp),
                "range_query_batch_async")
-        return PendingRange(self, counts, vals, tot, stream)
+        return PendingRange(self, counts, vals, tot, _record_on(sp, dev))
 
     # -- reference single-op API (Tree.h:47-54) -------------------------------
     def _dev(self, name, n):

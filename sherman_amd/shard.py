@@ -72,6 +72,7 @@ class ShardRouter:
     def __init__(self, local, world, dist, group=None):
         self.local, self.world, self.dist, self.group = local, world, dist, group
         self._bufs = {}
+        self._pending = False  # a search_begin not yet ended (it owns kb / perm)
 
     def _buf(self, name, n, dtype, device):
         b = self._bufs.get(name)
@@ -88,26 +89,29 @@ class ShardRouter:
         n, dev = keys.numel(), keys.device
         kb = self._buf("kb", n, torch.int64, dev)
         perm = self._buf("perm", n, torch.int32, dev)
-        # send and receive counts side by side: one read-back fetches both
-        cnts = self._buf("cnts", 2 * self.world, torch.int64, dev)
+        # send and receive counts side by side (one read-back fetches both);
+        # a fresh buffer per batch, so a pending batch keeps its own counts
+        cnts = torch.empty(2 * self.world, dtype=torch.int64, device=dev)
         cnt, rcnt = cnts[:self.world], cnts[self.world:2 * self.world]
         self.local.route_bucket(keys, self.world, kb, perm, cnt)
         self._a2a(rcnt, cnt)
-        return kb, perm, cnt, rcnt
+        return kb, perm, cnts
 
-    def _counts(self, cnt_t, rcnt_t):
-        """Both count vectors on the host (the RCCL split sizes): one
-        zero-copy read-back of the shared buffer (Tree.read_i64) on a GPU."""
+    def _counts(self, cnts):
+        """Both count vectors of one batch (its own `cnts` buffer: sent, then
+        received) on the host, the RCCL split sizes: one zero-copy read-back
+        (Tree.read_i64) on a GPU."""
         w = self.world
         rd = getattr(self.local, "read_i64", None)
-        if rd is not None and cnt_t.device.type == "cuda" and w <= 16:
-            both = rd(self._bufs["cnts"][:2 * w])
-            return both[:w], both[w:]
-        return cnt_t.tolist(), rcnt_t.tolist()
+        if rd is not None and cnts.device.type == "cuda" and w <= 16:
+            both = rd(cnts[:2 * w])
+        else:
+            both = cnts[:2 * w].tolist()
+        return both[:w], both[w:]
 
     def _bucket(self, keys):
-        kb, perm, cnt, rcnt = self._bucket_async(keys)
-        return (kb, perm) + self._counts(cnt, rcnt)
+        kb, perm, cnts = self._bucket_async(keys)
+        return (kb, perm) + self._counts(cnts)
 
     def search(self, keys, vals_out, found_out):
         """Batched get of this rank's keys; results land in input order."""
@@ -120,14 +124,19 @@ class ShardRouter:
         the time they are needed instead of queueing behind batch i's walk
         (bench.py, N > 1).  Every rank must begin and end the same batches
         in the same order (collectives)."""
+        # the bucketed keys and permutation live in this router's buffers: one
+        # batch in flight per router (bench.py alternates two routers)
+        assert not self._pending, "ShardRouter: search_begin while a batch is in flight"
+        self._pending = True
         return (keys,) + self._bucket_async(keys)
 
     def search_end(self, pending, vals_out, found_out):
         """Second half: key exchange, local batched get, value exchange,
         un-permute into vals_out / found_out (input order)."""
-        keys, kb, perm, cnt_t, rcnt_t = pending
+        keys, kb, perm, cnts = pending
+        self._pending = False
         n, dev = keys.numel(), keys.device
-        cnt, rcnt = self._counts(cnt_t, rcnt_t)
+        cnt, rcnt = self._counts(cnts)
         nrecv = sum(rcnt)
         recv = self._buf("recv", nrecv, torch.int64, dev)
         self._a2a(recv, kb, rcnt, cnt)
