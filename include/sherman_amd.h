@@ -16,7 +16,7 @@
  *   shm_tree_destroy    (process teardown; DSM is a singleton, src/DSM.cpp:23-35)
  *   shm_search_batch    Tree::search(const Key&, Value&)  include/Tree.h:49-50, src/Tree.cpp:405-459
  *   shm_insert_batch    Tree::insert(const Key&, const Value&)
- *                                                         include/Tree.h:47-48, src/Tree.cpp:353-403
+ *   shm_insert_batch_async                                include/Tree.h:47-48, src/Tree.cpp:353-403
  *   shm_del_batch       Tree::del(const Key&)             include/Tree.h:51,   src/Tree.cpp:542-591
  *   shm_range_query     Tree::range_query(from, to, Value*)
  *                                                         include/Tree.h:53-54, src/Tree.cpp:461-540
@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 3
+#define SHM_ABI_VERSION 4
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -111,9 +111,20 @@ int shm_search_batch(shm_tree *t, const uint64_t *keys, uint64_t n,
                      uint64_t *vals_out, uint8_t *found_out, void *stream);
 /* Upsert keys[i] -> vals[i] in batch order (last writer in the batch wins).
  * vals[i] == 0 (kValueNull) deletes keys[i]. Mutating calls on one handle are
- * serialised internally. Returns after the batch is applied on `stream`. */
+ * serialised internally. Returns once the batch has been applied on `stream`
+ * (one host synchronisation, for the status): SHM_EINVAL if the batch held
+ * kKeyMax (the max_batch chunk holding it is rejected whole, earlier chunks
+ * stay applied), SHM_ENOMEM if the arena ran out (the splits that did not fit
+ * are left unapplied), SHM_EIO on a device fault. */
 int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
                      uint64_t n, void *stream);
+/* The same batch queued on `stream` without any host wait (the reference's
+ * Tree::insert returns nothing either, include/Tree.h:47-48): ordering, leaf
+ * upserts, splits, parent levels and root growth all run on the device.  The
+ * status of the batch is reported by the next synchronising call on the
+ * handle (shm_synchronize, shm_insert_batch, shm_del_batch) as above. */
+int shm_insert_batch_async(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
+                           uint64_t n, void *stream);
 /* Tree::del for every key. */
 int shm_del_batch(shm_tree *t, const uint64_t *keys, uint64_t n, void *stream);
 /* Batched inclusive range scans [from[i], to[i]]: values of valid entries in

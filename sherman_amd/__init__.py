@@ -94,7 +94,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 3  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 4  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -105,6 +105,7 @@ _SIGNATURES = [
     ("shm_abi_version", ctypes.c_int, []),
     ("shm_search_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
     ("shm_insert_batch", ctypes.c_int, [vp, vp, vp, u64, vp]),
+    ("shm_insert_batch_async", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_del_batch", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
     ("shm_range_query_batch", ctypes.c_int,
@@ -271,8 +272,15 @@ class Tree:
                                       _stream_ptr(stream)), "search_batch")
 
     def insert_batch(self, keys, vals, stream=None):
+        """Apply the batch and return its status (one host synchronisation)."""
         _check(lib().shm_insert_batch(self.h, _ptr(keys), _ptr(vals), keys.numel(),
                                       _stream_ptr(stream)), "insert_batch")
+
+    def insert_batch_async(self, keys, vals, stream=None):
+        """Queue the batch on the device without a host wait; its status is
+        raised by the next synchronising call (synchronize, insert_batch)."""
+        _check(lib().shm_insert_batch_async(self.h, _ptr(keys), _ptr(vals), keys.numel(),
+                                            _stream_ptr(stream)), "insert_batch_async")
 
     def del_batch(self, keys, stream=None):
         _check(lib().shm_del_batch(self.h, _ptr(keys), keys.numel(),

@@ -41,9 +41,7 @@ __device__ __forceinline__ uint64_t lds_u64(const uint32_t* lp, int d) {
 
 }  // namespace
 
-// LOC = the leaf-locate walk of the insert path (Tree::insert's descent to
-// level 0, Tree.cpp:353-403): out_page[i] = the leaf whose fences hold key i.
-template <int G, int NB, int WPB, bool LOC = false>
+template <int G, int NB, int WPB>
 __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   constexpr int L = kWave / G;                               // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;          // entries per lane
@@ -70,7 +68,6 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   const uint64_t wave_base = ((uint64_t)lblock * WPB + (uint64_t)wv) * kWave;
   if (wave_base >= n) return;  // wave-uniform
   const uint32_t nact = (uint32_t)(n - wave_base < (uint64_t)kWave ? n - wave_base : kWave);
-  const uint64_t t_start = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint32_t* ring = &s_ring[wv * kWaveRing];
   const uint32_t ring_lds = lds_addr_of(ring);
 
@@ -80,13 +77,10 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   wave_sort64(k, tag);
   const bool active = tag < nact;
 
+  // leaf directory: start at the leaf (or the covering internal page), else
+  // at the root
   uint64_t ptr = a.root;
-  if (a.dir) {
-    // leaf directory: start at the leaf (or the covering internal page)
-    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
-  } else if (a.start) {
-    ptr = a.start[k >> a.start_shift];
-  }
+  if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
   // occupancy bound of my page (kLeafHwFull after a move: read it whole)
   uint32_t hw = kLeafHwFull;
   if (a.leaf_hw && ptr_ok(ptr, a.node, a.arena_bytes)) hw = a.leaf_hw[ga_offset(ptr) >> 10];
@@ -191,7 +185,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
       int hsrc = hq[0];
       uint64_t kq = 0;
       uint32_t hwq = kLeafHwFull;  // slots of page q that were loaded
-      if constexpr (!LOC) {
+      {
         const uint32_t* ep = buf + q * kPageDwords + chunk_dw;
 #pragma unroll
         for (int i = 0; i < CD; ++i) D[i] = ep[i];
@@ -250,9 +244,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 
       // ---- leaf pages: lane groups hold the entries -----------------------
       uint64_t lq = ballot(qleaf);
-      if constexpr (LOC) {
-        val = qleaf ? ptr : val;  // the leaf holding the key
-      } else if (lq) {
+      if (lq) {
         uint64_t ekey[E], evalue[E];
         uint32_t efr[E], erv[E];
         chunk_entries<E>(D, ekey, evalue, efr, erv);
@@ -297,66 +289,23 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
     if (retries > kMaxRetries) break;
   }
   if (err) atomicOr(a.err, err);
-  if (a.stamps && lane < 2) {
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-    a.stamps[2 * (wave_base / kWave) + lane] = lane == 0 ? t_start : t_end;
-  }
   if (active) {
     const uint64_t i = wave_base + tag;
     const uint64_t o = a.perm ? (uint64_t)a.perm[i] : i;
-    if constexpr (LOC) {
-      a.out_page[o] = val;
-    } else {
-      a.out_val[o] = val;
-      if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
-    }
+    a.out_val[o] = val;
+    if (a.out_found) a.out_found[o] = val != kValueNull ? 1 : 0;
   }
 }
 
-// SHM_GET_CFG="G,NB,WPB" picks pages per group, group buffers per wave and
-// waves per block (measurement knob; default 4,1,4)
-static int get_cfg() {
-  static const int c = [] {
-    const char* e = getenv("SHM_GET_CFG");
-    int g = 4, nb = 1, w = 4;
-    if (e) sscanf(e, "%d,%d,%d", &g, &nb, &w);
-    return g * 100 + nb * 10 + w;
-  }();
-  return c;
-}
-
-template <int G, int NB, int WPB>
-static void launch_cfg(const WalkArgs& a, uint64_t waves, hipStream_t s) {
-  const dim3 grid((unsigned)((waves + WPB - 1) / WPB));
-  hipLaunchKernelGGL((k_get<G, NB, WPB>), grid, dim3(WPB * kWave), 0, s, a);
-}
-
-void launch_locate_leaf(const WalkArgs& a, uint64_t n, hipStream_t s) {
-  if (n == 0) return;
-  const uint64_t waves = (n + kWave - 1) / kWave;
-  hipLaunchKernelGGL((k_get<4, 1, 4, true>), dim3((unsigned)((waves + 3) / 4)), dim3(4 * kWave),
-                     0, s, a);
-}
-
+// G = 4 pages per group, NB = 1 group buffer, 4 waves per block: 16 KB of
+// LDS per block, 24-28 waves per CU (deeper buffers lost
+// occupancy and measured 2-8 % slower)
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s) {
   if (n == 0) return;
+  constexpr int G = 4, NB = 1, WPB = 4;
   const uint64_t waves = (n + kWave - 1) / kWave;
-  switch (get_cfg()) {
-    case 414: launch_cfg<4, 1, 4>(a, waves, s); break;
-    case 411: launch_cfg<4, 1, 1>(a, waves, s); break;
-    case 412: launch_cfg<4, 1, 2>(a, waves, s); break;
-    case 214: launch_cfg<2, 1, 4>(a, waves, s); break;
-    case 221: launch_cfg<2, 2, 1>(a, waves, s); break;
-    case 224: launch_cfg<2, 2, 4>(a, waves, s); break;
-    case 231: launch_cfg<2, 3, 1>(a, waves, s); break;
-    case 241: launch_cfg<2, 4, 1>(a, waves, s); break;
-    case 244: launch_cfg<2, 4, 4>(a, waves, s); break;
-    case 421: launch_cfg<4, 2, 1>(a, waves, s); break;
-    case 431: launch_cfg<4, 3, 1>(a, waves, s); break;
-    case 422: launch_cfg<4, 2, 2>(a, waves, s); break;
-    case 424: launch_cfg<4, 2, 4>(a, waves, s); break;
-    default: launch_cfg<4, 1, 4>(a, waves, s); break;
-  }
+  hipLaunchKernelGGL((k_get<G, NB, WPB>), dim3((unsigned)((waves + WPB - 1) / WPB)),
+                     dim3(WPB * kWave), 0, s, a);
 }
 
 }  // namespace dev

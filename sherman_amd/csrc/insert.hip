@@ -1,28 +1,42 @@
-// insert.hip — batched Tree::insert / Tree::del on HBM pages.
+// insert.hip — split propagation and deletes of a batched insert, driven by
+// the device (no host read-back between the levels).
 //
-// Restates src/Tree.cpp:828-991 (leaf_page_store), 699-826
-// (internal_page_store), 993-1057 (leaf_page_del) and 126-149
-// (update_new_root) for a sorted, de-duplicated batch.  The host runtime
-// (tree.cpp) groups the batch's keys into *segments* (runs of keys whose
-// B-link walk ends at the same page) and runs, per tree level:
+// Restates src/Tree.cpp:828-991 (leaf_page_store's split half), 699-826
+// (internal_page_store), 126-149 (update_new_root) and 993-1057
+// (leaf_page_del) for a sorted, de-duplicated batch.  The in-place half of
+// leaf_page_store (the common case) is upsert.hip; what it leaves behind is a
+// set of flagged leaf segments (seg_P > 1: the page would reach 54 entries)
+// whose per-range new-page counts it accumulated in UpperCtl.
 //
-//   plan   (1 wave / segment, read-only): entries after the batch T and the
-//          page count P (P = 1: applied in place; P > 1: k-way split into
-//          ceil(T / fill) pages, fill = 36 leaf / 40 internal).
-//   build  (1 wave / NEW page): new right siblings, written before anything
-//          links to them (Sherman writes the sibling first, Tree.cpp:962).
-//   update (1 wave / segment): lock the page in the HBM lock table
-//          (atomicCAS 0 -> tag on lock[CityHash64(page) % num_locks], the
-//          reference's on-chip lock word, Tree.cpp:205-242/832-842), re-read
-//          it, check the front_version the plan saw (optimistic check), then
-//          either apply the updates in place with the reference's slot rule
-//          (update the valid slot with the key, else first empty slot; entry
-//          versions f++ / r = f, Tree.cpp:878-912) or rewrite page 0 of the
-//          split (set_consistent: front++ , rear = front), release the lock.
-//
-// A split page's new separators (first key of each new leaf / the pushed-up
-// key of each new internal page) are emitted already sorted and become the
-// next level's batch; a split root gets a new root above it.
+// k_upper is ONE persistent launch (one block per CU, all resident) that
+// finishes the batch:
+//   leaf level     P2  per block: ordered scan of its segment range's new-page
+//                      counts -> seg_pbase and a dense list of split segments
+//                  --- grid barrier ---
+//                  P3  every wave: build new right siblings (k-way split,
+//                      ceil(T / 36) pages), each emitting its separator and the
+//                      parent it belongs to (a header walk from the root);
+//                      then page 0 of each split segment is rewritten in
+//                      place (set_consistent: front++ , rear = front) once
+//                      every sibling builder has read the old page (a per-
+//                      segment counter), and its lock word released
+//                  --- grid barrier ---
+//   level L >= 1   I1  per block: segment heads of its separator range, one
+//                      wave per head: lock the page (HBM lock table), plan T
+//                      and P (in place if T <= 60, else ceil((T + 1) / 41))
+//                  --- barrier ---  I2 prefix: dense segment list + page bases
+//                  --- barrier ---  I3 build / rewrite as for leaves
+//                  --- barrier ---  next level while separators remain
+// Pages come from a device bump cursor (the superblock's next_page; the
+// reference's LocalAllocator bump, include/LocalAllocator.h:21-43), checked
+// against the arena capacity before each level.  The root page never moves:
+// when the root splits, its left half is written to a fresh page X and the
+// root page itself becomes the new internal root {leftmost = X} one level up
+// (update_new_root, Tree.cpp:126-149, without the root-pointer CAS and the
+// NEW_ROOT broadcast, Tree.cpp:116-124: every reader already starts there).
+// Separators come out sorted (segment order = key order) and become the next
+// level's batch.  Nothing here waits for the host; the superblock and a
+// mapped host mirror are updated at the end of the launch.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -31,6 +45,11 @@ namespace dev {
 
 namespace {
 
+constexpr int kUpT = 512;                  // threads per k_upper block
+constexpr int kUpWaves = kUpT / kWave;     // 8 waves
+constexpr uint32_t kBarrierSpins = 1u << 22;
+constexpr uint32_t kFanSpins = 1u << 22;
+
 struct WaveLds {
   uint32_t page[kPageDwords + 8];
   uint64_t a_key[kWave];
@@ -38,64 +57,34 @@ struct WaveLds {
   uint32_t a_ver[kWave];
 };
 
-__device__ __forceinline__ uint64_t new_page_ga(const SegArgs& a, uint32_t g,
-                                                int p) {
-  const uint64_t idx = a.first_new_page + a.seg_pbase[g] + (uint64_t)(p - 1);
-  return ga_make(a.node, idx * kPageSize);
-}
-
 __device__ __forceinline__ uint32_t lock_index(uint64_t page, uint32_t n) {
   return (uint32_t)(cityhash64_u64(page) % n);
 }
 
-// lane 0 spins on atomicCAS(0 -> tag); bounded (Tree.cpp:218-238)
-__device__ __forceinline__ bool lock_page(const SegArgs& a, uint64_t page,
-                                          uint64_t tag) {
-  int ok = 0;
-  if (lane_id() == 0) {
-    unsigned long long* w =
-        reinterpret_cast<unsigned long long*>(a.locks + lock_index(page, a.num_locks));
-    for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-      if (atomicCAS(w, 0ull, (unsigned long long)tag) == 0ull) {
-        ok = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  return rl32((uint32_t)ok, 0) != 0;
+__device__ __forceinline__ void release_word(const uint64_t* locks, uint32_t num, uint64_t page) {
+  __hip_atomic_store(const_cast<uint64_t*>(locks) + lock_index(page, num), 0ull,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void unlock_page(const SegArgs& a, uint64_t page) {
-  // The page stores are performed (vmcnt(0)) before the lock word is cleared
-  // (write_page_and_unlock batches "write page, then release", Tree.cpp:
-  // 266-298).  No agent-scope release fence: within one batch every page is
-  // written by exactly one wave (lock holders that collide on a lock word
-  // touch other pages), and the next kernel on the stream sees all stores;
-  // a release here costs an L2 write-back per segment (measured 11 ms per
-  // 1 Mi-insert batch).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane_id() == 0) {
-    __hip_atomic_store(a.locks + lock_index(page, a.num_locks), 0ull,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
+// the ops of one segment: keys [st, st + nb) of a sorted unique op array
+struct Ops {
+  const uint64_t* key;
+  const uint64_t* val;
+  uint32_t st, nb;
+};
 
-// Does `key` occur among ops [st, en)?  (ops are sorted, unique)
-__device__ __forceinline__ bool op_contains(const SegArgs& a, uint32_t st,
-                                            uint32_t en, uint64_t key) {
-  const uint64_t i = lower_bound64(a.op_key, st, en, key);
-  return i < en && a.op_key[i] == key;
+__device__ __forceinline__ bool op_contains(const Ops& o, uint64_t key) {
+  const uint64_t i = lower_bound64(o.key, o.st, (uint64_t)o.st + o.nb, key);
+  return i < (uint64_t)o.st + o.nb && o.key[i] == key;
 }
 
 // Surviving entries of the staged leaf (valid, not overwritten by an op),
 // sorted by key into L.a_* ; returns their count.
-__device__ int leaf_survivors(const SegArgs& a, WaveLds& L, uint32_t st,
-                              uint32_t en) {
+__device__ int leaf_survivors(WaveLds& L, const Ops& o) {
   const int lane = lane_id();
   const LeafEnt e = leaf_entry(L.page, lane < kLeafCardinality ? lane : 0);
   bool keep = lane < kLeafCardinality && e.val != kValueNull;
-  if (keep && op_contains(a, st, en, e.key)) keep = false;
+  if (keep && op_contains(o, e.key)) keep = false;
   uint64_t key = keep ? e.key : kKeyMax;
   uint32_t tag = (uint32_t)lane;
   wave_sort64(key, tag);
@@ -109,13 +98,12 @@ __device__ int leaf_survivors(const SegArgs& a, WaveLds& L, uint32_t st,
   return na;
 }
 
-// Surviving records of the staged internal page, in key order.
-__device__ int internal_survivors(const SegArgs& a, WaveLds& L, const u32x4 w,
-                                  int cnt, uint32_t st, uint32_t en) {
+// Surviving records of an internal page (lane slice w), in key order.
+__device__ int internal_survivors(WaveLds& L, const u32x4 w, int cnt, const Ops& o) {
   const int lane = lane_id();
   const IntRec r = internal_record(w);
   bool keep = lane >= 3 && lane - 3 < cnt;
-  if (keep && op_contains(a, st, en, r.key)) keep = false;
+  if (keep && op_contains(o, r.key)) keep = false;
   const uint64_t km = ballot(keep);
   if (keep) {
     const int pos = popc64(km & lanemask_lt());
@@ -127,77 +115,85 @@ __device__ int internal_survivors(const SegArgs& a, WaveLds& L, const u32x4 w,
   return popc64(km);
 }
 
-// Element r of merge(A = survivors (na), B = ops [st, st + nb)); keys are
-// disjoint.  Merge-path binary search (distinct keys).
-__device__ __forceinline__ void merged_elem(const SegArgs& a, const WaveLds& L,
-                                            int na, uint32_t st, uint32_t nb,
-                                            uint32_t r, uint64_t& key,
-                                            uint64_t& val, uint32_t& ver) {
+// Element r of merge(A = survivors (na), B = ops); keys are disjoint.
+// Merge-path binary search (distinct keys).
+__device__ __forceinline__ void merged_elem(const WaveLds& L, int na, const Ops& o, uint32_t r,
+                                            uint64_t& key, uint64_t& val, uint32_t& ver) {
+  const uint32_t nb = o.nb, st = o.st;
   uint32_t lo = r > nb ? r - nb : 0;
   uint32_t hi = r < (uint32_t)na ? r : (uint32_t)na;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (L.a_key[mid] < a.op_key[st + r - mid - 1])
+    if (L.a_key[mid] < o.key[st + r - mid - 1])
       lo = mid + 1;
     else
       hi = mid;
   }
   const uint32_t i = lo, j = r - lo;
-  if (i < (uint32_t)na && (j >= nb || L.a_key[i] < a.op_key[st + j])) {
+  if (i < (uint32_t)na && (j >= nb || L.a_key[i] < o.key[st + j])) {
     key = L.a_key[i];
     val = L.a_val[i];
     ver = L.a_ver[i];
   } else {
-    key = a.op_key[st + j];
-    val = a.op_val[st + j];
+    key = o.key[st + j];
+    val = o.val[st + j];
     ver = 0;  // fresh LeafEntry() in the sibling (Tree.cpp:934, 944-948)
   }
 }
 
-// Write page p (0 <= p < P) of a leaf k-way split of segment g into L.page and
-// store it.  Survivors must already be in L.a_*.
-__device__ void build_leaf_page(const SegArgs& a, WaveLds& L, uint32_t g,
-                                const Hdr& h, int na, int p, int P,
-                                uint32_t T, uint64_t page_ga) {
+// one page of a k-way split: page p of P of a segment with T entries after
+// the batch; new page q >= 1 sits at arena page first_new + q - 1
+struct SplitPage {
+  int p, P;
+  uint32_t T;
+  uint64_t first_new;
+  uint64_t dest;  // GlobalAddress written (page 0: the segment's page, or X)
+};
+
+__device__ __forceinline__ uint64_t new_ga(uint16_t node, uint64_t first_new, int q) {
+  return ga_make(node, (first_new + (uint64_t)(q - 1)) * kPageSize);
+}
+
+// Write leaf page p of the split (survivors in L.a_*); returns its lowest
+// fence (the separator of p > 0, copied up as in Tree.cpp:939-950).
+__device__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
+                                    const Ops& o, const SplitPage& s) {
   const int lane = lane_id();
-  const uint32_t st = a.seg_start[g], nb = a.seg_start[g + 1] - st;
-  const uint32_t base = T / (uint32_t)P, rem = T % (uint32_t)P;
-  const uint32_t c = base + ((uint32_t)p < rem ? 1u : 0u);
-  const uint32_t s0 = (uint32_t)p * base + ((uint32_t)p < rem ? (uint32_t)p : rem);
+  const uint32_t base = s.T / (uint32_t)s.P, rem = s.T % (uint32_t)s.P;
+  const uint32_t p = (uint32_t)s.p;
+  const uint32_t c = base + (p < rem ? 1u : 0u);
+  const uint32_t s0 = p * base + (p < rem ? p : rem);
   uint64_t key = 0, val = 0;
   uint32_t ver = 0;
-  const bool has_next = p + 1 < P;
+  const bool has_next = s.p + 1 < s.P;
   if ((uint32_t)lane < c || ((uint32_t)lane == c && has_next))
-    merged_elem(a, L, na, st, nb, s0 + (uint32_t)lane, key, val, ver);
-  const uint64_t lowest = p == 0 ? h.lowest : rl64(key, 0);
+    merged_elem(L, na, o, s0 + (uint32_t)lane, key, val, ver);
+  const uint64_t lowest = s.p == 0 ? h.lowest : rl64(key, 0);
   const uint64_t highest = has_next ? rl64(key, (int)c) : h.highest;
-  const uint64_t sibling = has_next ? new_page_ga(a, g, p + 1) : h.sibling;
-  const uint32_t fver = p == 0 ? ((h.fver + 1) & 0xFF) : 1u;
+  const uint64_t sibling = has_next ? new_ga(a.node, s.first_new, s.p + 1) : h.sibling;
+  const uint32_t fver = s.p == 0 ? ((h.fver + 1) & 0xFF) : 1u;
   wave_lds_sync();
   init_page_image(L.page, fver, 0, sibling, 0, (int32_t)c - 1, lowest, highest);
   wave_lds_sync();
   if ((uint32_t)lane < c) put_leaf_entry(L.page, lane, key, val, ver & 0xFF, ver >> 8);
   if (lane == 0) L.page[kOffLeafRear / 4] = fver;  // rear_version, byte 1016
-  store_page(a.arena, ga_offset(page_ga), L.page);
-  if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(page_ga) >> 10] = (uint8_t)c;  // slots [0, c)
-  if (p > 0 && lane == 0) {
-    const uint64_t o = a.seg_pbase[g] + (uint64_t)(p - 1);
-    a.sep_key[o] = lowest;
-    a.sep_ptr[o] = page_ga;
-  }
+  store_page(a.arena, ga_offset(s.dest), L.page);
+  if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = (uint8_t)c;  // slots [0, c)
+  return lowest;
 }
 
-__device__ void build_internal_page(const SegArgs& a, WaveLds& L, uint32_t g,
-                                    const Hdr& h, int na, int p, int P,
-                                    uint32_t T, uint64_t page_ga) {
+// Internal page p of the split: q = T - (P - 1) records stay, one record per
+// extra page is pushed up (its ptr becomes that page's leftmost, its key the
+// separator, Tree.cpp:779-793).  Returns the page's lowest fence.
+__device__ uint64_t build_internal_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
+                                        const Ops& o, const SplitPage& s, uint32_t level) {
   const int lane = lane_id();
-  const uint32_t st = a.seg_start[g], nb = a.seg_start[g + 1] - st;
-  const uint32_t q = T - (uint32_t)(P - 1);  // records kept (non pushed-up)
-  const uint32_t base = q / (uint32_t)P, rem = q % (uint32_t)P;
-  const uint32_t c = base + ((uint32_t)p < rem ? 1u : 0u);
-  const uint32_t s0 = (uint32_t)p * base + ((uint32_t)p < rem ? (uint32_t)p : rem) +
-                      (uint32_t)p;
-  const bool has_next = p + 1 < P;
+  const uint32_t q = s.T - (uint32_t)(s.P - 1);
+  const uint32_t base = q / (uint32_t)s.P, rem = q % (uint32_t)s.P;
+  const uint32_t p = (uint32_t)s.p;
+  const uint32_t c = base + (p < rem ? 1u : 0u);
+  const uint32_t s0 = p * base + (p < rem ? p : rem) + p;
+  const bool has_next = s.p + 1 < s.P;
   uint64_t key = 0, val = 0;
   uint32_t ver = 0;
   bool want = false;
@@ -205,22 +201,21 @@ __device__ void build_internal_page(const SegArgs& a, WaveLds& L, uint32_t g,
   if ((uint32_t)lane < c) {
     want = true;
     r = s0 + (uint32_t)lane;
-  } else if (lane == 62 && p > 0) {
+  } else if (lane == 62 && s.p > 0) {
     want = true;
     r = s0 - 1;  // record pushed up to the parent; its ptr becomes leftmost
   } else if (lane == 63 && has_next) {
     want = true;
     r = s0 + c;  // next page's pushed-up key = this page's highest
   }
-  if (want) merged_elem(a, L, na, st, nb, r, key, val, ver);
-  const uint64_t leftmost = p == 0 ? h.leftmost : rl64(val, 62);
-  const uint64_t lowest = p == 0 ? h.lowest : rl64(key, 62);
+  if (want) merged_elem(L, na, o, r, key, val, ver);
+  const uint64_t leftmost = s.p == 0 ? h.leftmost : rl64(val, 62);
+  const uint64_t lowest = s.p == 0 ? h.lowest : rl64(key, 62);
   const uint64_t highest = has_next ? rl64(key, 63) : h.highest;
-  const uint64_t sibling = has_next ? new_page_ga(a, g, p + 1) : h.sibling;
-  const uint32_t fver = p == 0 ? ((h.fver + 1) & 0xFF) : 1u;
+  const uint64_t sibling = has_next ? new_ga(a.node, s.first_new, s.p + 1) : h.sibling;
+  const uint32_t fver = s.p == 0 ? ((h.fver + 1) & 0xFF) : 1u;
   wave_lds_sync();
-  init_page_image(L.page, fver, leftmost, sibling, (uint32_t)a.level,
-                  (int32_t)c - 1, lowest, highest);
+  init_page_image(L.page, fver, leftmost, sibling, level, (int32_t)c - 1, lowest, highest);
   wave_lds_sync();
   if ((uint32_t)lane < c) {
     uint32_t* d = L.page + (kOffRecords + kInternalEntry * lane) / 4;
@@ -230,21 +225,140 @@ __device__ void build_internal_page(const SegArgs& a, WaveLds& L, uint32_t g,
     d[3] = (uint32_t)(val >> 32);
   }
   if (lane == 0) L.page[kOffInternalRear / 4] = fver;  // byte 1020
-  store_page(a.arena, ga_offset(page_ga), L.page);
-  if (p > 0 && lane == 0) {
-    const uint64_t o = a.seg_pbase[g] + (uint64_t)(p - 1);
-    a.sep_key[o] = lowest;
-    a.sep_ptr[o] = page_ga;
-  }
+  store_page(a.arena, ga_offset(s.dest), L.page);
+  if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = kLeafHwFull;
+  return lowest;
 }
 
-// segment index owning global new-page index gp (last s with pbase[s] <= gp)
-__device__ __forceinline__ uint32_t seg_of_new_page(const SegArgs& a,
-                                                    uint32_t gp) {
-  uint32_t lo = 0, hi = a.num_seg;
+// The root page becomes the new internal root one level up, {leftmost = X}
+// with no records (update_new_root, Tree.cpp:126-149); the level's separators
+// are then inserted into it by the next level.
+__device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint32_t level,
+                               uint32_t old_fver) {
+  wave_lds_sync();
+  init_page_image(L.page, (old_fver + 1) & 0xFF, x, 0, level, -1, kKeyMin, kKeyMax);
+  wave_lds_sync();
+  if (lane_id() == 0) L.page[kOffInternalRear / 4] = (old_fver + 1) & 0xFF;
+  store_page(a.arena, ga_offset(a.root), L.page);
+  if (a.leaf_hw && lane_id() == 0) a.leaf_hw[ga_offset(a.root) >> 10] = kLeafHwFull;
+}
+
+// The page of `level` whose fences hold k: header walk from the root with
+// page_search's sibling rule (Tree.cpp:593-663) and internal_page_search
+// (665-685), one wave.  0 on an inconsistency (error bits in *err).
+__device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err) {
+  uint64_t ptr = a.root;
+  int retries = 0;
+  for (int hop = 0; hop < kMaxRounds; ++hop) {
+    if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
+      *err |= kErrBadPtr;
+      return 0;
+    }
+    const u32x4 w = load_page_slice(a.arena, ga_offset(ptr));
+    const Hdr h = parse_hdr(w);
+    const bool is_leaf = h.leftmost == 0;
+    if (h.fver != (is_leaf ? h.rver_leaf : h.rver_internal)) {
+      if (++retries > kMaxRetries) {
+        *err |= kErrInconsistent;
+        return 0;
+      }
+      continue;
+    }
+    if (k >= h.highest && h.sibling != 0) {  // turn right (Tree.cpp:626-629)
+      ptr = h.sibling;
+      continue;
+    }
+    if (k < h.lowest || k >= h.highest || h.level < level) {
+      *err |= kErrFence;
+      return 0;
+    }
+    if (h.level == level) return ptr;
+    // child = #keys <= k (keys strictly increase; record j in lane j + 3)
+    const IntRec r = internal_record(w);
+    const int cnt = h.last_index + 1;
+    const uint64_t le = ballot(lane_id() >= 3 && lane_id() - 3 < cnt && r.key <= k);
+    const int pos = popc64(le);
+    ptr = pos == 0 ? h.leftmost : rl64(r.ptr, pos + 2);
+  }
+  *err |= kErrRounds;
+  return 0;
+}
+
+// ---- block / grid helpers (kUpT threads) ------------------------------------
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+  __syncthreads();
+  if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kUpWaves; ++i) s += red[i];
+  return s;
+}
+
+// exclusive block scan; *total = block sum
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* red, uint32_t* total) {
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+    if (lane_id() >= off) incl += y;
+  }
+  __syncthreads();
+  if (lane_id() == kWave - 1) red[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kUpWaves; ++i) {
+    base += i < w ? red[i] : 0u;
+    all += red[i];
+  }
+  *total = all;
+  return base + incl - v;
+}
+
+// Grid barrier over all resident blocks: every wave's stores performed, one
+// agent-scope release per block, arrive on a monotonic counter, poll it with
+// relaxed agent loads, one agent-scope acquire per block (MI355X_MICROARCH.md
+// "barrier-counter"; the counter is a multiple of nb between launches).
+// Bounded: a spin past kBarrierSpins sets the abort word, which releases every
+// other block too; returns false then.
+__device__ bool grid_sync(UpperCtl* ctl, uint32_t nb, uint32_t* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t old =
+        __hip_atomic_fetch_add(&ctl->bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t target = (old / nb + 1) * nb;
+    uint32_t ok = 1;
+    for (uint32_t spin = 0;; ++spin) {
+      if (__hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+          spin > kBarrierSpins) {
+        __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *flag = ok;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// last index s in [0, n) with base[s] <= x (base non-decreasing, base[0] = 0)
+__device__ __forceinline__ uint32_t last_le(const uint32_t* base, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (a.seg_pbase[mid] <= gp)
+    if (base[mid] <= x)
       lo = mid + 1;
     else
       hi = mid;
@@ -252,263 +366,472 @@ __device__ __forceinline__ uint32_t seg_of_new_page(const SegArgs& a,
   return lo - 1;
 }
 
+// [first, end) of block b's share of n items (the upsert kernel assigns item g
+// to range g * nb / n, i.e. exactly these)
+__device__ __forceinline__ void block_range(uint32_t n, uint32_t b, uint32_t nb, uint32_t& r0,
+                                            uint32_t& r1) {
+  r0 = (uint32_t)(((uint64_t)b * n + nb - 1) / nb);
+  r1 = (uint32_t)(((uint64_t)(b + 1) * n + nb - 1) / nb);
+}
+
+// wait until *cnt == want (the sibling builders of a split have read page 0)
+__device__ __forceinline__ bool fan_in(uint32_t* cnt, uint32_t want) {
+  uint32_t ok = 1;
+  if (lane_id() == 0) {
+    ok = 0;
+    for (uint32_t spin = 0; spin < kFanSpins; ++spin) {
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) {
+        ok = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return rl32(ok, 0) != 0;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// leaf plan: T = valid + ops - overwritten; P = 1 if T <= 53 else ceil(T/36)
-__global__ __launch_bounds__(kBlock) void k_leaf_plan(SegArgs a) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const int lane = lane_id();
-  const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= a.num_seg) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  const uint64_t page = a.seg_page[g];
-  if (!ptr_ok(page, a.node, a.arena_bytes)) {
-    if (lane == 0) {
-      atomicOr(a.err, kErrBadPtr);
-      a.seg_T[g] = 0; a.seg_P[g] = 1; a.seg_newpages[g] = 0; a.seg_ver[g] = ~0u;
+__global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
+  __shared__ __attribute__((aligned(16))) WaveLds s_l[kUpWaves];
+  __shared__ uint32_t s_red[kUpWaves];
+  __shared__ uint32_t s_flag;
+  __shared__ uint32_t s_list[kUpT];  // segment heads of one separator chunk
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const uint32_t b = blockIdx.x, nb = gridDim.x;
+  const uint64_t W = (uint64_t)nb * kUpWaves;
+  const uint64_t wid = (uint64_t)b * kUpWaves + (uint64_t)wv;
+  const uint64_t T = (uint64_t)nb * kUpT, tid = (uint64_t)b * kUpT + (uint64_t)t;
+  WaveLds& L = s_l[wv];
+  UpperCtl* ctl = a.ctl;
+  Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
+  uint64_t cursor = sb->next_page;
+  uint32_t root_level = (uint32_t)sb->root_level;
+  const uint64_t cap = sb->capacity_pages;
+  uint64_t made = 0;  // pages created by splits
+  uint32_t err = 0;
+  const uint32_t ns = *a.ns_dev;
+  const uint32_t par = a.par;
+  // the other parity's range sums and split counts start the next batch at 0
+  for (uint64_t j = tid; j < (uint64_t)kMaxUpper; j += T) {
+    ctl->leaf_np[par ^ 1][j] = 0;
+    ctl->leaf_ns[par ^ 1][j] = 0;
+  }
+  // leaf level: the upsert kernel left per-range new-page / split counts
+  const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
+  const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
+  const uint32_t total = block_sum(v_np, s_red);
+  const uint32_t nsplit = block_sum(v_ns, s_red);
+  const uint32_t pre_np = block_sum((uint32_t)t < b ? v_np : 0u, s_red);
+  const uint32_t pre_ns = block_sum((uint32_t)t < b ? v_ns : 0u, s_red);
+  // in-place segments were written by the upsert kernel: release their words
+  // (write_page_and_unlock's unlock half, Tree.cpp:266-298)
+  for (uint64_t g = tid; g < ns; g += T)
+    if (a.seg_lk[g] && a.seg_P[g] <= 1) release_word(a.locks, a.num_locks, a.seg_page[g]);
+
+  bool ok = true;
+  uint32_t nsep = 0;
+  const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
+  const bool fits = cursor + total + (grow0 ? 1u : 0u) <= cap;
+  if (total && !fits) {
+    // arena exhausted: the flagged segments stay unapplied (reported)
+    err |= kErrNoMem;
+    for (uint64_t g = tid; g < ns; g += T)
+      if (a.seg_lk[g] && a.seg_P[g] > 1) release_word(a.locks, a.num_locks, a.seg_page[g]);
+  } else if (total) {
+    // ---- P2: this block's segment range in order -> seg_pbase, split list --
+    uint32_t r0, r1;
+    block_range(ns, b, nb, r0, r1);
+    uint32_t run_np = pre_np, run_ns = pre_ns;
+    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
+      const uint32_t g = c0 + (uint32_t)t;
+      const uint32_t np = g < r1 ? a.seg_np[g] : 0u;
+      uint32_t tnp, tns;
+      const uint32_t xnp = block_scan(np, s_red, &tnp);
+      const uint32_t xns = block_scan(np ? 1u : 0u, s_red, &tns);
+      if (np) {
+        a.spl_seg[run_ns + xns] = g;
+        a.spl_base[run_ns + xns] = run_np + xnp;
+      }
+      run_np += tnp;
+      run_ns += tns;
     }
-    return;
+    ok = grid_sync(ctl, nb, &s_flag);
+    // ---- P3: new right siblings, then page 0 of every split ----------------
+    const uint64_t first = cursor;  // arena page of global new page 0
+    const uint64_t xroot = cursor + total;  // the root's left half (grow0)
+    for (uint64_t gp = wid; ok && gp < total; gp += W) {
+      const uint32_t k = last_le(a.spl_base, nsplit, (uint32_t)gp);
+      const uint32_t g = a.spl_seg[k];
+      const uint32_t pb = a.spl_base[k];
+      const int p = (int)(gp - pb) + 1;
+      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_start[g + 1] - a.seg_start[g]};
+      const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
+      const Hdr h = parse_hdr(w);
+      stage_page(L.page, w);
+      wave_lds_sync();
+      const int na = leaf_survivors(L, o);
+      // the old page 0 has been read: its rewrite may go ahead
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(a.leaf_rd + g, 1u);
+      const SplitPage sp{p, (int)a.seg_P[g], a.seg_T[g], first + pb,
+                         new_ga(a.node, first + pb, p)};
+      const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
+      const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
+      if (lane == 0) {
+        a.sep_key[0][gp] = low;
+        a.sep_ptr[0][gp] = sp.dest;
+        a.ipage[0][gp] = par_pg;
+      }
+    }
+    for (uint64_t k = wid; ok && k < nsplit; k += W) {
+      const uint32_t g = a.spl_seg[k];
+      const uint32_t pb = a.spl_base[k];
+      const int P = (int)a.seg_P[g];
+      const uint64_t page = a.seg_page[g];
+      if (!fan_in(a.leaf_rd + g, (uint32_t)(P - 1))) err |= kErrLock;
+      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_start[g + 1] - a.seg_start[g]};
+      const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+      const Hdr h = parse_hdr(w);
+      if (h.fver != a.seg_ver[g] || h.fver != h.rver_leaf) err |= kErrPlan;
+      stage_page(L.page, w);
+      wave_lds_sync();
+      const int na = leaf_survivors(L, o);
+      const uint64_t dest = grow0 ? ga_make(a.node, xroot * kPageSize) : page;
+      const SplitPage sp{0, P, a.seg_T[g], first + pb, dest};
+      (void)build_leaf_page(a, L, h, na, o, sp);
+      if (grow0) write_new_root(a, L, dest, 1, h.fver);
+      if (lane == 0) {
+        a.leaf_rd[g] = 0;  // for the next batch
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.seg_lk[g]) release_word(a.locks, a.num_locks, page);
+      }
+    }
+    cursor += total + (grow0 ? 1u : 0u);
+    if (grow0) root_level = 1;
+    made += total;
+    nsep = total;
+    ok = ok && grid_sync(ctl, nb, &s_flag);
   }
-  const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-  const Hdr h = parse_hdr(w);
-  stage_page(L.page, w);
-  wave_lds_sync();
-  const LeafEnt e = leaf_entry(L.page, lane < kLeafCardinality ? lane : 0);
-  const bool valid = lane < kLeafCardinality && e.val != kValueNull;
-  const bool hit = valid && op_contains(a, st, en, e.key);
-  const uint32_t V = (uint32_t)popc64(ballot(valid));
-  const uint32_t M = (uint32_t)popc64(ballot(hit));
-  const uint32_t T = V + (en - st) - M;
-  const uint32_t P = T <= (uint32_t)(kLeafCardinality - 1)
-                         ? 1u
-                         : (T + kLeafSplitFill - 1) / kLeafSplitFill;
-  if (lane == 0) {
-    a.seg_T[g] = T;
-    a.seg_P[g] = P;
-    a.seg_newpages[g] = P - 1;
-    a.seg_ver[g] = h.fver;
-    if (h.fver != h.rver_leaf || h.leftmost != 0) atomicOr(a.err, kErrInconsistent);
-  }
-}
 
-// new right-sibling leaves of k-way splits (1 wave per new page)
-__global__ __launch_bounds__(kBlock) void k_leaf_build(SegArgs a, uint32_t total) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const uint32_t gp = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (gp >= total) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint32_t g = seg_of_new_page(a, gp);
-  const int p = (int)(gp - a.seg_pbase[g]) + 1;
-  const int P = (int)a.seg_P[g];
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
-  const Hdr h = parse_hdr(w);
-  stage_page(L.page, w);
-  wave_lds_sync();
-  const int na = leaf_survivors(a, L, st, en);
-  build_leaf_page(a, L, g, h, na, p, P, a.seg_T[g], new_page_ga(a, g, p));
-}
-
-// lock, validate, apply in place or rewrite page 0, unlock (1 wave / segment)
-__global__ __launch_bounds__(kBlock) void k_leaf_update(SegArgs a) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const int lane = lane_id();
-  const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= a.num_seg) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint64_t page = a.seg_page[g];
-  if (!ptr_ok(page, a.node, a.arena_bytes)) return;
-  // after k_leaf_upsert only the segments it flagged for a split remain
-  if (a.split_only && a.seg_P[g] == 1) return;
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  if (!lock_page(a, page, a.tag_base + g + 1)) {
-    if (lane == 0) atomicOr(a.err, kErrLock);
-    return;
-  }
-  const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-  const Hdr h = parse_hdr(w);
-  if (h.fver != a.seg_ver[g] || h.fver != h.rver_leaf) {
-    if (lane == 0) atomicOr(a.err, kErrPlan);
-    unlock_page(a, page);
-    return;
-  }
-  stage_page(L.page, w);
-  wave_lds_sync();
-  const int P = (int)a.seg_P[g];
-  if (P == 1) {
-    // in place, sequential in key order (Tree.cpp:875-912)
-    LeafEnt e = leaf_entry(L.page, lane < kLeafCardinality ? lane : 0);
-    const bool slot = lane < kLeafCardinality;
-    bool dirty = false;
-    for (uint32_t j = st; j < en; ++j) {
-      const uint64_t kb = a.op_key[j];
-      const uint64_t vb = a.op_val[j];
-      uint64_t mm = ballot(slot && e.val != kValueNull && e.key == kb);
-      bool fresh = false;
-      if (!mm) {
-        mm = ballot(slot && e.val == kValueNull);  // first empty slot
-        fresh = true;
-        if (!mm) {
-          if (lane == 0) atomicOr(a.err, kErrOverflow);
-          break;
+  // ---- internal levels ------------------------------------------------------
+  for (uint32_t level = 1; ok && nsep > 0; ++level) {
+    if (level > (uint32_t)kMaxLevelOfTree) {
+      err |= kErrRounds;
+      break;
+    }
+    const int cur = (int)((level - 1) & 1), nxt = cur ^ 1;
+    const uint64_t* skey = a.sep_key[cur];
+    const uint64_t* sptr = a.sep_ptr[cur];
+    const uint64_t* spg = a.ipage[cur];
+    const bool grow = level == root_level;
+    // ---- I1: segment heads of my separator range; plan each under its lock --
+    uint32_t r0, r1;
+    block_range(nsep, b, nb, r0, r1);
+    uint32_t my_heads = 0, my_np = 0;
+    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
+      const uint32_t i = c0 + (uint32_t)t;
+      const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
+      uint32_t th;
+      const uint32_t x = block_scan(head ? 1u : 0u, s_red, &th);
+      __syncthreads();
+      if (head) s_list[x] = i;
+      __syncthreads();
+      for (uint32_t hx = (uint32_t)wv; hx < th; hx += kUpWaves) {
+        const uint32_t hi = s_list[hx];
+        const uint64_t page = spg[hi];
+        // segment end: first index past hi whose page differs
+        uint32_t e = hi + 1;
+        for (;;) {
+          const uint32_t j = e + (uint32_t)lane;
+          const bool diff = j >= nsep || spg[j] != page;
+          const uint64_t m = ballot(diff);
+          if (m) {
+            e += (uint32_t)ctz64(m);
+            break;
+          }
+          e += kWave;
+        }
+        const Ops o{skey, sptr, hi, e - hi};
+        uint32_t lk = 0, T2 = 0, P = 1, ver = ~0u;
+        if (!ptr_ok(page, a.node, a.arena_bytes)) {
+          err |= kErrBadPtr;
+        } else {
+          if (lane == 0) {
+            unsigned long long* wd =
+                reinterpret_cast<unsigned long long*>(a.locks) + lock_index(page, a.num_locks);
+            for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+              const unsigned long long old = atomicCAS(wd, 0ull, (unsigned long long)a.tag);
+              if (old == 0ull || old == a.tag) {
+                lk = 1;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+          lk = rl32(lk, 0);
+          if (!lk) err |= kErrLock;
+          const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+          const Hdr h = parse_hdr(w);
+          const IntRec r = internal_record(w);
+          const int cnt = h.last_index + 1;
+          const bool hit = lane >= 3 && lane - 3 < cnt && op_contains(o, r.key);
+          const uint32_t M = (uint32_t)popc64(ballot(hit));
+          T2 = (uint32_t)cnt + (e - hi) - M;
+          P = T2 <= (uint32_t)(kInternalCardinality - 1)
+                  ? 1u
+                  : (T2 + 1 + kInternalSplitFill) / (kInternalSplitFill + 1);
+          ver = h.fver;
+          if (h.fver != h.rver_internal || h.leftmost == 0 || h.level != level) {
+            err |= kErrInconsistent;
+            P = 1;
+            T2 = 0;  // left untouched (see I3)
+          }
+          if (!lk) {
+            P = 1;
+            T2 = 0;
+          }
+        }
+        if (lane == 0) {
+          a.h_end[hi] = e;
+          a.h_T[hi] = T2;
+          a.h_P[hi] = P;
+          a.h_ver[hi] = ver;
+          a.h_lk[hi] = lk;
+        }
+        my_np += P - 1;  // wave-uniform
+      }
+      my_heads += th;
+      __syncthreads();
+    }
+    {
+      const uint32_t bn = block_sum(lane == 0 ? my_np : 0u, s_red);
+      if (t == 0) {
+        ctl->int_heads[b] = my_heads;
+        ctl->int_np[b] = bn;
+      }
+    }
+    ok = grid_sync(ctl, nb, &s_flag);
+    if (!ok) break;
+    // ---- I2: dense segment list and new-page bases, in key order ------------
+    const uint32_t vh = (uint32_t)t < nb ? ctl->int_heads[t] : 0u;
+    const uint32_t vp = (uint32_t)t < nb ? ctl->int_np[t] : 0u;
+    const uint32_t nseg = block_sum(vh, s_red);
+    const uint32_t tot = block_sum(vp, s_red);
+    uint32_t run_h = block_sum((uint32_t)t < b ? vh : 0u, s_red);
+    uint32_t run_p = block_sum((uint32_t)t < b ? vp : 0u, s_red);
+    const bool fit = cursor + tot + (grow ? 1u : 0u) <= cap;
+    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
+      const uint32_t i = c0 + (uint32_t)t;
+      const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
+      const uint32_t np = head ? a.h_P[i] - 1 : 0u;
+      uint32_t th, tp;
+      const uint32_t xh = block_scan(head ? 1u : 0u, s_red, &th);
+      const uint32_t xp = block_scan(np, s_red, &tp);
+      if (head) {
+        a.d_head[run_h + xh] = i;
+        a.d_base[run_h + xh] = run_p + xp;
+      }
+      run_h += th;
+      run_p += tp;
+    }
+    if (!fit) {
+      // arena exhausted: this level stays unapplied (B-link keeps every key
+      // reachable through the siblings); release its locks
+      err |= kErrNoMem;
+      for (uint32_t i = r0 + (uint32_t)t; i < r1; i += kUpT)
+        if ((i == 0 || spg[i] != spg[i - 1]) && a.h_lk[i])
+          release_word(a.locks, a.num_locks, spg[i]);
+      break;
+    }
+    ok = grid_sync(ctl, nb, &s_flag);
+    if (!ok) break;
+    // ---- I3: new pages, then page 0 of every segment --------------------------
+    const uint64_t first = cursor;
+    const uint64_t xroot = cursor + tot;
+    for (uint64_t gp = wid; gp < tot; gp += W) {
+      const uint32_t s = last_le(a.d_base, nseg, (uint32_t)gp);
+      const uint32_t hi = a.d_head[s];
+      const uint32_t pb = a.d_base[s];
+      const int p = (int)(gp - pb) + 1;
+      const Ops o{skey, sptr, hi, a.h_end[hi] - hi};
+      const u32x4 w = load_page_slice(a.arena, ga_offset(spg[hi]));
+      const Hdr h = parse_hdr(w);
+      const int na = internal_survivors(L, w, h.last_index + 1, o);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(a.int_rd + s, 1u);
+      const SplitPage sp{p, (int)a.h_P[hi], a.h_T[hi], first + pb, new_ga(a.node, first + pb, p)};
+      const uint64_t low = build_internal_page(a, L, h, na, o, sp, level);
+      const uint64_t par_pg = grow ? a.root : parent_of(a, low, level + 1, &err);
+      if (lane == 0) {
+        a.sep_key[nxt][gp] = low;
+        a.sep_ptr[nxt][gp] = sp.dest;
+        a.ipage[nxt][gp] = par_pg;
+      }
+    }
+    for (uint64_t s = wid; s < nseg; s += W) {
+      const uint32_t hi = a.d_head[s];
+      const uint64_t page = spg[hi];
+      const int P = (int)a.h_P[hi];
+      const uint32_t T2 = a.h_T[hi];
+      if (P > 1 && !fan_in(a.int_rd + s, (uint32_t)(P - 1))) err |= kErrLock;
+      if (T2 > 0) {  // 0: inconsistent or not locked, left untouched
+        const Ops o{skey, sptr, hi, a.h_end[hi] - hi};
+        const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+        const Hdr h = parse_hdr(w);
+        if (h.fver != a.h_ver[hi] || h.fver != h.rver_internal) {
+          err |= kErrPlan;
+        } else {
+          const int na = internal_survivors(L, w, h.last_index + 1, o);
+          const bool rootsplit = grow && P > 1;
+          const uint64_t dest = rootsplit ? ga_make(a.node, xroot * kPageSize) : page;
+          const SplitPage sp{0, P, T2, first + a.d_base[s], dest};
+          (void)build_internal_page(a, L, h, na, o, sp, level);
+          if (rootsplit) write_new_root(a, L, dest, level + 1, h.fver);
         }
       }
-      if (lane == ctz64(mm)) {
-        if (fresh) e.key = kb;
-        e.val = vb;
-        const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
-        e.fraw = (e.fraw & 0xF0) | f;
-        e.rraw = (e.rraw & 0xF0) | f;
-        dirty = true;
+      if (lane == 0) {
+        a.int_rd[s] = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.h_lk[hi]) release_word(a.locks, a.num_locks, page);
       }
     }
-    wave_lds_sync();
-    if (dirty) put_leaf_entry(L.page, lane, e.key, e.val, e.fraw, e.rraw);
-    store_page(a.arena, ga_offset(page), L.page);
-    const uint64_t vm = ballot(slot && e.val != kValueNull);
-    if (a.leaf_hw && lane == 0)
-      a.leaf_hw[ga_offset(page) >> 10] = (uint8_t)(vm ? 64 - __builtin_clzll(vm) : 0);
-  } else {
-    const int na = leaf_survivors(a, L, st, en);
-    build_leaf_page(a, L, g, h, na, 0, P, a.seg_T[g], page);
+    const bool grew = grow && tot > 0;
+    cursor += tot + (grew ? 1u : 0u);
+    if (grew) root_level = level + 1;
+    made += tot;
+    nsep = tot;
+    ok = grid_sync(ctl, nb, &s_flag);
   }
-  unlock_page(a, page);
-}
-
-// Tree::del on each segment (leaf_page_del, Tree.cpp:1037-1055)
-__global__ __launch_bounds__(kBlock) void k_leaf_delete(SegArgs a) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const int lane = lane_id();
-  const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= a.num_seg) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint64_t page = a.seg_page[g];
-  if (!ptr_ok(page, a.node, a.arena_bytes)) return;
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  if (!lock_page(a, page, a.tag_base + g + 1)) {
-    if (lane == 0) atomicOr(a.err, kErrLock);
-    return;
-  }
-  const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-  const Hdr h = parse_hdr(w);
-  if (h.fver != h.rver_leaf) {
-    if (lane == 0) atomicOr(a.err, kErrInconsistent);
-    unlock_page(a, page);
-    return;
-  }
-  stage_page(L.page, w);
-  wave_lds_sync();
-  LeafEnt e = leaf_entry(L.page, lane < kLeafCardinality ? lane : 0);
-  const bool hit = lane < kLeafCardinality && e.val != kValueNull &&
-                   op_contains(a, st, en, e.key);
-  if (ballot(hit)) {
-    if (hit) {
-      e.val = kValueNull;
-      const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
-      e.fraw = (e.fraw & 0xF0) | f;
-      e.rraw = (e.rraw & 0xF0) | f;
+  if (!ok) err |= kErrRounds;
+  if (err && lane == 0) atomicOr(a.err, err);
+  if (b == 0 && t == 0) {
+    // superblock (device-authoritative) and its host mirror
+    sb->next_page = cursor;
+    sb->root_level = root_level;
+    sb->splits += made;
+    sb->batches = a.batch;
+    if (a.pub) {
+      __hip_atomic_store(a.pub + 1, cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.pub + 2, (uint64_t)root_level, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.pub + 3, sb->splits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    wave_lds_sync();
-    if (hit) put_leaf_entry(L.page, lane, e.key, e.val, e.fraw, e.rraw);
-    store_page(a.arena, ga_offset(page), L.page);
   }
-  unlock_page(a, page);
 }
 
 // ---------------------------------------------------------------------------
-// internal plan: T = cnt + ops - matched; P = 1 if T <= 60 else
-// ceil((T + 1) / 41) (each extra page pushes one record up)
-__global__ __launch_bounds__(kBlock) void k_int_plan(SegArgs a) {
+// Tree::del for every key of dk[0, *n_del) (leaf_page_del, Tree.cpp:993-1057):
+// one wave per key, grid-stride.  Walk from the leaf directory (or the root)
+// with page_search's sibling rule, lock the leaf's word, re-read it under the
+// lock (turning right again if needed), clear the first valid slot holding
+// the key (value = kValueNull, f++ , r = f) and write back that 18 B entry,
+// then release.  Keys are unique in the batch, so two waves never touch one
+// entry; they may share a page and serialise on its word.
+__global__ __launch_bounds__(kBlock) void k_delete(DelArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock][kPageDwords + 8];
   const int lane = lane_id();
-  const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= a.num_seg) return;
-  // a.num_seg may be an upper bound (num_seg_dev): zero the new-page counts
-  // past the device-side count, which the scan after this kernel covers
-  if (a.num_seg_dev && g >= *a.num_seg_dev) {
-    if (lane == 0) a.seg_newpages[g] = 0;
-    return;
-  }
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  const uint64_t page = a.seg_page[g];
-  if (!ptr_ok(page, a.node, a.arena_bytes)) {
-    if (lane == 0) {
-      atomicOr(a.err, kErrBadPtr);
-      a.seg_T[g] = 0; a.seg_P[g] = 1; a.seg_newpages[g] = 0; a.seg_ver[g] = ~0u;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t n = *a.n_del;
+  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint32_t* lp = s_pg[wv];
+  uint32_t err = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + wv; i < n; i += W) {
+    const uint64_t k = a.keys[i];
+    uint64_t ptr = a.root;
+    if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+    bool locked = false;
+    uint64_t lw = 0;
+    int retries = 0;
+    for (int hop = 0;; ++hop) {
+      if (hop > kMaxRounds) {
+        err |= kErrRounds;
+        break;
+      }
+      if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
+        err |= kErrBadPtr;
+        break;
+      }
+      const u32x4 w0 = load_page_slice(a.arena, ga_offset(ptr));
+      const Hdr h0 = parse_hdr(w0);
+      const bool leaf0 = h0.leftmost == 0;
+      if (h0.fver != (leaf0 ? h0.rver_leaf : h0.rver_internal)) {
+        if (++retries > kMaxRetries) {
+          err |= kErrInconsistent;
+          break;
+        }
+        continue;
+      }
+      if (k >= h0.highest && h0.sibling != 0) {
+        ptr = h0.sibling;
+        continue;
+      }
+      if (k < h0.lowest || k >= h0.highest) {
+        err |= kErrFence;
+        break;
+      }
+      if (!leaf0) {
+        const IntRec r = internal_record(w0);
+        const int cnt = h0.last_index + 1;
+        const int pos = popc64(ballot(lane >= 3 && lane - 3 < cnt && r.key <= k));
+        ptr = pos == 0 ? h0.leftmost : rl64(r.ptr, pos + 2);
+        continue;
+      }
+      // the leaf: lock_and_read_page (Tree.cpp:1014-1015)
+      lw = (uint64_t)lock_index(ptr, a.num_locks);
+      uint32_t got = 0;
+      if (lane == 0) {
+        unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.locks) + lw;
+        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+          if (atomicCAS(wd, 0ull, (unsigned long long)a.tag) == 0ull) {
+            got = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (rl32(got, 0) == 0) {
+        err |= kErrLock;
+        break;
+      }
+      locked = true;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const u32x4 w = load_page_slice(a.arena, ga_offset(ptr));
+      const Hdr h = parse_hdr(w);
+      if (h.fver != h.rver_leaf) {
+        err |= kErrInconsistent;
+        break;
+      }
+      if (k >= h.highest && h.sibling != 0) {  // Tree.cpp:1028-1032
+        if (lane == 0)
+          __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        locked = false;
+        ptr = h.sibling;
+        continue;
+      }
+      stage_page(lp, w);
+      wave_lds_sync();
+      LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
+      const uint64_t m = ballot(lane < kLeafCardinality && e.key == k && e.val != kValueNull);
+      if (m && lane == ctz64(m)) {
+        const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
+        put_leaf_entry(reinterpret_cast<uint32_t*>(a.arena + ga_offset(ptr)), lane, k,
+                       kValueNull, (e.fraw & 0xF0) | f, (e.rraw & 0xF0) | f);
+      }
+      break;
     }
-    return;
+    if (locked) {
+      // write_page_and_unlock (Tree.cpp:1049-1052): the entry store first
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
-  const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-  const Hdr h = parse_hdr(w);
-  const IntRec r = internal_record(w);
-  const int cnt = h.last_index + 1;
-  const bool valid = lane >= 3 && lane - 3 < cnt;
-  const bool hit = valid && op_contains(a, st, en, r.key);
-  const uint32_t M = (uint32_t)popc64(ballot(hit));
-  const uint32_t T = (uint32_t)cnt + (en - st) - M;
-  const uint32_t P = T <= (uint32_t)(kInternalCardinality - 1)
-                         ? 1u
-                         : (T + 1 + kInternalSplitFill) / (kInternalSplitFill + 1);
-  if (lane == 0) {
-    a.seg_T[g] = T;
-    a.seg_P[g] = P;
-    a.seg_newpages[g] = P - 1;
-    a.seg_ver[g] = h.fver;
-    if (h.fver != h.rver_internal || h.leftmost == 0 || (int)h.level != a.level)
-      atomicOr(a.err, kErrInconsistent);
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_int_build(SegArgs a, uint32_t total) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const uint32_t gp = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (gp >= total) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint32_t g = seg_of_new_page(a, gp);
-  const int p = (int)(gp - a.seg_pbase[g]) + 1;
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
-  const Hdr h = parse_hdr(w);
-  const int na = internal_survivors(a, L, w, h.last_index + 1, st, en);
-  build_internal_page(a, L, g, h, na, p, (int)a.seg_P[g], a.seg_T[g],
-                      new_page_ga(a, g, p));
-}
-
-__global__ __launch_bounds__(kBlock) void k_int_update(SegArgs a) {
-  __shared__ __attribute__((aligned(16))) WaveLds s_l[kWavesPerBlock];
-  const int lane = lane_id();
-  const uint32_t g = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (g >= a.num_seg) return;
-  WaveLds& L = s_l[threadIdx.x >> 6];
-  const uint64_t page = a.seg_page[g];
-  if (!ptr_ok(page, a.node, a.arena_bytes)) return;
-  const uint32_t st = a.seg_start[g], en = a.seg_start[g + 1];
-  if (!lock_page(a, page, a.tag_base + g + 1)) {
-    if (lane == 0) atomicOr(a.err, kErrLock);
-    return;
-  }
-  const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-  const Hdr h = parse_hdr(w);
-  if (h.fver != a.seg_ver[g] || h.fver != h.rver_internal) {
-    if (lane == 0) atomicOr(a.err, kErrPlan);
-    unlock_page(a, page);
-    return;
-  }
-  const int na = internal_survivors(a, L, w, h.last_index + 1, st, en);
-  build_internal_page(a, L, g, h, na, 0, (int)a.seg_P[g], a.seg_T[g], page);
-  unlock_page(a, page);
-}
-
-// InternalPage(level) with leftmost = old root and no records; the level's
-// separators are then inserted into it (update_new_root, Tree.cpp:126-149).
-__global__ void k_new_root(uint8_t* arena, uint64_t off, uint64_t old_root,
-                           uint32_t level) {
-  __shared__ __attribute__((aligned(16))) uint32_t lp[kPageDwords + 8];
-  init_page_image(lp, 1, old_root, 0, level, -1, kKeyMin, kKeyMax);
-  wave_lds_sync();
-  if (lane_id() == 0) lp[kOffInternalRear / 4] = 1;
-  store_page(arena, off, lp);
+  if (err && lane == 0) atomicOr(a.err, err);
 }
 
 // LeafPage() + set_consistent (Tree.cpp:47-52)
@@ -525,34 +848,27 @@ __global__ void k_write_superblock(uint8_t* arena, Superblock sb) {
 }
 
 // ---------------------------------------------------------------------------
-static dim3 seg_grid(uint64_t waves) {
-  return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+uint32_t upper_blocks() {
+  static const uint32_t nb = [] {
+    int cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int n = cus > 0 ? cus : 256;
+    return (uint32_t)(n < kMaxUpper ? n : kMaxUpper);
+  }();
+  return nb;
 }
-void launch_leaf_plan(const SegArgs& a, hipStream_t s) {
-  if (a.num_seg) hipLaunchKernelGGL(k_leaf_plan, seg_grid(a.num_seg), dim3(kBlock), 0, s, a);
+
+void launch_upper(const UpperArgs& a, hipStream_t s) {
+  // one block per CU: every block resident (grid barriers); 512 threads,
+  // ~20 KB of LDS
+  hipLaunchKernelGGL(k_upper, dim3(upper_blocks()), dim3(kUpT), 0, s, a);
 }
-void launch_leaf_build(const SegArgs& a, uint32_t total, hipStream_t s) {
-  if (total) hipLaunchKernelGGL(k_leaf_build, seg_grid(total), dim3(kBlock), 0, s, a, total);
+
+void launch_delete(const DelArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_delete, dim3(2 * upper_blocks()), dim3(kBlock), 0, s, a);
 }
-void launch_leaf_update(const SegArgs& a, hipStream_t s) {
-  if (a.num_seg) hipLaunchKernelGGL(k_leaf_update, seg_grid(a.num_seg), dim3(kBlock), 0, s, a);
-}
-void launch_leaf_delete(const SegArgs& a, hipStream_t s) {
-  if (a.num_seg) hipLaunchKernelGGL(k_leaf_delete, seg_grid(a.num_seg), dim3(kBlock), 0, s, a);
-}
-void launch_int_plan(const SegArgs& a, hipStream_t s) {
-  if (a.num_seg) hipLaunchKernelGGL(k_int_plan, seg_grid(a.num_seg), dim3(kBlock), 0, s, a);
-}
-void launch_int_build(const SegArgs& a, uint32_t total, hipStream_t s) {
-  if (total) hipLaunchKernelGGL(k_int_build, seg_grid(total), dim3(kBlock), 0, s, a, total);
-}
-void launch_int_update(const SegArgs& a, hipStream_t s) {
-  if (a.num_seg) hipLaunchKernelGGL(k_int_update, seg_grid(a.num_seg), dim3(kBlock), 0, s, a);
-}
-void launch_new_root(uint8_t* arena, uint64_t off, uint64_t old_root,
-                     uint32_t level, hipStream_t s) {
-  hipLaunchKernelGGL(k_new_root, dim3(1), dim3(kWave), 0, s, arena, off, old_root, level);
-}
+
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s) {
   hipLaunchKernelGGL(k_write_superblock, dim3(1), dim3(kWave), 0, s, arena, sb);
 }

@@ -9,13 +9,11 @@
 //                     hitters (zipf) shrink to one op per tile here.
 //   2. coarse pass    partition.hip: 256 bins by the top 8 bits of the key's
 //                     offset in the shard range, carrying the op index.
-//   3. k_bin_sort     every bin (<= 8192 ops) fully sorted by (key, index)
-//                     in LDS, in place.  A larger bin (skewed keys) sets
-//                     kErrSortOverflow and the host re-sorts the batch with
-//                     rocPRIM instead.
-// The result is what the stable radix sort of (key, index) produced before:
-// sorted keys, equal keys adjacent in index order, so mark_unique /
-// compact_unique keep working unchanged.
+//   3. k_bin_unique   every bin: last writer per key, sorted (below); a bin
+//                     over 6144 ops (clustered keys) is sorted by the same
+//                     block with a stable LSD radix sort through global
+//                     scratch, so every batch is ordered on the device.
+//   4. k_bin_emit     every bin's survivors at its prefix: uk / uv / dk.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -85,7 +83,7 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
                                                    uint64_t* __restrict__ keys_out,
                                                    uint32_t* __restrict__ idx_out,
                                                    uint32_t* __restrict__ gcount,
-                                                   uint32_t* err) {
+                                                   uint32_t* err, uint32_t* gate, uint32_t tag) {
   // LDS hash table of the tile's distinct keys: slot -> (key, 1 + last index)
   constexpr int kSlots = 2 * kIsortTile;
   constexpr int PER = kIsortTile / kIT;
@@ -122,7 +120,11 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
       h = (h + 1) & (kSlots - 1);
     }
   }
-  if (bad) atomicOr(err, kErrKeyMax);
+  if (bad) {
+    // the chunk is rejected whole (k_bin_emit emits nothing) and reported
+    atomicOr(err, kErrKeyMax);
+    *gate = tag;
+  }
   __syncthreads();
   uint32_t keep = 0;
 #pragma unroll
@@ -139,46 +141,6 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
     }
   }
   if (t == 0) gcount[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kIT) void k_bin_sort(uint64_t* __restrict__ keys1,
-                                                 uint32_t* __restrict__ pay1,
-                                                 const uint32_t* __restrict__ bins,
-                                                 uint32_t* __restrict__ S, uint32_t* err) {
-  constexpr int kCap = kFineCap;  // 8192 keys = 96 KB of LDS
-  constexpr int PER = kCap / kIT;
-  __shared__ uint64_t skey[kCap];
-  __shared__ uint32_t sidx[kCap];
-  const int t = threadIdx.x;
-  // the coarse pass is complete: clear its group sums for the next batch
-  if (blockIdx.x == 0)
-    for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
-  const uint32_t start = bins[2 * blockIdx.x], cnt = bins[2 * blockIdx.x + 1];
-  if (cnt <= 1) return;  // block-uniform
-  if (cnt > (uint32_t)kCap) {
-    if (t == 0) atomicOr(err, kErrSortOverflow);
-    return;
-  }
-  uint32_t m = 2;
-  while (m < cnt) m <<= 1;
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const uint32_t o = (uint32_t)(r * kIT + t);
-    if (o < m) {
-      skey[o] = o < cnt ? keys1[start + o] : kKeyMax;
-      sidx[o] = o < cnt ? pay1[start + o] : ~0u;
-    }
-  }
-  __syncthreads();
-  lds_bitonic<PER>(skey, sidx, m);
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const uint32_t o = (uint32_t)(r * kIT + t);
-    if (o < cnt) {
-      keys1[start + o] = skey[o];
-      pay1[start + o] = sidx[o];
-    }
-  }
 }
 
 // ---- step 3 + 4 without the library scan: per-bin dedup, sort, emit --------
@@ -205,6 +167,122 @@ constexpr int kUniqSlots = 8192;  // LDS hash slots (96 KB with the op indices)
 constexpr int kUniqCap = 6144;    // ops per bin handled here (load <= 0.75)
 constexpr int kUniqPer = kUniqCap / kIT;
 
+
+// ---- bins over kUniqCap ops: the same result through global scratch ---------
+// Stable LSD radix sort of the bin's (key, op index) pairs by 8-bit digits,
+// one block, ping-ponging between the bin's slots of keys1 / pay1 and the
+// same slots of the scratch arrays; digits on which every key agrees are
+// skipped (clustered keys need few passes).  Equal keys stay in op-index
+// order (the input holds at most one op per key per 4096-op tile, tiles in
+// order), so the last of each run is the batch's last writer.  Survivors
+// are then compacted to the bin's front with their ranks, as in the LDS path.
+// ldsw: >= 8 x 256 + 16 x 256 + 256 + 16 words of LDS.
+__device__ void big_bin_unique(uint64_t* __restrict__ keys1, uint32_t* __restrict__ pay1,
+                               uint64_t* __restrict__ kscr, uint32_t* __restrict__ iscr,
+                               uint32_t start, uint32_t cnt, const uint64_t* __restrict__ vals,
+                               uint32_t* __restrict__ lrank, uint32_t* __restrict__ bcnt,
+                               uint32_t b, uint32_t* ldsw) {
+  constexpr int kW = kIT / kWave;  // 16 waves
+  uint32_t* h8 = ldsw;                  // [8][256] digit histograms
+  uint32_t* wc = ldsw + 8 * 256;        // [16][256] per-wave digit counts
+  uint32_t* base = wc + kW * 256;       // [256] running digit offsets
+  uint32_t* wsum = base + 256;          // [16]
+  const int t = threadIdx.x, w = t >> 6;
+  for (int j = t; j < 8 * 256; j += kIT) h8[j] = 0;
+  __syncthreads();
+  for (uint32_t e = (uint32_t)t; e < cnt; e += kIT) {
+    const uint64_t k = keys1[start + e];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) atomicAdd(&h8[d * 256 + ((k >> (8 * d)) & 255)], 1u);
+  }
+  __syncthreads();
+  uint64_t* ka = keys1 + start;
+  uint32_t* ia = pay1 + start;
+  uint64_t* kb = kscr + start;
+  uint32_t* ib = iscr + start;
+  for (int d = 0; d < 8; ++d) {
+    // skip a digit every key shares (block-uniform after the barrier)
+    const uint32_t hv = t < 256 ? h8[d * 256 + t] : 0u;
+    if (__syncthreads_or(hv == cnt)) continue;
+    uint32_t tot;
+    const uint32_t ex = block_scan(hv, wsum, &tot);
+    if (t < 256) base[t] = ex;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < cnt; c0 += kIT) {
+      for (int j = t; j < kW * 256; j += kIT) wc[j] = 0;
+      __syncthreads();
+      const uint32_t e = c0 + (uint32_t)t;
+      const bool valid = e < cnt;
+      const uint64_t k = valid ? ka[e] : 0;
+      const uint32_t ix = valid ? ia[e] : 0;
+      const uint32_t dg = (uint32_t)(k >> (8 * d)) & 255u;
+      // lanes of this wave holding the same digit: rank among them in lane order
+      uint64_t m = ballot(valid);
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t on = ballot(valid && ((dg >> bit) & 1u));
+        m &= ((dg >> bit) & 1u) ? on : ~on;
+      }
+      const uint32_t rk = (uint32_t)popc64(m & lanemask_lt());
+      if (valid && rk == 0) wc[w * 256 + dg] = (uint32_t)popc64(m);
+      __syncthreads();
+      if (t < 256) {  // digit t: offsets of its elements per wave, in wave order
+        uint32_t run = base[t];
+        for (int x = 0; x < kW; ++x) {
+          const uint32_t v = wc[x * 256 + t];
+          wc[x * 256 + t] = run;
+          run += v;
+        }
+        base[t] = run;
+      }
+      __syncthreads();
+      if (valid) {
+        const uint32_t p = wc[w * 256 + dg] + rk;
+        kb[p] = k;
+        ib[p] = ix;
+      }
+      __syncthreads();
+    }
+    uint64_t* tk = ka;
+    ka = kb;
+    kb = tk;
+    uint32_t* ti = ia;
+    ia = ib;
+    ib = ti;
+  }
+  // survivors (last of each run of equal keys) compacted to keys1 / pay1 at
+  // the bin's front; ranks among upserts / deletes (bit 31)
+  uint32_t ru = 0, rd = 0, rs = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kIT) {
+    const uint32_t e = c0 + (uint32_t)t;
+    const bool valid = e < cnt;
+    const uint64_t k = valid ? ka[e] : 0;
+    const uint32_t ix = valid ? ia[e] : 0;
+    const bool surv = valid && (e + 1 == cnt || ka[e + 1] != k);
+    const bool del = surv && vals[ix] == kValueNull;
+    uint32_t tu, td, ts;
+    const uint32_t xu = block_scan(surv && !del ? 1u : 0u, wsum, &tu);
+    const uint32_t xd = block_scan(del ? 1u : 0u, wsum, &td);
+    const uint32_t xs = block_scan(surv ? 1u : 0u, wsum, &ts);
+    // every read of this tile is done: positions < c0 + kIT, later tiles
+    // read from c0 + kIT on
+    __syncthreads();
+    if (surv) {
+      keys1[start + rs + xs] = k;
+      pay1[start + rs + xs] = ix;
+      lrank[start + rs + xs] = del ? (0x80000000u | (rd + xd)) : (ru + xu);
+    }
+    ru += tu;
+    rd += td;
+    rs += ts;
+    __syncthreads();
+  }
+  if (t == 0) {
+    bcnt[2 * b] = ru;
+    bcnt[2 * b + 1] = rd;
+  }
+}
+
 __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1,
                                                    uint32_t* __restrict__ pay1,
                                                    const uint32_t* __restrict__ bins,
@@ -212,7 +290,10 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
                                                    const uint64_t* __restrict__ vals,
                                                    uint32_t* __restrict__ lrank,
                                                    uint32_t* __restrict__ bcnt,
-                                                   uint32_t* __restrict__ S, uint32_t* err) {
+                                                   uint64_t* __restrict__ kscr,
+                                                   uint32_t* __restrict__ iscr,
+                                                   uint32_t* __restrict__ S,
+                                                   const uint32_t* gate, uint32_t tag) {
   constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
   __shared__ unsigned long long hkey[kUniqSlots];  // hash, then the sorted keys
   __shared__ uint32_t hidx[kUniqSlots];            // 1 + op index, then op index
@@ -224,12 +305,11 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   // the coarse pass is complete: clear its group sums for the next batch
   if (b == 0)
     for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
+  if (*gate == tag) return;  // rejected chunk (k_bin_emit emits nothing)
   const uint32_t start = bins[2 * b], cnt = bins[2 * b + 1];
   if (cnt > (uint32_t)kUniqCap) {  // block-uniform
-    if (t == 0) {
-      atomicOr(err, kErrSortOverflow);  // the host re-orders with rocPRIM
-      bcnt[2 * b] = bcnt[2 * b + 1] = 0;
-    }
+    big_bin_unique(keys1, pay1, kscr, iscr, start, cnt, vals, lrank, bcnt, b,
+                   reinterpret_cast<uint32_t*>(hkey));
     return;
   }
   // a. last writer per key
@@ -353,10 +433,14 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
                                                  uint64_t* __restrict__ uv,
                                                  uint64_t* __restrict__ dk,
                                                  uint64_t* __restrict__ counts,
-                                                 const uint32_t* __restrict__ err) {
+                                                 const uint32_t* gate, uint32_t tag) {
   __shared__ uint32_t su[4], sd[4];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
+  if (*gate == tag) {  // kKeyMax in the chunk: nothing to apply
+    if (b == 0 && t == 0) counts[0] = counts[1] = 0;
+    return;
+  }
   // prefix over bins < b (and the totals): thread t holds bin t
   uint32_t cu = bcnt[2 * t], cd = bcnt[2 * t + 1];
   uint32_t pu = (uint32_t)t < b ? cu : 0u, pd = (uint32_t)t < b ? cd : 0u;
@@ -383,7 +467,6 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
     if (t == 0) {
       counts[0] = (uint64_t)su[0] + su[1] + su[2] + su[3];
       counts[1] = (uint64_t)sd[0] + sd[1] + sd[2] + sd[3];
-      counts[2] = *err;  // set by k_tile_dedup / k_bin_unique, read back with the counts
     }
   }
   const uint32_t start = bins[2 * b];
@@ -401,27 +484,24 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
 }
 
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
-                       uint32_t* gcount, uint32_t* err, hipStream_t s) {
+                       uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
+                       hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)((n + kIsortTile - 1) / kIsortTile)),
-                     dim3(kIT), 0, s, keys, n, keys_out, idx_out, gcount, err);
-}
-
-void launch_bin_sort(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint32_t* S,
-                     uint32_t* err, hipStream_t s) {
-  hipLaunchKernelGGL(k_bin_sort, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, S, err);
+                     dim3(kIT), 0, s, keys, n, keys_out, idx_out, gcount, err, gate, tag);
 }
 
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
-                       uint64_t* uk, uint64_t* uv, uint64_t* dk, uint64_t* counts, uint32_t* S,
-                       uint32_t* err, hipStream_t s) {
+                       uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
+                       uint64_t* counts, uint32_t* S, const uint32_t* gate, uint32_t tag,
+                       hipStream_t s) {
   const KeyRange kr{key_lo, key_bits};
   hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
-                     lrank, bcnt, S, err);
+                     lrank, bcnt, kscr, iscr, S, gate, tag);
   hipLaunchKernelGGL(k_bin_emit, dim3(kCoarse), dim3(256), 0, s, (const uint64_t*)keys1,
                      (const uint32_t*)pay1, (const uint32_t*)lrank, bins,
-                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts, (const uint32_t*)err);
+                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts, gate, tag);
 }
 
 }  // namespace dev

@@ -101,6 +101,7 @@ constexpr uint32_t kErrFence = 1u << 3;        // k < lowest on a walk
 constexpr uint32_t kErrLock = 1u << 4;         // lock spin bound exceeded
 constexpr uint32_t kErrPlan = 1u << 5;         // page changed between plan/apply
 constexpr uint32_t kErrOverflow = 1u << 6;     // page overfull at apply
+constexpr uint32_t kErrNoMem = 1u << 7;        // page arena exhausted (splits left unapplied)
 
 // CityHash64 v1.1 (google/cityhash, city.cc HashLen0to16 for len == 8).
 // Third-party dependency of the reference (script/installLibs.sh:16-20, HEAD,

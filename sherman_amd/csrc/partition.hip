@@ -18,9 +18,6 @@
 //   fine           : one block per <= kFineCap-key chunk of a coarse bin:
 //                    counting sort on the next 8 bits inside the chunk's own
 //                    range -> keys_out[p], src[p] = keys1 slot it came from
-//                    (direct mode: the coarse pass carries each key's input
-//                    index instead of writing pos1, src[p] = that index, the
-//                    walk stores results in input order, no unpartition)
 //   (walk)         : result of slot p stored at vals1[src[p]] — a scatter
 //                    confined to the chunk's range, which stays in L2
 //   unpartition    : out[i] = vals1[pos1[i]], found[i] = out[i] != 0
@@ -313,8 +310,7 @@ uint32_t partition_chunk_slots(uint64_t n) {
 
 void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_t key_bits,
                       uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
-                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, bool direct,
-                      hipStream_t s) {
+                      uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s) {
   if (!n) return;
   const KeyRange kr{key_lo, key_bits};
   const uint64_t all_groups = (n + kGrpKeys - 1) / kGrpKeys;
@@ -325,12 +321,10 @@ void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_
                      (const uint32_t*)nullptr, groups, M, S);
   hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, groups, tiles,
-                     (const uint32_t*)M, (const uint32_t*)S, keys1,
-                     direct ? pos1 : (uint32_t*)nullptr, direct ? (uint32_t*)nullptr : pos1,
+                     (const uint32_t*)M, (const uint32_t*)S, keys1, (uint32_t*)nullptr, pos1,
                      chunks, slots, (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_part_fine, dim3(slots), dim3(kPT), 0, s, (const uint64_t*)keys1,
-                     direct ? (const uint32_t*)pos1 : (const uint32_t*)nullptr, kr,
-                     (const uint32_t*)chunks, S, keys_out, src);
+                     (const uint32_t*)nullptr, kr, (const uint32_t*)chunks, S, keys_out, src);
 }
 
 void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* gcount,

@@ -102,44 +102,6 @@ void launch_range(const RangeArgs& a, hipStream_t s) {
                      dim3(kRangeWaves * kWave), 0, s, a);
 }
 
-// out[0] = offsets[n-1] + counts[n-1] (the scan's total), out[1] = *err
-__global__ void k_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_t n,
-                              const uint32_t* err, uint64_t* out) {
-  if (threadIdx.x == 0) {
-    out[0] = offsets[n - 1] + counts[n - 1];
-    out[1] = *err;
-  }
-}
-
-void launch_range_total(const uint64_t* offsets, const uint64_t* counts, uint64_t n,
-                        const uint32_t* err, uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_range_total, dim3(1), dim3(64), 0, s, offsets, counts, n, err, out);
-}
-
-// dst[i] = *src[i], i < 4: gathers scattered u32 results for one read-back
-__global__ void k_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
-                              const uint32_t* s2, const uint32_t* s3) {
-  if (threadIdx.x == 0) {
-    dst[0] = *s0;
-    dst[1] = *s1;
-    dst[2] = *s2;
-    dst[3] = *s3;
-  }
-}
-
-void launch_gather4_u32(uint32_t* dst, const uint32_t* s0, const uint32_t* s1,
-                        const uint32_t* s2, const uint32_t* s3, hipStream_t s) {
-  hipLaunchKernelGGL(k_gather4_u32, dim3(1), dim3(64), 0, s, dst, s0, s1, s2, s3);
-}
-
-__global__ void k_gather_u32(uint32_t* dst, Gather8 g) {
-  if ((int)threadIdx.x < g.n) dst[threadIdx.x] = *g.p[threadIdx.x];
-}
-
-void launch_gather_u32(uint32_t* dst, const Gather8& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_gather_u32, dim3(1), dim3(64), 0, s, dst, g);
-}
-
 // zero-copy read-back (tree.cpp readback): one wave copies the words into
 // mapped host memory with vector stores, fences at system scope, then lane 0
 // publishes the sequence number the host spins on
@@ -155,20 +117,6 @@ __global__ void k_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
                      uint32_t seq, hipStream_t s) {
   hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, dst, src, nw, flag, seq);
-}
-
-// the same for scattered words: dst[i] = *g.p[i]
-__global__ void k_readback_gather(uint32_t* dst, Gather8 g, uint32_t* flag, uint32_t seq) {
-  const int l = (int)threadIdx.x;
-  if (l < g.n) dst[l] = *g.p[l];
-  __threadfence_system();
-  __syncthreads();
-  if (l == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-void launch_readback_gather(uint32_t* dst, const Gather8& g, uint32_t* flag, uint32_t seq,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(k_readback_gather, dim3(1), dim3(64), 0, s, dst, g, flag, seq);
 }
 
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {

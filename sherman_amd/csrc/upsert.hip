@@ -3,13 +3,10 @@
 // (src/Tree.cpp:828-920).
 //
 // The batch's sorted unique keys are grouped into segments, one per target
-// leaf (tree.cpp: segment()).  A wave takes G = 4 consecutive segments:
-//   * lock: lanes 0..G-1 atomicCAS(0 -> tag) their segment's lock word
-//     lock[CityHash64(page) % num_locks] (the reference's on-chip lock word,
-//     Tree.cpp:832-842, 205-242), all at once.  If any word is held by
-//     another wave, the wave drops what it took and takes the words one at a
-//     time in increasing order, so no two waves ever wait on each other in a
-//     cycle.  Every spin is bounded (kErrLock).
+// leaf, and every segment's lock word lock[CityHash64(page) % num_locks] (the
+// reference's on-chip lock word, Tree.cpp:832-842, 205-242) is taken ahead by
+// the segmentation kernel (util.hip k_seg_fill_scan).  A wave takes G = 4
+// consecutive segments:
 //   * stage: the G pages by LDS-DMA, read under the locks
 //     (lock_and_read_page, Tree.cpp:851-852), checked with check_consistent
 //     (front == rear, Tree.cpp:857) and the fences of every key.
@@ -19,11 +16,11 @@
 //     f_version++ and r_version = f_version, 4-bit (Tree.cpp:878-912).
 //   * write back only the changed 18 B entries (the reference writes the
 //     entry, not the page: write_page_and_unlock(update_addr, ...),
-//     Tree.cpp:915-920), then release the locks.
+//     Tree.cpp:915-920); k_upper releases the words.
 // A segment whose page would reach 54 entries (the split point,
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
-// k-way split path of insert.hip; seg_T / seg_ver feed that path exactly as
-// the plan kernel's outputs did.
+// k-way split of insert.hip (k_upper), which also learns here how many new
+// pages each of its block ranges needs (UpperCtl.leaf_np / leaf_ns).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -37,24 +34,6 @@ namespace shm {
 namespace dev {
 
 namespace {
-
-__device__ __forceinline__ uint32_t lock_word(uint64_t page, uint32_t n) {
-  return (uint32_t)(cityhash64_u64(page) % n);
-}
-
-// release the distinct lock words of the lanes in m (lane 0 stores); the
-// wave's page stores are performed first (write, then unlock, Tree.cpp:266-298)
-__device__ __forceinline__ void release_words(unsigned long long* lk, uint32_t lw, uint64_t m) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (uint64_t r = m; r; r &= r - 1) {
-    const int s = ctz64(r);
-    const uint32_t w = rl32(lw, s);
-    bool dup = false;
-    for (uint64_t e = m & ((1ull << s) - 1); e; e &= e - 1) dup = dup || rl32(lw, ctz64(e)) == w;
-    if (!dup && lane_id() == 0)
-      __hip_atomic_store(lk + w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 
 }  // namespace
 
@@ -205,131 +184,24 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     if (live && !over && li == 0) a.leaf_hw[ga_offset(qpage) >> 10] = (uint8_t)hw;
   }
   const uint64_t gq = g0 + (uint64_t)q;
-  if (li == 0 && q < G && gq >= num_seg && gq < a.num_seg) a.seg_newpages[gq] = 0;
   if (li == 0 && q < G && gq < num_seg) {
     const uint32_t P = (live && over) ? (T + kLeafSplitFill - 1) / kLeafSplitFill : 1u;
     a.seg_T[gq] = live ? T : 0u;
     a.seg_P[gq] = P;
     a.seg_newpages[gq] = P - 1;
     a.seg_ver[gq] = live ? fver : ~0u;
+    if (P > 1) {
+      // k_upper block range of this segment (insert.hip block_range)
+      const uint32_t r = (uint32_t)((gq * a.up_nb) / num_seg);
+      atomicAdd(&a.ctl->leaf_np[a.par][r], P - 1);
+      atomicAdd(&a.ctl->leaf_ns[a.par][r], 1u);
+    }
   }
   return err;
 }
 
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_leaf_upsert(SegArgs a) {
-  constexpr int L = kWave / G;                       // lanes per page
-  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * G * kPageDwords];
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
-  const uint64_t g0 = wid * G;
-  // the grid may be sized for an upper bound of the segment count
-  // an ordering error flagged on the device (kKeyMax in the batch, a bin
-  // too large) rejects the batch before anything is written: the host sees
-  // it at its next read-back and re-orders or returns SHM_EINVAL
-  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
-  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
-  if (g0 >= num_seg) {
-    // past the last segment: zero the new-page counts the host scans
-    if (lane < G && g0 + (uint64_t)lane < a.num_seg) a.seg_newpages[g0 + lane] = 0;
-    return;  // wave-uniform
-  }
-  const uint32_t* buf = &s_pg[wv * G * kPageDwords];
-  const uint32_t buf_lds = lds_addr_of(buf);
-  uint32_t err = 0;
-
-  // ---- slot s (lane s < G) = segment g0 + s --------------------------------
-  const bool sl = lane < G && g0 + (uint64_t)lane < num_seg;
-  const uint64_t gs = sl ? g0 + (uint64_t)lane : g0;
-  const uint64_t page = sl ? a.seg_page[gs] : 0;
-  const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
-  if (ballot(sl && !pgok)) err |= kErrBadPtr;
-  // lock words taken ahead (k_seg_fill, SegArgs.seg_lk): a segment whose
-  // word could not be taken is skipped (kErrLock is already set)
-  const bool pre = a.seg_lk != nullptr;
-  const bool pok = pgok && (!pre || a.seg_lk[gs] != 0);
-  const uint32_t st = sl ? a.seg_start[gs] : 0u;
-  const uint32_t en = sl ? a.seg_start[gs + 1] : 0u;
-  // prefetch: lane li of group q holds op li of segment q (ops >= L are read
-  // in the apply loop), so the loop below makes no global round trip for the
-  // first L ops; the loads overlap the lock and the page staging
-  const int q = lane / L;
-  const int li = lane % L;
-  const uint32_t qst = shfl32(st, q), qen = shfl32(en, q);
-  const bool pf = (uint32_t)li < qen - qst;
-  const uint64_t pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
-  const uint64_t pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
-
-  // ---- lock -------------------------------------------------------------------
-  unsigned long long* lk = reinterpret_cast<unsigned long long*>(a.locks);
-  const uint32_t lw = pok ? lock_word(page, a.num_locks) : 0u;
-  const unsigned long long tag = (unsigned long long)(a.tag_base + wid + 1);
-  const uint64_t wantm = ballot(pok);
-  bool own = false, have = !pok || pre;
-  if (pok && !pre) {
-    // lanes sharing a word: the first takes it, the others see our tag
-    const unsigned long long o = atomicCAS(lk + lw, 0ull, tag);
-    own = o == 0ull;
-    have = own || o == tag;
-  }
-  bool locked = true;
-  if (ballot(!have)) {
-    release_words(lk, lw, ballot(own));
-    // one at a time, increasing word order
-    bool first = true;
-    uint32_t prev = 0;
-    for (int it = 0; it < G && locked; ++it) {
-      uint32_t best = ~0u;
-      bool found = false;
-      for (uint64_t r = wantm; r; r &= r - 1) {
-        const uint32_t w = rl32(lw, ctz64(r));
-        if ((first || w > prev) && (!found || w < best)) {
-          best = w;
-          found = true;
-        }
-      }
-      if (!found) break;
-      uint32_t ok = 0;
-      if (lane == 0) {
-        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-          if (atomicCAS(lk + best, 0ull, tag) == 0ull) {
-            ok = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      if (rl32(ok, 0) == 0) {
-        // give up: release the words below `best` and fail the group
-        uint64_t held = 0;
-        for (uint64_t r = wantm; r; r &= r - 1) {
-          const int s = ctz64(r);
-          if (!first && rl32(lw, s) <= prev) held |= 1ull << s;
-        }
-        release_words(lk, lw, held);
-        err |= kErrLock;
-        locked = false;
-      }
-      prev = best;
-      first = false;
-    }
-  }
-
-  // ---- stage the pages under the locks ---------------------------------------
-#pragma unroll
-  for (int s = 0; s < G; ++s)
-    glds16(a.arena + ga_offset(rl64(pok && locked ? page : 0, s)),
-           buf_lds + (uint32_t)(s * kPageSize));
-  wait_vm<0>();
-
-  err |= apply_group<G>(a, buf, g0, num_seg, page, pok, locked, qst, qen, pk, pv);
-  if (locked && !pre) release_words(lk, lw, wantm);  // else k_seg_unlock
-  if (err) atomicOr(a.err, err);
-}
-
-// Software-pipelined variant for lock words taken ahead (SegArgs.seg_lk): a
-// grid of about one resident wave set; each wave loops over groups
+// Software-pipelined: a grid of about one resident wave set; each wave loops
+// over groups
 // w, w + W, ... and, while it applies group g from one LDS buffer, the pages
 // of group g + W are already landing in the other (LDS-DMA) and the segment
 // records of g + 2W and the ops of g + W are in flight.  Per group the wave
@@ -342,11 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   const int wv = threadIdx.x >> 6;
   const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
-  const bool gate = (*a.err & (kErrKeyMax | kErrSortOverflow)) != 0;
-  const uint32_t num_seg = gate ? 0u : a.num_seg_dev ? *a.num_seg_dev : a.num_seg;
-  // the host scans a.num_seg (an upper bound) new-page counts
-  for (uint64_t i = (uint64_t)num_seg + w * kWave + (uint64_t)lane; i < a.num_seg; i += W * kWave)
-    a.seg_newpages[i] = 0;
+  const uint32_t num_seg = *a.num_seg_dev;
   const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
   uint64_t g = w;
   if (g >= ngroups) return;  // wave-uniform
@@ -427,29 +295,16 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
 void launch_leaf_upsert(const SegArgs& a, hipStream_t s) {
   constexpr int G = 4;
   if (!a.num_seg) return;
-  // SHM_UPSERT_PIPE=0: one group per wave even with the lock words taken ahead
-  static const bool pipe = [] {
-    const char* e = getenv("SHM_UPSERT_PIPE");
-    return !(e && strcmp(e, "0") == 0);
+  static const unsigned blocks = [] {
+    int per_cu = 0, cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_leaf_upsert_pipe<G>, kBlock, 0);
+    return (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
   }();
-  if (pipe && a.seg_lk) {
-    static const unsigned blocks = [] {
-      int per_cu = 0, cus = 0, dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_leaf_upsert_pipe<G>,
-                                                          kBlock, 0);
-      return (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
-    }();
-    const uint64_t groups = (a.num_seg + G - 1) / G;
-    const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, blocks)),
-                       dim3(kBlock), 0, s, a);
-    return;
-  }
-  const uint64_t waves = (a.num_seg + G - 1) / G;
-  hipLaunchKernelGGL(k_leaf_upsert<G>, dim3((unsigned)((waves + kWavesPerBlock - 1) /
-                                                       kWavesPerBlock)),
+  const uint64_t groups = (a.num_seg + G - 1) / G;
+  const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, blocks)),
                      dim3(kBlock), 0, s, a);
 }
 

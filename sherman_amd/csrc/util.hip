@@ -1,5 +1,5 @@
-// util.hip — batch bookkeeping kernels (sort companions, segmentation,
-// multi-GPU routing, key generation) and the batched range scan.
+// util.hip — batch bookkeeping kernels (segmentation with lock-ahead, tile
+// scans, multi-GPU routing, key generation).
 #include "device_common.h"
 #include "kernels.h"
 
@@ -13,167 +13,9 @@ inline dim3 grid1(uint64_t n, int per = kT) {
 }
 }  // namespace
 
-__global__ void k_iota(uint32_t* idx, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) idx[i] = (uint32_t)i;
-}
-void launch_iota(uint32_t* idx, uint64_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_iota, grid1(n), dim3(kT), 0, s, idx, n);
-}
-
-__global__ void k_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
-                        uint32_t* idx) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    out[i] = (uint32_t)(keys[i] >> 32);
-    idx[i] = (uint32_t)i;
-  }
-}
-void launch_top32(const uint64_t* keys, uint64_t n, uint32_t* out,
-                  uint32_t* idx, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_top32, grid1(n), dim3(kT), 0, s, keys, n, out, idx);
-}
-
-// last occurrence of each key in the (stable) sorted batch wins
-// (last writer in batch order); low word counts upserts, high word deletes.
-// bins (nullable): only the first bins[510] + bins[511] entries are ops (the
-// insert ordering's de-duplicated length, isort.hip); the rest get flag 0
-__global__ void k_mark_unique(const uint64_t* sk, const uint32_t* sidx,
-                              const uint64_t* vals, uint64_t n, const uint32_t* bins,
-                              uint64_t* flags, uint32_t* err) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t nv = bins ? (uint64_t)bins[2 * kCoarse - 2] + bins[2 * kCoarse - 1] : n;
-  if (i >= nv) {
-    flags[i] = 0;
-    return;
-  }
-  const uint64_t k = sk[i];
-  const bool last = i + 1 == nv || sk[i + 1] != k;
-  uint64_t f = 0;
-  if (k == kKeyMax) {
-    atomicOr(err, 1u << 31);  // EINVAL marker
-  } else if (last) {
-    f = vals[sidx[i]] != kValueNull ? 1ull : (1ull << 32);
-  }
-  flags[i] = f;
-}
-void launch_mark_unique(const uint64_t* sk, const uint32_t* sidx,
-                        const uint64_t* vals, uint64_t n, const uint32_t* bins,
-                        uint64_t* flags, uint32_t* err, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_mark_unique, grid1(n), dim3(kT), 0, s, sk, sidx, vals, n, bins, flags, err);
-}
-
-__global__ void k_compact_unique(const uint64_t* sk, const uint32_t* sidx,
-                                 const uint64_t* vals, const uint64_t* flags,
-                                 const uint64_t* pos, uint64_t n, uint64_t* uk,
-                                 uint64_t* uv, uint64_t* dk, uint64_t* counts) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t f = flags[i], p = pos[i];
-  if (f & 0xFFFFFFFFull) {
-    uk[p & 0xFFFFFFFFull] = sk[i];
-    uv[p & 0xFFFFFFFFull] = vals[sidx[i]];
-  } else if (f >> 32) {
-    dk[p >> 32] = sk[i];
-  }
-  if (i + 1 == n) {
-    const uint64_t t = p + f;
-    counts[0] = t & 0xFFFFFFFFull;
-    counts[1] = t >> 32;
-  }
-}
-void launch_compact_unique(const uint64_t* sk, const uint32_t* sidx,
-                           const uint64_t* vals, const uint64_t* flags,
-                           const uint64_t* pos, uint64_t n, uint64_t* uk,
-                           uint64_t* uv, uint64_t* dk, uint64_t* counts,
-                           hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_compact_unique, grid1(n), dim3(kT), 0, s, sk, sidx, vals, flags, pos, n, uk, uv, dk, counts);
-}
-
 // n_dev (nullable): the device-side op count, n its upper bound
 __device__ __forceinline__ uint64_t dev_n(const uint64_t* n_dev, uint64_t n) {
   return n_dev ? *n_dev : n;
-}
-
-__global__ void k_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev,
-                            uint32_t* heads) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t nv = dev_n(n_dev, n);
-  heads[i] = i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
-}
-void launch_seg_heads(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* heads,
-                      hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_seg_heads, grid1(n), dim3(kT), 0, s, page, n, n_dev, heads);
-}
-
-__global__ void k_seg_fill(const uint64_t* page, const uint32_t* heads,
-                           const uint32_t* pos, uint64_t n, const uint64_t* n_dev,
-                           uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
-                           SegLock lk) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t nv = dev_n(n_dev, n);
-  if (i < nv && heads[i]) {
-    const uint64_t pg = page[i];
-    seg_start[pos[i]] = (uint32_t)i;
-    seg_page[pos[i]] = pg;
-    if (lk.locks) {
-      // lock_and_read_page's lock half (Tree.cpp:205-242, 851): every
-      // segment of the batch takes its word with the batch's tag (segments
-      // sharing a word share the hold: their pages differ); a word held by
-      // another owner is waited for, bounded
-      unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
-                              cityhash64_u64(pg) % lk.num_locks;
-      uint32_t ok = 0;
-      for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-        const unsigned long long o = atomicCAS(w, 0ull, (unsigned long long)lk.tag);
-        if (o == 0ull || o == lk.tag) {
-          ok = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (!ok) atomicOr(lk.err, kErrLock);
-      lk.seg_lk[pos[i]] = ok;
-    }
-  }
-  if (i + 1 == nv) {
-    const uint32_t ns = pos[i] + heads[i];
-    *num_seg = ns;
-    seg_start[ns] = (uint32_t)nv;
-  } else if (nv == 0 && i == 0) {
-    *num_seg = 0;
-    seg_start[0] = 0;
-  }
-}
-void launch_seg_fill(const uint64_t* page, const uint32_t* heads,
-                     const uint32_t* pos, uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
-                     uint64_t* seg_page, uint32_t* num_seg, hipStream_t s) {
-  launch_seg_fill_lock(page, heads, pos, n, n_dev, seg_start, seg_page, num_seg, SegLock{},
-                       s);
-}
-void launch_seg_fill_lock(const uint64_t* page, const uint32_t* heads, const uint32_t* pos,
-                          uint64_t n, const uint64_t* n_dev, uint32_t* seg_start,
-                          uint64_t* seg_page, uint32_t* num_seg, const SegLock& lk,
-                          hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_seg_fill, grid1(n), dim3(kT), 0, s, page, heads, pos, n, n_dev, seg_start, seg_page, num_seg, lk);
-}
-
-// unlock_addr (Tree.cpp:244-264) for every segment holding its word, after
-// the page writes of the kernels before it (a kernel boundary orders them)
-__global__ void k_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev,
-                             uint64_t n_max, SegLock lk) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_max || i >= (uint64_t)*num_seg_dev || !lk.seg_lk[i]) return;
-  unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
-                          cityhash64_u64(seg_page[i]) % lk.num_locks;
-  __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-void launch_seg_unlock(const uint64_t* seg_page, const uint32_t* num_seg_dev, uint64_t n_max,
-                       const SegLock& lk, hipStream_t s) {
-  if (n_max) hipLaunchKernelGGL(k_seg_unlock, grid1(n_max), dim3(kT), 0, s, seg_page, num_seg_dev, n_max, lk);
 }
 
 // ---- two-launch tile scans ---------------------------------------------------
@@ -333,15 +175,6 @@ __global__ __launch_bounds__(kT) void k_tile_scan(const T* in, uint64_t n, const
       tot[1] = *err;
     }
   }
-}
-
-void launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* bsum,
-                     hipStream_t s) {
-  if (!n) return;
-  const dim3 g((unsigned)seg_tiles(n));
-  hipLaunchKernelGGL(k_tile_sum<uint32_t>, g, dim3(kT), 0, s, in, n, bsum);
-  hipLaunchKernelGGL(k_tile_scan<uint32_t>, g, dim3(kT), 0, s, in, n, (const uint32_t*)bsum, out,
-                     (const uint32_t*)nullptr, (uint64_t*)nullptr);
 }
 
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,

@@ -615,10 +615,10 @@ def test_searches_on_two_streams_with_an_insert_between(lib_ok):
 
 
 def test_insert_bin_overflow_reorders(lib_ok):
-    """Clustered keys put > 6144 ops into one ordering bin: k_bin_unique flags
-    the overflow, the upsert kernel is gated off, and the batch is re-ordered
-    by the rocPRIM path (tree.cpp kRedoOrder) with the same result; a bin of
-    <= 6144 clustered keys takes the LDS bitonic fallback inside the bin."""
+    """Clustered keys put > 6144 ops into one ordering bin: k_bin_unique sorts
+    that bin on the device with its global-scratch LSD radix path
+    (isort.hip big_bin_unique) with the same result; a bin of <= 6144
+    clustered keys takes the LDS bitonic fallback inside the bin."""
     t = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 14)
     orc = OracleTree(64 << 20)
     rng = np.random.default_rng(11)
@@ -671,4 +671,108 @@ def test_leaf_occupancy_bound_with_holes(lib_ok, from_image):
         gpu_insert(t, ks, vs)
         orc.apply_batch(ks, vs)
     compare_contents(t, orc)
+    t.close()
+
+
+def test_async_inserts_grow_from_empty_tree(lib_ok):
+    """shm_insert_batch_async: batches queued without any host wait, from an
+    empty tree (the root leaf splits, the root page is relocated and grows
+    several levels inside one batch, k_upper) through small batches, in-batch
+    duplicates and deletes; searches queued between the batches see exactly
+    the state after the batches before them; one synchronize at the end."""
+    rng = np.random.default_rng(4242)
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18)
+    orc = OracleTree(512 << 20)
+    universe = hashed_keys(1, 400001)
+    plan = [300000, 1, 37, 4096, 50000, 200000, 120000]
+    pend = []
+    keep = []
+    for i, b in enumerate(plan):
+        ks = universe[rng.integers(0, universe.size if i else 300000, b)]
+        vs = rng.integers(1, 1 << 62, b).astype(U64)
+        if i >= 3:
+            vs[rng.random(b) < 0.05] = 0
+        dk, dv = dev(ks), dev(vs)
+        t.insert_batch_async(dk, dv)
+        orc.apply_batch(ks, vs)
+        probe = universe[rng.integers(0, universe.size, 20000)]
+        pk = dev(probe)
+        pv = torch.empty_like(pk)
+        pf = torch.empty(pk.numel(), dtype=torch.uint8, device=pk.device)
+        t.search_batch(pk, pv, pf)
+        pend.append((probe, pv, pf) + orc.search_batch(probe))
+        keep += [dk, dv, pk]
+    t.synchronize()
+    for probe, pv, pf, ov, of in pend:
+        assert_same(probe, ov, of, host(pv), pf.cpu().numpy())
+    st = compare_contents(t, orc)
+    assert t.stats()["height"] >= 3, st
+    t.close()
+    orc.close()
+
+
+def test_async_batch_with_kkeymax_is_rejected_and_reported(lib_ok):
+    """A queued batch holding kKeyMax is dropped whole on the device and the
+    error surfaces at the next synchronising call; batches after it apply."""
+    t = shm.Tree(arena_bytes=32 << 20, max_batch=4096)
+    bad_k = dev(np.array([5, (1 << 64) - 1, 6], dtype=U64))
+    bad_v = dev(np.array([1, 2, 3], dtype=U64))
+    ok_k, ok_v = dev(np.array([7], dtype=U64)), dev(np.array([70], dtype=U64))
+    t.insert_batch_async(bad_k, bad_v)
+    t.insert_batch_async(ok_k, ok_v)
+    with pytest.raises(shm.ShermanError) as ei:
+        t.synchronize()
+    assert ei.value.rc == shm.SHM_EINVAL
+    assert t.search(5) == (False, 0) and t.search(6) == (False, 0)
+    assert t.search(7) == (True, 70)
+    t.synchronize()  # reported once
+    t.check()
+    t.close()
+
+
+def test_arena_exhaustion_reports_enomem_and_stays_consistent(lib_ok):
+    """Splits that do not fit the arena are left unapplied and reported as
+    SHM_ENOMEM; the tree stays a valid B-link tree and every key it holds
+    has the value last written for it."""
+    t = shm.Tree(arena_bytes=1 << 20, max_batch=1 << 16)  # 1024 pages
+    ks = hashed_keys(1, 60001)
+    vs = np.arange(1, ks.size + 1, dtype=U64) * U64(3)
+    with pytest.raises(shm.ShermanError) as ei:
+        for c in range(0, ks.size, 1 << 14):
+            gpu_insert(t, ks[c:c + (1 << 14)], vs[c:c + (1 << 14)])
+    assert ei.value.rc == shm.SHM_ENOMEM
+    st = t.check()
+    img, root = t.dump_image()
+    orc = OracleTree(image=img, root_ptr=root)
+    k, v = orc.dump()
+    want = dict(zip(ks.tolist(), vs.tolist()))
+    assert k.size == st["keys"] and k.size > 0
+    assert all(want[a] == b for a, b in zip(k.tolist(), v.tolist()))
+    orc.close()
+    t.close()
+
+
+def test_pending_range_waits_for_its_issue_stream(lib_ok):
+    """range_query_batch_async issued on a side stream (stream=None there
+    means that stream) and .result() called outside it: the result waits for
+    the stream the scans were queued on, not the one current at .result()."""
+    t = shm.Tree(arena_bytes=128 << 20, max_batch=1 << 14)
+    ks = hashed_keys(1, 30001)
+    gpu_insert(t, ks, ks + U64(7))
+    rng = np.random.default_rng(12)
+    lo = rng.integers(0, 1 << 63, 400, dtype=np.uint64) * U64(2)
+    hi = lo + (U64(1) << U64(54))
+    hi[hi < lo] = U64((1 << 64) - 2)
+    sc, sv = t.range_query_batch(dev(lo), dev(hi))
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        dlo, dhi = dev(lo), dev(hi)
+        pend = t.range_query_batch_async(dlo, dhi)
+        # keep the side stream busy behind the scans
+        junk = torch.randn(1 << 22, device="cuda")
+        for _ in range(20):
+            junk = junk * 1.0001
+    ac, av = pend.result()
+    assert np.array_equal(ac.cpu().numpy(), sc.cpu().numpy())
+    assert np.array_equal(host(av), host(sv))
     t.close()
