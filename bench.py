@@ -28,13 +28,14 @@ Default workload, C2 (BASELINE.json configs[1]) — the headline line:
     inserts apply.  N > 1: scans are cut at shard boundaries and routed, and
     inserts routed to their owners, with RCCL all-to-all.
 
-N > 1 (python -m torch.distributed.run ... bench.py --gpus N, C2 / C5):
+N > 1 (python -m torch.distributed.run ... bench.py --gpus N, C4 / C5):
   * The key space is range-partitioned, one shard per GPU: shard s owns
     [s*2^64/N, (s+1)*2^64/N).
-  * Each rank holds 2^26 keys of a 2^26*N global key set.
+  * C4 (BASELINE.json configs[3]): 2^30 keys in all, 2^30 / N per rank
+    (--keys-log2 overrides the per-rank size).
   * Each rank issues 1 Mi uniform queries over the whole set per step.
   * Queries and replies are routed with RCCL all-to-all (sherman_amd.shard),
-    i.e. weak scaling.
+    i.e. weak scaling in queries per GPU.
 
 Prints ONE JSON line on rank 0 (DESIGN.md §Measurement explains every field).
 """
@@ -60,7 +61,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2")
-    p.add_argument("--keys-log2", type=int, default=26, help="keys per GPU = 2^k")
+    p.add_argument("--keys-log2", type=int, default=None,
+                   help="keys per GPU = 2^k (default: 26 at N = 1 (C2), 30 - log2(N) at "
+                        "N > 1 (C4: 2^30 keys in all))")
     p.add_argument("--batch-log2", type=int, default=20, help="ops per step per GPU")
     p.add_argument("--theta", type=float, default=0.99, help="c3 zipf skew")
     p.add_argument("--read-ratio", type=int, default=50, help="c3 get percentage")
@@ -76,6 +79,8 @@ def parse():
                    help="c5, N=1: range scans read their total back before the "
                         "batch's inserts are queued (default: async, checked after)")
     p.add_argument("--profile-steps", type=int, default=10)
+    p.add_argument("--latency-steps", type=int, default=None,
+                   help="steps of the per-batch latency pass (default: --steps)")
     p.add_argument("--streams", type=int, default=2, choices=(1, 2),
                    help="c2, N=1: consecutive batches alternate over this many HIP "
                         "streams, so one batch's ordering overlaps the previous walk")
@@ -160,6 +165,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    if args.keys_log2 is None:
+        # C2 at N = 1; C4 (2^30 keys over N GPUs) and C5 at N > 1
+        args.keys_log2 = 26 if world == 1 else 30 - (world.bit_length() - 1)
     n_keys = 1 << args.keys_log2
     batch = 1 << args.batch_log2
     dev = torch.device(f"cuda:{local}")
@@ -276,10 +284,10 @@ def main():
                 scan_out["r"] = pr = tree.range_query_batch_async(lo, hi)
                 if pr.tot is not None:  # only the (total, error) words stay alive
                     scan_out.setdefault("all", []).append((pr.tot, pr.vals.numel()))
-                tree.insert_batch(pk, pv)
+                tree.insert_batch_async(pk, pv)
             elif route is None:
                 scan_out["r"] = PendingRange(None, *tree.range_query_batch(lo, hi))
-                tree.insert_batch(pk, pv)
+                tree.insert_batch_async(pk, pv)
             else:
                 scan_out["r"] = PendingRange(None, *route.range_query(lo, hi))
                 route.insert(pk, pv)
@@ -297,9 +305,11 @@ def main():
         del keys_local
 
         def step(i):
+            # the batch's gets, then its inserts, queued without a host wait
+            # (the status of every insert is checked after the timed steps)
             gk, pk, pv = mixed[i % N_BATCHES]
             tree.search_batch(gk, vals[:gk.numel()], found[:gk.numel()])
-            tree.insert_batch(pk, pv)
+            tree.insert_batch_async(pk, pv)
 
     # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
     cpu = parity = None
@@ -322,10 +332,19 @@ def main():
     host_issue = time.perf_counter() - t_start  # host time to issue the steps
     barrier()
     elapsed = time.perf_counter() - t_start
+    tree.synchronize()  # raises any error of the queued batches
+    rank_mops = batch * args.steps / elapsed / 1e6
+    cluster_sum = rank_mops
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # per-rank rates summed over the cluster, as the reference's per-window
+        # cluster sum (test/benchmark.cpp:320-337 via DSMKeeper::sum,
+        # src/DSMKeeper.cpp:163-176)
+        cs = torch.tensor([rank_mops], dtype=torch.float64, device=dev)
+        dist.all_reduce(cs, op=dist.ReduceOp.SUM)
+        cluster_sum = float(cs.item())
     st_end = tree.stats()
     total_ops = batch * args.steps * world
     mops = total_ops / elapsed / 1e6
@@ -343,6 +362,25 @@ def main():
     else:
         n_get = mixed[(args.steps - 1) % N_BATCHES][0].numel()
         hit_rate = float(found[:n_get].float().mean().item())
+
+    # ---- per-batch latency (untimed pass): HIP events around each step on
+    # its stream, in the order the reference reports them
+    # (test/benchmark.cpp:207-249: p50 / p90 / p95 / p99 / p99.9) ------------
+    if args.workload == "c2" and world > 1:
+        lat_route = ShardRouter(tree, world, dist)  # the pipeline keeps a batch begun
+
+        def one(i):  # one routed batch, not pipelined with the next
+            lat_route.search(qs[i % N_BATCHES], outs[0][0], outs[0][1])
+    elif args.workload == "c2":
+        def one(i):
+            tree.search_batch(qs[i % N_BATCHES], vals, found)
+    else:
+        one = step
+    lat = latency_pass(one, args, dist)
+    if dist is not None:
+        lt = torch.tensor(lat, dtype=torch.float64, device=dev)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        lat = lt.tolist()
 
     # ---- roofline: k_walk timed with HIP events on its launch stream -------
     tree.profile(True)
@@ -447,6 +485,9 @@ def main():
             },
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
+            "batch_latency_us": dict(zip(("p50", "p90", "p95", "p99", "p99.9", "max"),
+                                         [round(x, 1) for x in lat])),
+            "cluster_sum_mops": round(cluster_sum, 2),
         }
         if args.workload == "c5":
             # the insert pipeline dominates: ops x 1074 B over its measured
@@ -475,6 +516,30 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     tree.close()
+
+
+def latency_pass(one, args, dist):
+    """Latency of single batches: each of the pass's batches is issued alone
+    (barrier and device idle before, synchronize after) and timed on the
+    host clock, issue included; returns [p50, p90, p95, p99, p99.9, max] in
+    us (max over ranks at N > 1), the percentiles the reference prints
+    (test/benchmark.cpp:207-249, there per op)."""
+    import numpy as np
+    import torch
+    n = args.latency_steps if args.latency_steps is not None else args.steps
+    if n <= 0:
+        return [0.0] * 6
+    us = []
+    for i in range(n):
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        one(i)
+        torch.cuda.synchronize()
+        us.append((time.perf_counter() - t0) * 1e6)
+    us = np.array(us)
+    return [float(np.percentile(us, q)) for q in (50, 90, 95, 99, 99.9)] + [float(us.max())]
 
 
 def _oracle_on_gpu_image(tree, spare_bytes=0):

@@ -27,6 +27,7 @@
 //                  --- barrier ---  I2 prefix: dense segment list + page bases
 //                  --- barrier ---  I3 build / rewrite as for leaves
 //                  --- barrier ---  next level while separators remain
+//   deletes            every wave: Tree::del of the chunk's deletes
 // Pages come from a device bump cursor (the superblock's next_page; the
 // reference's LocalAllocator bump, include/LocalAllocator.h:21-43), checked
 // against the arena capacity before each level.  The root page never moves:
@@ -390,6 +391,108 @@ __device__ __forceinline__ bool fan_in(uint32_t* cnt, uint32_t want) {
   return rl32(ok, 0) != 0;
 }
 
+// Tree::del of one key (leaf_page_del, Tree.cpp:993-1057), one wave: walk
+// from the leaf directory (or the root) with page_search's sibling rule, lock
+// the leaf's word, re-read it under the lock (turning right again if needed),
+// clear the first valid slot holding the key (value = kValueNull, f++ ,
+// r = f) and write back that 18 B entry, then release.  Keys are unique in a
+// batch, so two waves never touch one entry; they may share a page and
+// serialise on its word.
+__device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_t& err) {
+  const int lane = lane_id();
+  uint64_t ptr = a.root;
+  if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+  bool locked = false;
+  uint64_t lw = 0;
+  int retries = 0;
+  for (int hop = 0;; ++hop) {
+    if (hop > kMaxRounds) {
+      err |= kErrRounds;
+      break;
+    }
+    if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
+      err |= kErrBadPtr;
+      break;
+    }
+    const u32x4 w0 = load_page_slice(a.arena, ga_offset(ptr));
+    const Hdr h0 = parse_hdr(w0);
+    const bool leaf0 = h0.leftmost == 0;
+    if (h0.fver != (leaf0 ? h0.rver_leaf : h0.rver_internal)) {
+      if (++retries > kMaxRetries) {
+        err |= kErrInconsistent;
+        break;
+      }
+      continue;
+    }
+    if (k >= h0.highest && h0.sibling != 0) {
+      ptr = h0.sibling;
+      continue;
+    }
+    if (k < h0.lowest || k >= h0.highest) {
+      err |= kErrFence;
+      break;
+    }
+    if (!leaf0) {
+      const IntRec r = internal_record(w0);
+      const int cnt = h0.last_index + 1;
+      const int pos = popc64(ballot(lane >= 3 && lane - 3 < cnt && r.key <= k));
+      ptr = pos == 0 ? h0.leftmost : rl64(r.ptr, pos + 2);
+      continue;
+    }
+    // the leaf: lock_and_read_page (Tree.cpp:1014-1015)
+    lw = (uint64_t)lock_index(ptr, a.num_locks);
+    uint32_t got = 0;
+    if (lane == 0) {
+      unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.locks) + lw;
+      for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+        if (atomicCAS(wd, 0ull, (unsigned long long)a.tag) == 0ull) {
+          got = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (rl32(got, 0) == 0) {
+      err |= kErrLock;
+      break;
+    }
+    locked = true;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const u32x4 w = load_page_slice(a.arena, ga_offset(ptr));
+    const Hdr h = parse_hdr(w);
+    if (h.fver != h.rver_leaf) {
+      err |= kErrInconsistent;
+      break;
+    }
+    if (k >= h.highest && h.sibling != 0) {  // Tree.cpp:1028-1032
+      if (lane == 0)
+        __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      locked = false;
+      ptr = h.sibling;
+      continue;
+    }
+    stage_page(lp, w);
+    wave_lds_sync();
+    LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
+    const uint64_t m = ballot(lane < kLeafCardinality && e.key == k && e.val != kValueNull);
+    if (m && lane == ctz64(m)) {
+      const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
+      put_leaf_entry(reinterpret_cast<uint32_t*>(a.arena + ga_offset(ptr)), lane, k, kValueNull,
+                     (e.fraw & 0xF0) | f, (e.rraw & 0xF0) | f);
+    }
+    wave_lds_sync();
+    break;
+  }
+  if (locked) {
+    // write_page_and_unlock (Tree.cpp:1049-1052): the entry store first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -426,10 +529,10 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   const uint32_t pre_np = block_sum((uint32_t)t < b ? v_np : 0u, s_red);
   const uint32_t pre_ns = block_sum((uint32_t)t < b ? v_ns : 0u, s_red);
   // in-place segments were written by the upsert kernel: release their words
-  // (write_page_and_unlock's unlock half, Tree.cpp:266-298)
+  // (write_page_and_unlock's unlock half, Tree.cpp:266-298); split ones stay
+  // held until their page 0 is rewritten below
   for (uint64_t g = tid; g < ns; g += T)
     if (a.seg_lk[g] && a.seg_P[g] <= 1) release_word(a.locks, a.num_locks, a.seg_page[g]);
-
   bool ok = true;
   uint32_t nsep = 0;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
@@ -705,6 +808,10 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     ok = grid_sync(ctl, nb, &s_flag);
   }
   if (!ok) err |= kErrRounds;
+  // the chunk's deletes, after every split (Tree::del, Tree.cpp:542-591):
+  // the keys are located afresh, so pages that moved right are followed
+  const uint64_t n_del = *a.n_del;
+  for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
   if (b == 0 && t == 0) {
     // superblock (device-authoritative) and its host mirror
@@ -720,118 +827,6 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// Tree::del for every key of dk[0, *n_del) (leaf_page_del, Tree.cpp:993-1057):
-// one wave per key, grid-stride.  Walk from the leaf directory (or the root)
-// with page_search's sibling rule, lock the leaf's word, re-read it under the
-// lock (turning right again if needed), clear the first valid slot holding
-// the key (value = kValueNull, f++ , r = f) and write back that 18 B entry,
-// then release.  Keys are unique in the batch, so two waves never touch one
-// entry; they may share a page and serialise on its word.
-__global__ __launch_bounds__(kBlock) void k_delete(DelArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock][kPageDwords + 8];
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const uint64_t n = *a.n_del;
-  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint32_t* lp = s_pg[wv];
-  uint32_t err = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + wv; i < n; i += W) {
-    const uint64_t k = a.keys[i];
-    uint64_t ptr = a.root;
-    if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
-    bool locked = false;
-    uint64_t lw = 0;
-    int retries = 0;
-    for (int hop = 0;; ++hop) {
-      if (hop > kMaxRounds) {
-        err |= kErrRounds;
-        break;
-      }
-      if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
-        err |= kErrBadPtr;
-        break;
-      }
-      const u32x4 w0 = load_page_slice(a.arena, ga_offset(ptr));
-      const Hdr h0 = parse_hdr(w0);
-      const bool leaf0 = h0.leftmost == 0;
-      if (h0.fver != (leaf0 ? h0.rver_leaf : h0.rver_internal)) {
-        if (++retries > kMaxRetries) {
-          err |= kErrInconsistent;
-          break;
-        }
-        continue;
-      }
-      if (k >= h0.highest && h0.sibling != 0) {
-        ptr = h0.sibling;
-        continue;
-      }
-      if (k < h0.lowest || k >= h0.highest) {
-        err |= kErrFence;
-        break;
-      }
-      if (!leaf0) {
-        const IntRec r = internal_record(w0);
-        const int cnt = h0.last_index + 1;
-        const int pos = popc64(ballot(lane >= 3 && lane - 3 < cnt && r.key <= k));
-        ptr = pos == 0 ? h0.leftmost : rl64(r.ptr, pos + 2);
-        continue;
-      }
-      // the leaf: lock_and_read_page (Tree.cpp:1014-1015)
-      lw = (uint64_t)lock_index(ptr, a.num_locks);
-      uint32_t got = 0;
-      if (lane == 0) {
-        unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.locks) + lw;
-        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-          if (atomicCAS(wd, 0ull, (unsigned long long)a.tag) == 0ull) {
-            got = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      if (rl32(got, 0) == 0) {
-        err |= kErrLock;
-        break;
-      }
-      locked = true;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const u32x4 w = load_page_slice(a.arena, ga_offset(ptr));
-      const Hdr h = parse_hdr(w);
-      if (h.fver != h.rver_leaf) {
-        err |= kErrInconsistent;
-        break;
-      }
-      if (k >= h.highest && h.sibling != 0) {  // Tree.cpp:1028-1032
-        if (lane == 0)
-          __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        locked = false;
-        ptr = h.sibling;
-        continue;
-      }
-      stage_page(lp, w);
-      wave_lds_sync();
-      LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
-      const uint64_t m = ballot(lane < kLeafCardinality && e.key == k && e.val != kValueNull);
-      if (m && lane == ctz64(m)) {
-        const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
-        put_leaf_entry(reinterpret_cast<uint32_t*>(a.arena + ga_offset(ptr)), lane, k,
-                       kValueNull, (e.fraw & 0xF0) | f, (e.rraw & 0xF0) | f);
-      }
-      break;
-    }
-    if (locked) {
-      // write_page_and_unlock (Tree.cpp:1049-1052): the entry store first
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  if (err && lane == 0) atomicOr(a.err, err);
 }
 
 // LeafPage() + set_consistent (Tree.cpp:47-52)
@@ -863,10 +858,6 @@ void launch_upper(const UpperArgs& a, hipStream_t s) {
   // one block per CU: every block resident (grid barriers); 512 threads,
   // ~20 KB of LDS
   hipLaunchKernelGGL(k_upper, dim3(upper_blocks()), dim3(kUpT), 0, s, a);
-}
-
-void launch_delete(const DelArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_delete, dim3(2 * upper_blocks()), dim3(kBlock), 0, s, a);
 }
 
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s) {

@@ -83,7 +83,9 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
                                                    uint64_t* __restrict__ keys_out,
                                                    uint32_t* __restrict__ idx_out,
                                                    uint32_t* __restrict__ gcount,
-                                                   uint32_t* err, uint32_t* gate, uint32_t tag) {
+                                                   uint32_t* err, uint32_t* gate, uint32_t tag,
+                                                   KeyRange kr, uint32_t* __restrict__ M,
+                                                   uint32_t* __restrict__ S) {
   // LDS hash table of the tile's distinct keys: slot -> (key, 1 + last index)
   constexpr int kSlots = 2 * kIsortTile;
   constexpr int PER = kIsortTile / kIT;
@@ -91,7 +93,9 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
   __shared__ unsigned long long hkey[kSlots];
   __shared__ uint32_t hidx[kSlots];
   __shared__ uint32_t wsum[kIT / kWave];
+  __shared__ uint32_t hist[kCoarse];  // the coarse pass's tile histogram (M != nullptr)
   const int t = threadIdx.x;
+  if (t < kCoarse) hist[t] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kIsortTile;
 #pragma unroll
   for (int r = 0; r < SPT; ++r) {
@@ -138,9 +142,20 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
       keys_out[base + pos] = k;
       idx_out[base + pos] = hidx[SPT * t + r] - 1u;
       ++pos;
+      if (M) atomicAdd(&hist[coarse_of(k, kr)], 1u);
     }
   }
   if (t == 0) gcount[blockIdx.x] = total;
+  if (M) {
+    // this tile is one coarse-pass tile (batches of <= 256 tiles): its
+    // histogram and group sums, as k_part_coarse_hist would write them
+    __syncthreads();
+    if (t < kCoarse) {
+      const uint32_t c = hist[t];
+      M[(uint64_t)blockIdx.x * kCoarse + t] = c;
+      if (c) atomicAdd(&S[(blockIdx.x / 16) * kCoarse + t], c);
+    }
+  }
 }
 
 // ---- step 3 + 4 without the library scan: per-bin dedup, sort, emit --------
@@ -485,10 +500,13 @@ __global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ k
 
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
+                       uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
                        hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)((n + kIsortTile - 1) / kIsortTile)),
-                     dim3(kIT), 0, s, keys, n, keys_out, idx_out, gcount, err, gate, tag);
+  const uint64_t tiles = (n + kIsortTile - 1) / kIsortTile;
+  if (tiles > (uint64_t)kMaxTiles) M = S = nullptr;  // the coarse pass counts for itself
+  hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)tiles), dim3(kIT), 0, s, keys, n, keys_out,
+                     idx_out, gcount, err, gate, tag, KeyRange{key_lo, key_bits}, M, S);
 }
 
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,

@@ -85,6 +85,7 @@ struct SegArgs {
   uint32_t* seg_newpages;     // P - 1
   uint32_t* seg_ver;          // front_version observed
   // per segment: 1 = its page's lock word was taken ahead by k_seg_fill_scan
+  // (k_upper releases them)
   const uint32_t* seg_lk;
   uint32_t* err;
   // per-page occupancy bound kept by every leaf writer (see WalkArgs)
@@ -139,28 +140,16 @@ struct UpperArgs {
   uint32_t* d_base;
   uint32_t* int_rd;          // zero between chunks
   uint64_t* pub;             // mapped host mirror {batch, next_page, root_level, splits} (nullable)
-};
-uint32_t upper_blocks();
-void launch_upper(const UpperArgs& a, hipStream_t s);
-
-// Tree::del for every key of keys[0, *n_del) (insert.hip)
-struct DelArgs {
-  uint8_t* arena;
-  uint64_t arena_bytes;
-  uint16_t node;
-  uint64_t root;
-  const uint64_t* keys;
+  // the chunk's deletes (Tree::del), applied after the splits
+  const uint64_t* dk;
   const uint64_t* n_del;
-  const uint64_t* dir;   // leaf directory (nullable)
+  const uint64_t* dir;       // leaf directory (nullable), as in WalkArgs
   uint64_t dir_lo;
   uint64_t dir_n;
   uint32_t dir_shift;
-  uint64_t* locks;
-  uint32_t num_locks;
-  uint64_t tag;
-  uint32_t* err;
 };
-void launch_delete(const DelArgs& a, hipStream_t s);
+uint32_t upper_blocks();
+void launch_upper(const UpperArgs& a, hipStream_t s);
 
 void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s);
@@ -196,8 +185,11 @@ void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* g
 // sticky error word gets kErrKeyMax.
 constexpr int kIsortTile = 4096;
 constexpr uint32_t kErrKeyMax = 1u << 31;
+// For batches of <= kMaxTiles tiles it also writes the coarse pass's tile
+// histograms M and group sums S (launch_partition_coarse then skips its own).
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
+                       uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
                        hipStream_t s);
 // steps 3-4: per-bin last-writer dedup + sort (bins of <= 6144 ops in LDS,
 // larger ones by an LSD radix sort through global scratch kscr / iscr, n

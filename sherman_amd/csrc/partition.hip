@@ -336,8 +336,10 @@ void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* g
   const uint64_t all_groups = (n + kGrpKeys - 1) / kGrpKeys;
   const uint32_t groups = (uint32_t)((all_groups + kMaxTiles - 1) / kMaxTiles);
   const uint32_t tiles = (uint32_t)((all_groups + groups - 1) / groups);
-  hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, gcount,
-                     groups, M, S);
+  // one group per tile: k_tile_dedup already wrote the histograms
+  if (groups > 1)
+    hipLaunchKernelGGL(k_part_coarse_hist, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, gcount,
+                       groups, M, S);
   hipLaunchKernelGGL(k_part_coarse_scatter, dim3(tiles), dim3(kPT), 0, s, keys, n, kr, gcount,
                      pay_in, groups, tiles, (const uint32_t*)M, (const uint32_t*)S, keys1, pay1,
                      (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, bins);

@@ -451,8 +451,8 @@ int drain_profile(shm_tree* t) {
 //   2. k_locate: each upsert's leaf from the leaf directory (header walk);
 //   3. segmentation + lock words taken ahead (k_seg_count, k_seg_fill_scan);
 //   4. k_leaf_upsert_pipe: in-place upserts, splits flagged and counted;
-//   5. k_upper: leaf splits, parent levels, root growth, unlocks, superblock;
-//   6. k_delete: Tree::del of the chunk's deletes.
+//   5. k_upper: leaf splits, parent levels, root growth, unlocks, the
+//      chunk's deletes, superblock.
 int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
                  uint64_t n) {
   const uint32_t tag = ++t->chunks;
@@ -462,7 +462,8 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
     const int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
     if (rc) return rc;
   }
-  dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag, s);
+  dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
+                         t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S, s);
   dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
                                t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
   dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
@@ -552,22 +553,11 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   u.d_base = t->d_base;
   u.int_rd = t->int_rd;
   u.pub = reinterpret_cast<uint64_t*>(t->h_pin_dev) + kPubWord / 2;
+  u.dk = t->dk;
+  u.n_del = t->d_counts + 1;
+  set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   dev::launch_upper(u, s);
   DBG(s, "upper");
-  dev::DelArgs d{};
-  d.arena = t->arena;
-  d.arena_bytes = t->arena_bytes;
-  d.node = t->cfg.node_id;
-  d.root = t->root;
-  d.keys = t->dk;
-  d.n_del = t->d_counts + 1;
-  set_dir(t, &d.dir, &d.dir_lo, &d.dir_shift, &d.dir_n);
-  d.locks = t->locks;
-  d.num_locks = t->cfg.num_locks;
-  d.tag = lock_tag;
-  d.err = t->d_err;
-  dev::launch_delete(d, s);
-  DBG(s, "delete");
   HIP_OK(hipGetLastError());
   t->err_pending = true;
   if (t->prof_on) {

@@ -184,8 +184,8 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     if (live && !over && li == 0) a.leaf_hw[ga_offset(qpage) >> 10] = (uint8_t)hw;
   }
   const uint64_t gq = g0 + (uint64_t)q;
+  const uint32_t P = (live && over) ? (T + kLeafSplitFill - 1) / kLeafSplitFill : 1u;
   if (li == 0 && q < G && gq < num_seg) {
-    const uint32_t P = (live && over) ? (T + kLeafSplitFill - 1) / kLeafSplitFill : 1u;
     a.seg_T[gq] = live ? T : 0u;
     a.seg_P[gq] = P;
     a.seg_newpages[gq] = P - 1;

@@ -160,7 +160,9 @@ class ShardRouter:
         rv = self._buf("rvi", nrecv, torch.int64, dev)
         self._a2a(rk, kb, rcnt, cnt)
         self._a2a(rv, vb, rcnt, cnt)
-        self.local.insert_batch(rk, rv)
+        # queued without a host wait where the shard supports it (the
+        # status surfaces at the shard's next synchronising call)
+        getattr(self.local, "insert_batch_async", self.local.insert_batch)(rk, rv)
 
     def range_query(self, lo, hi):
         """Batched range scans [lo_i, hi_i] (inclusive, u64 held as int64).
