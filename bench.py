@@ -90,6 +90,10 @@ def parse():
     p.add_argument("--sim-rank", type=int, default=0)
     p.add_argument("--no-range-hint", action="store_true",
                    help="do not pass the shard key range to the tree (A/B)")
+    p.add_argument("--router", choices=("auto", "cabi", "python"), default="auto",
+                   help="N > 1: route gets / inserts through the C-ABI shard (C++ over "
+                        "RCCL, shm_shard_*) or the Python exchange; auto = the C-ABI on "
+                        "the nccl backend once it matched the Python route on one batch")
     return p.parse_args()
 
 
@@ -185,6 +189,9 @@ def main():
     n_keys = inserted if sim else n_keys
     build_s = time.time() - t0
     st = tree.stats()
+    cshard, router_kind = None, None
+    if world > 1:
+        cshard, router_kind = make_cshard(tree, world, rank, dist, dev, args, keys_local)
     log(f"[rank {rank}] built {inserted} keys in {build_s:.1f}s "
         f"({inserted / build_s / 1e6:.2f} M inserts/s), height {st['height']}, "
         f"pages {st['pages_used']}")
@@ -217,7 +224,7 @@ def main():
         routes = [None] * nstr
         if world > 1:
             groups = [None] + [dist.new_group(list(range(world))) for _ in range(nstr - 1)]
-            routes = [ShardRouter(tree, world, dist, group=gr) for gr in groups]
+            routes = [ShardRouter(tree, world, dist, group=gr, cshard=cshard) for gr in groups]
         for sx in streams:
             if sx is not None:
                 sx.wait_stream(torch.cuda.current_stream())
@@ -273,7 +280,7 @@ def main():
             mixed.append((lo, umin(hi, torch.full_like(lo, -2)), k[~is_scan].contiguous(),
                           (op_idx[~is_scan] + 1).contiguous()))
         del keys_local
-        route = ShardRouter(tree, world, dist) if world > 1 else None
+        route = ShardRouter(tree, world, dist, cshard=cshard) if world > 1 else None
         scan_out = {}
 
         def step(i):
@@ -367,7 +374,9 @@ def main():
     # its stream, in the order the reference reports them
     # (test/benchmark.cpp:207-249: p50 / p90 / p95 / p99 / p99.9) ------------
     if args.workload == "c2" and world > 1:
-        lat_route = ShardRouter(tree, world, dist)  # the pipeline keeps a batch begun
+        # the pipeline keeps a batch begun: a separate Python router, or the C
+        # shard (two slots: one holds the begun batch)
+        lat_route = ShardRouter(tree, world, dist, cshard=cshard)
 
         def one(i):  # one routed batch, not pipelined with the next
             lat_route.search(qs[i % N_BATCHES], outs[0][0], outs[0][1])
@@ -457,6 +466,7 @@ def main():
                 "get_order": args.sort,
                 "streams": (len(outs) if args.workload == "c2" else 1),
                 "rccl_groups": (len(outs) if args.workload == "c2" and world > 1 else None),
+                "router": router_kind,
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
                 "splits_in_timed_steps": st_end["splits"] - splits0,
@@ -516,6 +526,37 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     tree.close()
+
+
+def make_cshard(tree, world, rank, dist, dev, args, keys_local):
+    """The C-ABI shard (sherman_amd.CShard: routed get / insert in C++ over
+    its own RCCL communicators) when the backend is nccl and --router allows;
+    with "auto" it must first return the Python route's results on one batch
+    of stored keys (every rank agrees, else all fall back)."""
+    import torch
+    import sherman_amd as shm
+    from sherman_amd.shard import ShardRouter
+    if args.router == "python" or dist.get_backend() != "nccl":
+        return None, "python"
+    cs = shm.CShard(tree, world, rank, dist)
+    if args.router == "cabi":
+        return cs, "cabi"
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0FFEE + rank)
+    q = keys_local[torch.randint(0, keys_local.numel(), (1 << 16,), device=dev, generator=g)]
+    q = torch.cat([q, q + 1])  # hits and (mostly) misses
+    va, fa = torch.empty_like(q), torch.empty(q.numel(), dtype=torch.uint8, device=dev)
+    vb, fb = torch.empty_like(q), torch.empty(q.numel(), dtype=torch.uint8, device=dev)
+    ShardRouter(tree, world, dist).search(q, va, fa)
+    cs.search(q, vb, fb)
+    torch.cuda.synchronize()
+    ok = torch.tensor([int(torch.equal(va, vb) and torch.equal(fa, fb))], device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        return cs, "cabi"
+    log("[bench] C-ABI shard route disagreed with the Python route: using Python")
+    cs.close()
+    return None, "python (C-ABI self-check failed)"
 
 
 def latency_pass(one, args, dist):

@@ -26,6 +26,10 @@
  *                       the MN arena + root pointer (src/DSM.cpp:37-53, src/Tree.cpp:90-114)
  *   shm_route_*         (no reference counterpart: the multi-GPU key routing
  *                        that replaces DSM chunk round-robin, include/DSM.h:198-224)
+ *   shm_shard_*         a Tree spread over memory nodes: DSM::alloc's chunk
+ *                       round-robin over nodes (include/DSM.h:198-224) and the
+ *                       remote page reads of Tree::search / Tree::insert
+ *                       (src/Tree.cpp:353-459), here range shards over RCCL
  */
 #ifndef SHERMAN_AMD_H
 #define SHERMAN_AMD_H
@@ -94,6 +98,8 @@ typedef struct shm_stats_t {
 int shm_config_init(shm_config *cfg);
 int shm_tree_create(const shm_config *cfg, shm_tree **out);
 int shm_tree_destroy(shm_tree *t);
+/* cfg.max_batch of the handle (the largest chunk one batch call processes) */
+uint64_t shm_tree_max_batch(const shm_tree *t);
 const char *shm_strerror(int status);
 int shm_abi_version(void);
 
@@ -218,6 +224,37 @@ int shm_route_unpermute(shm_tree *t, const uint64_t *in, const uint32_t *perm,
  * (Tree::search's bool, Tree.cpp:445-448) in the same pass */
 int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *perm,
                               uint64_t n, uint64_t *out, uint8_t *found_out, void *stream);
+
+/* multi-GPU range shards over RCCL ------------------------------------------
+ * Rank r of P (P <= 16) owns keys [r * 2^64 / P, (r+1) * 2^64 / P) in its own
+ * shm_tree (create it with key_lo / key_bits of that slice).  One process per
+ * GPU; every rank makes the same calls in the same order (collectives).
+ * A routed get: bucket by owner, exchange counts (ncclAllToAll), one host
+ * read-back of the split sizes, keys out and values back (grouped
+ * ncclSend / ncclRecv), local shm_search_batch, un-permute.  A routed insert:
+ * the same exchange with the values, then shm_insert_batch_async on the
+ * owner (rank-major batch order across ranks).  Device pointers; n <=
+ * the local tree's max_batch. */
+typedef struct shm_shard shm_shard;
+/* rank 0 makes the id (NCCL_UNIQUE_ID_BYTES = 128), the caller broadcasts it */
+int shm_nccl_unique_id(void *id_out, uint64_t bytes);
+int shm_shard_create(shm_tree *local, const void *nccl_id, uint64_t id_bytes, uint32_t world,
+                     uint32_t rank, shm_shard **out);
+/* the same over a caller's communicator (an ncclComm_t as void*; not freed) */
+int shm_shard_create_with_comm(shm_tree *local, void *nccl_comm, uint32_t world, uint32_t rank,
+                               shm_shard **out);
+int shm_shard_destroy(shm_shard *s);
+/* vals_out / found_out in input order (Tree::search per key) */
+int shm_shard_search(shm_shard *s, const uint64_t *keys, uint64_t n, uint64_t *vals_out,
+                     uint8_t *found_out, void *stream);
+/* the same in two halves for pipelining: begin = bucketing + count exchange
+ * (no host wait), end = the rest.  Two batches may be begun at once (two
+ * slots, each with its own communicator); end them in order. */
+int shm_shard_search_begin(shm_shard *s, const uint64_t *keys, uint64_t n, void *stream,
+                           uint32_t *ticket);
+int shm_shard_search_end(shm_shard *s, uint32_t ticket, uint64_t *vals_out, uint8_t *found_out);
+int shm_shard_insert(shm_shard *s, const uint64_t *keys, const uint64_t *vals, uint64_t n,
+                     void *stream);
 
 /* workload generators on device (test/benchmark.cpp:43-46, zipf.h) ----------- */
 /* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */

@@ -124,6 +124,15 @@ _SIGNATURES = [
     ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute_found", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp]),
+    ("shm_tree_max_batch", u64, [vp]),
+    ("shm_nccl_unique_id", ctypes.c_int, [vp, u64]),
+    ("shm_shard_create", ctypes.c_int, [vp, vp, u64, u32, u32, ctypes.POINTER(vp)]),
+    ("shm_shard_create_with_comm", ctypes.c_int, [vp, vp, u32, u32, ctypes.POINTER(vp)]),
+    ("shm_shard_destroy", ctypes.c_int, [vp]),
+    ("shm_shard_search", ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
+    ("shm_shard_search_begin", ctypes.c_int, [vp, vp, u64, vp, ctypes.POINTER(u32)]),
+    ("shm_shard_search_end", ctypes.c_int, [vp, u32, vp, vp]),
+    ("shm_shard_insert", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     ("shm_hash_keys", ctypes.c_int, [vp, vp, u64, u64, vp, vp]),
 ]
@@ -451,8 +460,62 @@ def from_i64(x):
     return x & ((1 << 64) - 1)
 
 
+class CShard:
+    """A range shard of a multi-GPU tree behind the C-ABI (shm_shard_*): the
+    routed get / insert (bucketing, RCCL count exchange, grouped
+    ncclSend / ncclRecv of keys and values, local batch, un-permute) runs in
+    C++ over its own RCCL communicators.  All ranks construct it together
+    (ncclCommInitRank); rank 0's unique id travels over `dist`."""
+
+    def __init__(self, tree, world, rank, dist, group=None):
+        import torch
+        L = lib()
+        idb = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            _check(L.shm_nccl_unique_id(idb.data_ptr(), 128), "nccl_unique_id")
+        backend = dist.get_backend(group)
+        t = idb.to(f"cuda:{tree.device}") if backend == "nccl" else idb
+        dist.broadcast(t, 0, group=group)
+        idb = t.cpu()
+        h = vp()
+        _check(L.shm_shard_create(tree.h, idb.data_ptr(), 128, world, rank, ctypes.byref(h)),
+               "shard_create")
+        self.h, self.tree, self.world, self.rank = h, tree, world, rank
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().shm_shard_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def search(self, keys, vals_out, found_out, stream=None):
+        _check(lib().shm_shard_search(self.h, _ptr(keys), keys.numel(), _ptr(vals_out),
+                                      _ptr(found_out), _stream_ptr(stream)), "shard_search")
+
+    def search_begin(self, keys, stream=None):
+        tk = u32()
+        _check(lib().shm_shard_search_begin(self.h, _ptr(keys), keys.numel(),
+                                            _stream_ptr(stream), ctypes.byref(tk)),
+               "shard_search_begin")
+        return tk.value
+
+    def search_end(self, ticket, vals_out, found_out):
+        _check(lib().shm_shard_search_end(self.h, ticket, _ptr(vals_out), _ptr(found_out)),
+               "shard_search_end")
+
+    def insert(self, keys, vals, stream=None):
+        _check(lib().shm_shard_insert(self.h, _ptr(keys), _ptr(vals), keys.numel(),
+                                      _stream_ptr(stream)), "shard_insert")
+
+
 def header_symbols(path=HEADER_PATH):
     """Names of every function declared in include/sherman_amd.h."""
     import re
     txt = open(path).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(shm_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char \*)\s*(shm_\w+)\s*\(",
+                                 txt, re.M)))

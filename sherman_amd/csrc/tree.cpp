@@ -910,6 +910,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   return SHM_OK;
 }
 
+uint64_t shm_tree_max_batch(const shm_tree* t) { return t ? t->nmax : 0; }
+
 int shm_tree_destroy(shm_tree* t) {
   if (!t) return SHM_EINVAL;
   (void)hipSetDevice(t->cfg.device);

@@ -26,6 +26,12 @@ the GPU box, gloo in the CPU tests):
 `local` is the per-rank shard: a sherman_amd.Tree on the GPU path.  Any
 object with the same five methods works (the multi-rank CPU tests plug in an
 oracle-backed shard to check the exchange logic itself).
+
+With `cshard` (a sherman_amd.CShard) the get and insert routes run in C++
+behind the C-ABI (include/sherman_amd.h shm_shard_*, csrc/shard.cpp) over
+their own RCCL communicators, and this class only forwards to them; the
+Python exchange below remains the logic the CPU tests check and the range
+route.
 """
 import torch
 
@@ -69,8 +75,9 @@ def shard_range(rank, world):
 
 
 class ShardRouter:
-    def __init__(self, local, world, dist, group=None):
+    def __init__(self, local, world, dist, group=None, cshard=None):
         self.local, self.world, self.dist, self.group = local, world, dist, group
+        self.cshard = cshard
         self._bufs = {}
         self._pending = False  # a search_begin not yet ended (it owns kb / perm)
 
@@ -115,6 +122,9 @@ class ShardRouter:
 
     def search(self, keys, vals_out, found_out):
         """Batched get of this rank's keys; results land in input order."""
+        if self.cshard is not None:
+            self.cshard.search(keys, vals_out, found_out)
+            return
         self.search_end(self.search_begin(keys), vals_out, found_out)
 
     def search_begin(self, keys):
@@ -124,6 +134,8 @@ class ShardRouter:
         the time they are needed instead of queueing behind batch i's walk
         (bench.py, N > 1).  Every rank must begin and end the same batches
         in the same order (collectives)."""
+        if self.cshard is not None:  # two batches in flight per C shard
+            return ("cabi", keys, self.cshard.search_begin(keys))
         # the bucketed keys and permutation live in this router's buffers: one
         # batch in flight per router (bench.py alternates two routers)
         assert not self._pending, "ShardRouter: search_begin while a batch is in flight"
@@ -133,6 +145,9 @@ class ShardRouter:
     def search_end(self, pending, vals_out, found_out):
         """Second half: key exchange, local batched get, value exchange,
         un-permute into vals_out / found_out (input order)."""
+        if pending[0] == "cabi":
+            self.cshard.search_end(pending[2], vals_out, found_out)
+            return
         keys, kb, perm, cnts = pending
         self._pending = False
         n, dev = keys.numel(), keys.device
@@ -151,6 +166,9 @@ class ShardRouter:
 
     def insert(self, keys, vals):
         """Batched insert (value 0 deletes) of this rank's (key, value) pairs."""
+        if self.cshard is not None:
+            self.cshard.insert(keys, vals)
+            return
         dev = keys.device
         kb, perm, cnt, rcnt = self._bucket(keys)
         vb = self._buf("vb", keys.numel(), torch.int64, dev)
@@ -168,51 +186,51 @@ class ShardRouter:
         """Batched range scans [lo_i, hi_i] (inclusive, u64 held as int64).
         Returns (counts[n] int64, values): scan i's values are
         values[sum(counts[:i]) : sum(counts[:i+1])], in key order across shards
-        (leaf order, then slot order, inside a shard)."""
+        (leaf order, then slot order, inside a shard).
+
+        Every scan is cut into P pieces, piece s = its overlap with shard s
+        (empty, lo > hi, where it misses the shard), and row s of the P x n
+        piece matrix goes to rank s: no bucketing and no key-count exchange.
+        Host synchronisations: the ranks' scan counts (the receive splits) and
+        the ranks' value totals (the value splits), each one read-back."""
         n, dev, P = lo.numel(), lo.device, self.world
-        s0 = owner_of(lo, P)
-        s1 = torch.maximum(owner_of(hi, P), s0)        # lo > hi: one empty piece
-        s1 = torch.where((lo ^ _SIGN) > (hi ^ _SIGN), s0, s1)
-        npc = s1 - s0 + 1
-        total = int(npc.sum().item()) if n else 0
-        scan = torch.repeat_interleave(torch.arange(n, device=dev), npc)
-        first = torch.cumsum(npc, 0) - npc
-        shard = s0[scan] + (torch.arange(total, device=dev) - first[scan])
         bnd = shard_bounds(P, dev)
-        plo = umax(lo[scan], bnd[shard])
-        last = torch.where(shard + 1 < P, bnd[(shard + 1).clamp(max=P - 1)] - 1, bnd[P])
-        phi = umin(hi[scan], last)
-        # bucket the pieces by owner (stable) and exchange their bounds
-        kb, perm, cnt, rcnt = self._bucket(plo)
-        hb = self._buf("rq_hb", total, torch.int64, dev)
-        self.local.route_permute(phi, perm, hb)
-        nrecv = sum(rcnt)
+        first = bnd[:P]
+        last = torch.cat([bnd[1:P] - 1, bnd[P:P + 1]])  # inclusive top of shard s
+        plo = umax(lo.unsqueeze(0).expand(P, n), first.unsqueeze(1).expand(P, n)).contiguous()
+        phi = umin(hi.unsqueeze(0).expand(P, n), last.unsqueeze(1).expand(P, n)).contiguous()
+        # scan counts of every rank (receive splits)
+        cn = torch.full((2 * P,), n, dtype=torch.int64, device=dev)
+        self._a2a(cn[P:], cn[:P])
+        nr = self._counts(cn)[1]
+        nrecv = sum(nr)
         rlo = self._buf("rq_rlo", nrecv, torch.int64, dev)
         rhi = self._buf("rq_rhi", nrecv, torch.int64, dev)
-        self._a2a(rlo, kb, rcnt, cnt)
-        self._a2a(rhi, hb, rcnt, cnt)
+        self._a2a(rlo, plo.view(-1), nr, [n] * P)
+        self._a2a(rhi, phi.view(-1), nr, [n] * P)
         rc, rv = self.local.range_query_batch(rlo, rhi)
-        # counts back (piece order as sent), then values with per-rank splits
-        bc = self._buf("rq_bc", total, torch.int64, dev)
-        self._a2a(bc, rc.to(torch.int64), cnt, rcnt)
+        rc = rc.to(torch.int64)
+        # counts back: row s of c = this rank's piece counts on shard s
+        c = self._buf("rq_bc", P * n, torch.int64, dev)
+        self._a2a(c, rc, [n] * P, nr)
+        # value totals per peer (sent, received), one read-back for both
         seg = torch.repeat_interleave(torch.arange(P, device=dev),
-                                      torch.tensor(rcnt, device=dev))
-        vsend = torch.zeros(P, dtype=torch.int64, device=dev).index_add_(0, seg, rc.to(torch.int64))
-        vrecv = self._buf("rq_vr", P, torch.int64, dev)
-        self._a2a(vrecv, vsend)
-        vs, vr = vsend.tolist(), vrecv.tolist()
-        bv = self._buf("rq_bv", sum(vr), torch.int64, dev)
+                                      torch.tensor(nr, device=dev))
+        vt = torch.zeros(2 * P, dtype=torch.int64, device=dev)
+        vt[:P].index_add_(0, seg, rc)
+        self._a2a(vt[P:], vt[:P].clone())
+        vs, vr = self._counts(vt)
+        nv = sum(vr)
+        bv = self._buf("rq_bv", nv, torch.int64, dev)
         self._a2a(bv, rv, vr, vs)
-        # bucketed piece p is original piece perm[p]; reorder values to scan order
-        pc = torch.empty(total, dtype=torch.int64, device=dev)
-        pc[perm.long()] = bc
-        src_off = torch.cumsum(bc, 0) - bc                # offsets in bv (bucketed order)
-        src_of_orig = torch.empty(total, dtype=torch.int64, device=dev)
-        src_of_orig[perm.long()] = src_off
-        dst_off = torch.cumsum(pc, 0) - pc
-        nv = int(pc.sum().item()) if total else 0
-        shift = torch.repeat_interleave(src_of_orig - dst_off, pc)
+        # bv holds piece (s, i) at src_off[s, i] (shard-major); scan i takes
+        # its pieces s = 0 .. P - 1 in that order (key order across shards)
+        c = c.view(P, n)
+        src_off = (torch.cumsum(c.reshape(-1), 0) - c.reshape(-1)).view(P, n)
+        ct = c.t().contiguous()                       # [n, P], scan-major
+        dst_off = (torch.cumsum(ct.reshape(-1), 0) - ct.reshape(-1))
+        shift = torch.repeat_interleave(src_off.t().reshape(-1) - dst_off, ct.reshape(-1),
+                                        output_size=nv)
         values = bv[torch.arange(nv, device=dev) + shift] if nv else bv[:0]
-        counts = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, scan, pc)
+        counts = ct.sum(1)
         return counts, values
-

@@ -8,7 +8,10 @@ routed gets with misses, routed range scans across shard boundaries).
     makes at N > 1 (all_to_all_single with split lists, int64 payloads) run
     through RCCL on the box's one GPU;
   * world 2 over "gloo" with CUDA tensors: two ranks, two trees sharing the
-    GPU, each built with its shard's key-range hint, a real two-way exchange.
+    GPU, each built with its shard's key-range hint, a real two-way exchange;
+  * world 1 through the C-ABI shard (sherman_amd.CShard, shm_shard_* in
+    csrc/shard.cpp): routed get and insert in C++ over its own RCCL
+    communicators, including two batches in flight (begin, begin, end, end).
 
 One GPU is all a gpurun box has, and RCCL refuses two ranks on one device, so
 the RCCL exchange at world > 1 is covered by the driver's 8-GPU run; its
@@ -31,7 +34,7 @@ pytestmark = pytest.mark.gpu
 U64 = np.uint64
 
 
-def gpu_worker(rank, world, port, outdir, backend):
+def gpu_worker(rank, world, port, outdir, backend, cabi=False):
     import sherman_amd as shm
     from sherman_amd.shard import ShardRouter, shard_range
 
@@ -43,7 +46,8 @@ def gpu_worker(rank, world, port, outdir, backend):
     lo, bits = shard_range(rank, world)
     tree = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 14, device=0, node_id=rank,
                     key_lo=lo, key_bits=bits)
-    router = ShardRouter(tree, world, dist)
+    cs = shm.CShard(tree, world, rank, dist) if cabi else None
+    router = ShardRouter(tree, world, dist, cshard=cs)
 
     def d(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
@@ -55,6 +59,23 @@ def gpu_worker(rank, world, port, outdir, backend):
     vals = torch.empty(q.size, dtype=torch.int64, device=dev)
     found = torch.empty(q.size, dtype=torch.uint8, device=dev)
     router.search(d(q), vals, found)
+    if cabi:
+        # two batches in flight on two streams (the C shard's two slots)
+        q1, q2 = d(q), d(q[::-1].copy())
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        s1.wait_stream(torch.cuda.current_stream())
+        s2.wait_stream(torch.cuda.current_stream())
+        v1, f1 = torch.empty_like(vals), torch.empty_like(found)
+        v2, f2 = torch.empty_like(vals), torch.empty_like(found)
+        with torch.cuda.stream(s1):
+            p1 = router.search_begin(q1)
+        with torch.cuda.stream(s2):
+            p2 = router.search_begin(q2)
+        router.search_end(p1, v1, f1)
+        router.search_end(p2, v2, f2)
+        torch.cuda.synchronize()
+        assert torch.equal(v1, vals) and torch.equal(f1, found)
+        assert torch.equal(v2, vals.flip(0)) and torch.equal(f2, found.flip(0))
     slo, shi = scan_batch(rank, world)
     counts, svals = router.range_query(d(slo), d(shi))
     torch.cuda.synchronize()
@@ -63,6 +84,8 @@ def gpu_worker(rank, world, port, outdir, backend):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), keys=keys, values=values,
              vals=vals.cpu().numpy(), found=found.cpu().numpy(), check=np.array([rc]),
              scounts=counts.cpu().numpy(), svals=svals.cpu().numpy())
+    if cs is not None:
+        cs.close()
     tree.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -79,9 +102,11 @@ def tree_contents(tree):
     return k, v
 
 
-@pytest.mark.parametrize("backend,world", [("nccl", 1), ("gloo", 2)])
-def test_routed_gpu_shards_match_unsharded_oracle(backend, world):
+@pytest.mark.parametrize("backend,world,cabi", [("nccl", 1, False), ("gloo", 2, False),
+                                                ("nccl", 1, True)])
+def test_routed_gpu_shards_match_unsharded_oracle(backend, world, cabi):
     assert torch.cuda.is_available(), "GPU test without a GPU"
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(gpu_worker, args=(world, free_port(), d, backend), nprocs=world, join=True)
+        mp.spawn(gpu_worker, args=(world, free_port(), d, backend, cabi), nprocs=world,
+                 join=True)
         verify_against_unsharded(d, world)
