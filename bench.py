@@ -71,7 +71,8 @@ def parse():
     p.add_argument("--scan-keys", type=int, default=100,
                    help="c5: expected stored keys per range scan")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=6.0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU baseline sample length (C1: >= 5 two-second windows)")
     p.add_argument("--sort", choices=("auto", "on", "off"), default="auto",
                    help="order get batches by key before the walk: always "
                         "(SHM_FLAG_SORT_GETS), never, or when dense (default)")
@@ -322,7 +323,7 @@ def main():
     cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
-            cpu, parity = cpu_baseline_get(tree, qs, vals, found, args, step)
+            cpu, parity = cpu_baseline_get(tree, qs, vals, found, args, step, dev)
         elif args.workload == "c5":
             cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step)
         else:
@@ -591,49 +592,113 @@ def _oracle_on_gpu_image(tree, spare_bytes=0):
     return orc
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), or None
+    when unlimited / not readable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
 def _threads():
+    """T = the CPUs this process may actually run on, one pinned thread each
+    (test/benchmark.cpp:96 bindCore; SURVEY §8d: T = nproc): the affinity
+    mask, capped by the cgroup CPU quota.  On the GPU box the mask lists all
+    256 host CPUs but cpu.max grants 16; 256 threads there are throttled to
+    16 CPUs' worth of time and the C1 leg measures 15 Mops/s against 44 at
+    T = 16 (profiles/r02_cpu_threads.txt)."""
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return max(1, min(16, ncpu))
+    q = _cgroup_cpus()
+    return max(1, min(ncpu, q) if q else ncpu)
 
 
-def cpu_baseline_get(tree, qs, vals, found, args, step):
-    """Reference Tree::search restated in C (oracle/, "port"), run on this
-    host's cores over the GPU's own page image (identical tree), on a bounded
-    sample: repeated 1 Mi-query batches for ~args.cpu_seconds."""
+C1_KEYSPACE = 64 << 20     # kKeySpace (test/benchmark.cpp:21)
+C1_WARM = 0.8              # kWarmRatio (test/benchmark.cpp:22)
+C1_PRELOAD = 1024000       # test/benchmark.cpp:269-274
+
+
+def c1_tree_image(dev):
+    """The reference benchmark's tree at C1 (kKeySpace = 2^26 WITH the
+    modulus): preload to_key(i) -> 2i for i = 1..1,024,000, then the warm-up
+    inserts to_key(i) -> 2i for i in [1, 0.8 * kKeySpace) (the preload is a
+    subset with the same values), built through the GPU batch insert (the
+    same key -> value contents; keys that collide under the modulus keep the
+    largest i, one of the orders the reference's racing warm-up threads can
+    produce).  Returns (image, root) for the oracle."""
+    import torch
+    import sherman_amd as shm
+    t = shm.Tree(arena_bytes=3 << 30, max_batch=1 << 20, device=dev.index or 0)
+    end = int(C1_WARM * C1_KEYSPACE)
+    k = torch.empty(1 << 20, dtype=torch.int64, device=dev)
+    for first in range(1, end, 1 << 20):
+        m = min(1 << 20, end - first)
+        t.gen_keys(first, m, k[:m], keyspace=C1_KEYSPACE)
+        ids = torch.arange(first, first + m, dtype=torch.int64, device=dev)
+        t.insert_batch_async(k[:m], ids * 2)
+    t.synchronize()
+    img, root = t.dump_image()
+    t.close()
+    return img, root
+
+
+def cpu_baseline_c1(dev, seconds):
+    """C1 (BASELINE.json configs[0]): the reference benchmark's measured
+    phase, kNodeCount = 1, kReadRatio = 100, zipf theta = 0 over kKeySpace,
+    restated in C (oracle/ orc_c1_bench: pinned threads, key =
+    to_key(zipf_next()), Tree::search, per-thread op counters sampled every
+    2 s), on every CPU of the affinity mask; the steady-state mean over
+    >= 5 two-second windows (test/benchmark.cpp:165-188, 302-341)."""
+    import numpy as np
+    from oracle.pyoracle import OracleTree
+    img, root = c1_tree_image(dev)
+    orc = OracleTree(image=img, root_ptr=root)
+    threads = _threads()
+    windows = max(5, int(round(seconds / 2.0)))
+    w = orc.c1_bench(threads, C1_KEYSPACE, theta=0.0, windows=windows, window_s=2.0)
+    rc, shape = orc.check()
+    orc.close()
+    del img
+    return {
+        "value": round(float(np.mean(w[1:])), 3),
+        "unit": "Mops/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"C1: reference test/benchmark read phase restated in C (oracle/), "
+                  f"kKeySpace 2^26 with the modulus, {shape['keys']} keys (preload 1,024,000 + "
+                  f"warm 0.8), uniform to_key(zipf(theta=0)) searches, {threads} pinned "
+                  f"threads on {cpu_name()}, {windows} x 2 s windows (first dropped): "
+                  + ", ".join("%.2f" % x for x in w),
+    }
+
+
+def cpu_baseline_get(tree, qs, vals, found, args, step, dev):
+    """Parity of one full C2 batch against the oracle's Tree::search over the
+    GPU's own page image, then the C1 CPU baseline (cpu_baseline_c1)."""
     import numpy as np
     import torch
 
     orc = _oracle_on_gpu_image(tree)
-    threads = _threads()
     q0 = qs[0].cpu().numpy().view(np.uint64)
-    step(0)  # parity on one full batch: same queries through the GPU path
+    step(0)  # the same queries through the GPU path
     torch.cuda.synchronize()
     gv = vals.cpu().numpy().view(np.uint64)
     gf = found.cpu().numpy()
-    done, secs, parity = 0, 0.0, None
-    while secs < args.cpu_seconds or done == 0:
-        ov, of, s = orc.search_batch_mt(q0, threads)
-        if parity is None:
-            parity = bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
-        secs += s
-        done += q0.size
+    ov, of, _ = orc.search_batch_mt(q0, _threads())
+    parity = bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
     orc.close()
-    cpu = {
-        "value": round(done / secs / 1e6, 3),
-        "unit": "Mops/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{done} uniform gets ({done // q0.size} x 1 Mi batch) over the "
-                  f"GPU-built tree image, oracle Tree::search restatement, "
-                  f"{threads} pinned threads on {cpu_name()}",
-    }
-    return cpu, parity
+    return cpu_baseline_c1(dev, args.cpu_seconds), parity
 
 
 def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     """C5 batches on the oracle over the GPU's image: the batch's range scans
-    (restated Tree::range_query, one call per scan) then its inserts (restated
-    Tree::insert), single-threaded, for ~args.cpu_seconds.  Parity: the first
+    (restated Tree::range_query) then its inserts (restated Tree::insert), on
+    every CPU of the affinity mask (inserts partitioned by page lock word,
+    orc_apply_batch_mt), for ~args.cpu_seconds.  Parity: the first
     two batches' scans return the GPU's values per scan (as multisets: leaf
     boundaries after the batched splits may differ from the one-op-at-a-time
     oracle's, and slots inside a leaf are unsorted)."""
@@ -641,6 +706,7 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     import torch
 
     orc = _oracle_on_gpu_image(tree, spare_bytes=2 << 30)  # C5 inserts new keys
+    threads = _threads()
     parity = True
     done, secs, b = 0, 0.0, 0
     while secs < args.cpu_seconds or b < 2:
@@ -656,10 +722,9 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
         hih = hi.cpu().numpy().view(np.uint64)
         pkh = pk.cpu().numpy().view(np.uint64)
         pvh = pv.cpu().numpy().view(np.uint64)
-        t0 = time.perf_counter()
-        oc, ov = orc.range_query_batch(loh, hih)
-        orc.apply_batch(pkh, pvh)
-        secs += time.perf_counter() - t0
+        oc, ov, s1 = orc.range_query_batch_mt(loh, hih, threads)
+        s2 = orc.apply_batch_mt(pkh, pvh, threads)
+        secs += s1 + s2
         if b < 2:
             ooff = np.concatenate([[0], np.cumsum(oc)]).astype(np.int64)
             parity = parity and bool(np.array_equal(oc.astype(np.int64), gc))
@@ -672,19 +737,20 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     cpu = {
         "value": round(done / secs / 1e6, 3),
         "unit": "Mops/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
         "sample": f"{b} C5 1 Mi-op batches ({done} ops) over the GPU-built tree image: "
                   f"range scans then inserts, oracle Tree::range_query / Tree::insert "
-                  f"restatement, 1 thread on {cpu_name()}",
+                  f"restatement, {threads} pinned threads (inserts partitioned by page "
+                  f"lock word) on {cpu_name()}",
     }
     return cpu, parity
 
 
 def cpu_baseline_mixed(tree, mixed, vals, found, args, step):
     """Mixed batches on the oracle over the GPU's image: gets on `threads`
-    pinned threads, then the batch's inserts (the restated Tree::insert is
-    single-threaded), for ~args.cpu_seconds.  Parity: the first two batches'
+    pinned threads, then the batch's inserts on the same threads partitioned
+    by page lock word (orc_apply_batch_mt), for ~args.cpu_seconds.  Parity: the first two batches'
     get results (the second sees the first's inserts) equal the GPU's."""
     import numpy as np
     import torch
@@ -704,9 +770,7 @@ def cpu_baseline_mixed(tree, mixed, vals, found, args, step):
         pkh = pk.cpu().numpy().view(np.uint64)
         pvh = pv.cpu().numpy().view(np.uint64)
         ov, of, s = orc.search_batch_mt(gkh, threads)
-        t0 = time.perf_counter()
-        orc.apply_batch(pkh, pvh)
-        s += time.perf_counter() - t0
+        s += orc.apply_batch_mt(pkh, pvh, threads)
         if b < 2:
             parity = parity and bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
         secs += s
@@ -719,8 +783,9 @@ def cpu_baseline_mixed(tree, mixed, vals, found, args, step):
         "cores": threads,
         "kind": "port",
         "sample": f"{b} mixed 1 Mi-op batches ({done} ops) over the GPU-built tree "
-                  f"image: gets on {threads} pinned threads, inserts on 1 thread "
-                  f"(oracle Tree::search / Tree::insert restatement) on {cpu_name()}",
+                  f"image on {threads} pinned threads: gets, then inserts partitioned by "
+                  f"page lock word (oracle Tree::search / Tree::insert restatement) on "
+                  f"{cpu_name()}",
     }
     return cpu, parity
 

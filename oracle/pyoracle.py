@@ -47,6 +47,13 @@ def lib():
         L.orc_search_batch_mt.restype = ctypes.c_double
         L.orc_search_batch_mt.argtypes = [vp, vp, u64, vp, vp, ctypes.c_int]
         L.orc_apply_batch.argtypes = [vp, vp, vp, u64]
+        L.orc_apply_batch_mt.restype = ctypes.c_double
+        L.orc_apply_batch_mt.argtypes = [vp, vp, vp, u64, ctypes.c_int]
+        L.orc_range_query_batch_mt.restype = u64
+        L.orc_range_query_batch_mt.argtypes = [vp, vp, vp, u64, vp, vp, u64, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_double)]
+        L.orc_c1_bench.argtypes = [vp, ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_int,
+                                   ctypes.c_double, vp]
         L.orc_root_ptr.restype = u64
         L.orc_root_ptr.argtypes = [vp]
         L.orc_root_level.restype = ctypes.c_int
@@ -161,6 +168,37 @@ class OracleTree:
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         vals = np.ascontiguousarray(vals, dtype=np.uint64)
         lib().orc_apply_batch(self.h, _p(keys), _p(vals), keys.size)
+
+    def apply_batch_mt(self, keys, vals, nthreads):
+        """apply_batch on `nthreads` threads partitioned by page lock word
+        (same contents); returns seconds."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals, dtype=np.uint64)
+        return lib().orc_apply_batch_mt(self.h, _p(keys), _p(vals), keys.size, nthreads)
+
+    def range_query_batch_mt(self, lo, hi, nthreads):
+        """range_query_batch on `nthreads` threads: (counts, values, seconds)."""
+        lo = np.ascontiguousarray(lo, dtype=np.uint64)
+        hi = np.ascontiguousarray(hi, dtype=np.uint64)
+        counts = np.zeros(lo.size, dtype=np.uint64)
+        cap = max(1024, 128 * lo.size)
+        secs = ctypes.c_double()
+        while True:
+            out = np.empty(cap, dtype=np.uint64)
+            total = lib().orc_range_query_batch_mt(self.h, _p(lo), _p(hi), lo.size, _p(counts),
+                                                   _p(out), cap, nthreads, ctypes.byref(secs))
+            if total <= cap:
+                return counts, out[:total].copy(), secs.value
+            cap = int(total)
+
+    def c1_bench(self, nthreads, keyspace, theta=0.0, seed_base=0x5EED0000, windows=5,
+                 window_s=2.0):
+        """The reference benchmark's read phase on pinned threads
+        (test/benchmark.cpp:165-188, 302-341): Mops/s of each window."""
+        out = np.zeros(windows, dtype=np.float64)
+        lib().orc_c1_bench(self.h, nthreads, keyspace, theta, seed_base, windows, window_s,
+                           _p(out))
+        return out
 
     def dump(self, cap=None):
         L = lib()

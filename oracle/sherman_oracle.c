@@ -96,6 +96,7 @@ struct orc_tree {
   uint64_t root;     /* g_root_ptr / *root_ptr_ptr (Tree.cpp:90-114) */
   int root_level;    /* g_root_level (Directory.cpp:72-79) */
   uint64_t read_pages;
+  int mt; /* multi-threaded run in progress: page reads are not counted */
   uint64_t path[K_MAX_LEVEL]; /* path_stack (Tree.cpp:21-22), single coro */
 };
 
@@ -128,7 +129,9 @@ static uint64_t orc_alloc(orc_tree *t) {
 /* dsm->read_sync(page_buffer, addr, 1024) */
 static void read_page(orc_tree *t, uint64_t ga, uint8_t *buf) {
   memcpy(buf, page_at(t, ga), K_PAGE);
-  __atomic_fetch_add(&t->read_pages, 1, __ATOMIC_RELAXED);
+  /* DSM read counter (DSM.cpp:119-120); not kept while threads share the
+   * tree, so the threads do not contend on one counter line */
+  if (!t->mt) t->read_pages++;
 }
 static void write_bytes(orc_tree *t, uint64_t ga, const uint8_t *src,
                         uint32_t n) {
@@ -652,6 +655,7 @@ static void *mt_worker(void *a_) {
 double orc_search_batch_mt(orc_tree *t, const uint64_t *keys, uint64_t n,
                            uint64_t *vals, uint8_t *found, int nthreads) {
   if (nthreads < 1) nthreads = 1;
+  t->mt = 1;
   pthread_t th[256];
   mt_arg args[256];
   if (nthreads > 256) nthreads = 256;
@@ -676,6 +680,7 @@ double orc_search_batch_mt(orc_tree *t, const uint64_t *keys, uint64_t n,
   }
   for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
   clock_gettime(CLOCK_MONOTONIC, &e);
+  t->mt = 0;
   return (double)(e.tv_sec - s.tv_sec) + 1e-9 * (double)(e.tv_nsec - s.tv_nsec);
 }
 
@@ -928,4 +933,349 @@ void orc_op_mix(unsigned int seed, int read_ratio, uint8_t *is_get,
                 uint64_t count) {
   for (uint64_t i = 0; i < count; ++i)
     is_get[i] = (uint8_t)(rand_r(&seed) % 100 < read_ratio);
+}
+
+/* ---- multi-threaded CPU baseline (the reference benchmark's thread model) --
+ * Threads pinned 1:1 to the CPUs of the affinity mask (bindCore,
+ * src/Common.cpp:11-20; test/benchmark.cpp:96). */
+static int avail_cpus(int *cpus, int max) {
+  cpu_set_t avail;
+  CPU_ZERO(&avail);
+  sched_getaffinity(0, sizeof(avail), &avail);
+  int n = 0;
+  for (int c = 0; c < CPU_SETSIZE && n < max; ++c)
+    if (CPU_ISSET(c, &avail)) cpus[n++] = c;
+  if (n == 0) cpus[n++] = 0;
+  return n;
+}
+static void pin_cpu(int cpu) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpu, &set);
+  pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+static double now_s(void) {
+  struct timespec s;
+  clock_gettime(CLOCK_MONOTONIC, &s);
+  return (double)s.tv_sec + 1e-9 * (double)s.tv_nsec;
+}
+
+/* Tree::insert's descent to the leaf (Tree.cpp:353-403), read-only */
+static uint64_t locate_leaf(orc_tree *t, uint64_t k) {
+  uint64_t p = t->root;
+  search_result r;
+  for (int hops = 0; hops < 1 << 20; ++hops) {
+    if (!page_search(t, p, k, &r, 0)) return 0;
+    if (r.is_leaf) {
+      if (r.sibling != 0) { /* k >= highest: turn right */
+        p = r.sibling;
+        continue;
+      }
+      return p;
+    }
+    p = r.sibling != 0 ? r.sibling : r.next_level;
+    if (p == 0) return 0;
+  }
+  return 0;
+}
+
+/* leaf_page_store's no-split path (Tree.cpp:875-921) applied in place by the
+ * thread that owns the page's lock word; 0 when the insert would reach 54
+ * entries (the split point, Tree.cpp:914): the page is left untouched */
+static int leaf_store_inplace(orc_tree *t, uint64_t page_addr, uint64_t k, uint64_t v) {
+  uint8_t *page = page_at(t, page_addr);
+  int cnt = 0, empty_index = -1;
+  for (int i = 0; i < K_LEAF_CARD; ++i) {
+    uint8_t *e = L_BASE(page, i);
+    if (L_VAL(page, i) != K_VALUE_NULL) {
+      cnt++;
+      if (L_KEY(page, i) == k) {
+        st64(e + 9, v);
+        set_fver(e, (L_FVER(page, i) + 1) & 0xF);
+        set_rver(e, L_FVER(page, i));
+        return 1;
+      }
+    } else if (empty_index == -1) {
+      empty_index = i;
+    }
+  }
+  if (cnt + 1 >= K_LEAF_CARD || empty_index < 0) return 0;
+  uint8_t *e = L_BASE(page, empty_index);
+  st64(e + 1, k);
+  st64(e + 9, v);
+  set_fver(e, (L_FVER(page, empty_index) + 1) & 0xF);
+  set_rver(e, L_FVER(page, empty_index));
+  return 1;
+}
+
+/* leaf_page_del's body (Tree.cpp:1037-1055) on the located leaf */
+static void leaf_del_inplace(orc_tree *t, uint64_t page_addr, uint64_t k) {
+  uint8_t *page = page_at(t, page_addr);
+  for (int i = 0; i < K_LEAF_CARD; ++i) {
+    uint8_t *e = L_BASE(page, i);
+    if (L_KEY(page, i) == k && L_VAL(page, i) != K_VALUE_NULL) {
+      st64(e + 9, K_VALUE_NULL);
+      set_fver(e, (L_FVER(page, i) + 1) & 0xF);
+      set_rver(e, L_FVER(page, i));
+      return;
+    }
+  }
+}
+
+typedef struct {
+  orc_tree *t;
+  const uint64_t *keys, *vals;
+  uint64_t n;
+  uint64_t *leaf;
+  uint16_t *owner;
+  uint8_t *defer;
+  int tid, nthreads, cpu;
+  pthread_barrier_t *bar;
+} am_arg;
+
+/* tiny open-addressing set of page addresses (per thread) */
+typedef struct {
+  uint64_t *slot;
+  uint64_t cap, n;
+} pset;
+static int pset_has(const pset *s, uint64_t x) {
+  if (!s->cap) return 0;
+  for (uint64_t h = (x * 0x9E3779B97F4A7C15ull) & (s->cap - 1);; h = (h + 1) & (s->cap - 1)) {
+    if (s->slot[h] == x) return 1;
+    if (s->slot[h] == 0) return 0;
+  }
+}
+static void pset_add(pset *s, uint64_t x) {
+  if (2 * (s->n + 1) > s->cap) {
+    pset o = *s;
+    s->cap = o.cap ? 2 * o.cap : 64;
+    s->slot = (uint64_t *)calloc(s->cap, 8);
+    s->n = 0;
+    for (uint64_t i = 0; i < o.cap; ++i)
+      if (o.slot[i]) pset_add(s, o.slot[i]);
+    free(o.slot);
+  }
+  uint64_t h = (x * 0x9E3779B97F4A7C15ull) & (s->cap - 1);
+  while (s->slot[h] != 0 && s->slot[h] != x) h = (h + 1) & (s->cap - 1);
+  if (s->slot[h] == 0) {
+    s->slot[h] = x;
+    s->n++;
+  }
+}
+
+static void *am_worker(void *a_) {
+  am_arg *a = (am_arg *)a_;
+  pin_cpu(a->cpu);
+  /* 1. every op's leaf (a read-only descent; no page splits yet) and the
+   *    thread owning its lock word lock[CityHash64(page) % kNumOfLock]
+   *    (Tree.cpp:832-842, kNumOfLock = 16384, include/Common.h:87-93) */
+  const uint64_t lo = a->n * (uint64_t)a->tid / a->nthreads;
+  const uint64_t hi = a->n * (uint64_t)(a->tid + 1) / a->nthreads;
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t k = a->keys[i];
+    const uint64_t lf = k == K_KEY_MAX ? 0 : locate_leaf(a->t, k);
+    a->leaf[i] = lf;
+    a->owner[i] = (uint16_t)(lf ? (orc_cityhash64(&lf, 8) % 16384) % (uint64_t)a->nthreads : 0);
+  }
+  pthread_barrier_wait(a->bar);
+  /* 2. this thread's pages, in batch order: in place, or (the page would
+   *    split) left for the serial pass together with every later op on it */
+  pset deferred = {0, 0, 0};
+  for (uint64_t i = 0; i < a->n; ++i) {
+    if (a->owner[i] != (uint16_t)a->tid) continue;
+    const uint64_t lf = a->leaf[i];
+    if (!lf || pset_has(&deferred, lf)) {
+      a->defer[i] = 1;
+      continue;
+    }
+    if (a->vals[i] == K_VALUE_NULL) {
+      leaf_del_inplace(a->t, lf, a->keys[i]);
+    } else if (!leaf_store_inplace(a->t, lf, a->keys[i], a->vals[i])) {
+      pset_add(&deferred, lf);
+      a->defer[i] = 1;
+    }
+  }
+  free(deferred.slot);
+  return NULL;
+}
+
+/* The batch applied in order (Tree::insert / Tree::del per op) by `nthreads`
+ * threads partitioned by page lock word, as concurrent Sherman clients
+ * serialise on those words; ops on a page that must split run afterwards in
+ * batch order on one thread (splits touch parents).  Same key->value
+ * contents as orc_apply_batch.  Returns seconds. */
+double orc_apply_batch_mt(orc_tree *t, const uint64_t *keys, const uint64_t *vals, uint64_t n,
+                          int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  static int cpus[1024];
+  const int ncpu = avail_cpus(cpus, 1024);
+  uint64_t *leaf = (uint64_t *)malloc(8 * (n ? n : 1));
+  uint16_t *owner = (uint16_t *)malloc(2 * (n ? n : 1));
+  uint8_t *defer = (uint8_t *)calloc(n ? n : 1, 1);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+  am_arg *args = (am_arg *)malloc(sizeof(am_arg) * nthreads);
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+  const double t0 = now_s();
+  t->mt = 1;
+  for (int i = 0; i < nthreads; ++i) {
+    args[i] = (am_arg){t, keys, vals, n, leaf, owner, defer, i, nthreads, cpus[i % ncpu], &bar};
+    pthread_create(&th[i], NULL, am_worker, &args[i]);
+  }
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  t->mt = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!defer[i]) continue;
+    if (vals[i] == K_VALUE_NULL)
+      orc_del(t, keys[i]);
+    else
+      orc_insert(t, keys[i], vals[i]);
+  }
+  const double secs = now_s() - t0;
+  pthread_barrier_destroy(&bar);
+  free(leaf);
+  free(owner);
+  free(defer);
+  free(th);
+  free(args);
+  return secs;
+}
+
+typedef struct {
+  orc_tree *t;
+  const uint64_t *from, *to;
+  uint64_t lo, hi;
+  uint64_t *counts;
+  const uint64_t *offs;
+  uint64_t *out;
+  int cpu;
+} rq_arg;
+static void *rq_worker(void *a_) {
+  rq_arg *a = (rq_arg *)a_;
+  pin_cpu(a->cpu);
+  for (uint64_t i = a->lo; i < a->hi; ++i) {
+    if (a->offs)
+      (void)orc_range_query(a->t, a->from[i], a->to[i], a->out + a->offs[i], a->counts[i]);
+    else
+      a->counts[i] = orc_range_query(a->t, a->from[i], a->to[i], NULL, 0);
+  }
+  return NULL;
+}
+
+/* orc_range_query_batch on `nthreads` threads: counts, then the values at
+ * their offsets (out must hold the total, which is returned).  Seconds in
+ * *secs. */
+uint64_t orc_range_query_batch_mt(orc_tree *t, const uint64_t *from, const uint64_t *to,
+                                  uint64_t n, uint64_t *counts, uint64_t *out, uint64_t cap,
+                                  int nthreads, double *secs) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  static int cpus[1024];
+  const int ncpu = avail_cpus(cpus, 1024);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+  rq_arg *args = (rq_arg *)malloc(sizeof(rq_arg) * nthreads);
+  uint64_t *offs = (uint64_t *)malloc(8 * (n ? n : 1));
+  const double t0 = now_s();
+  t->mt = 1;
+  uint64_t total = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      for (uint64_t i = 0; i < n; ++i) {
+        offs[i] = total;
+        total += counts[i];
+      }
+      if (total > cap) break;
+    }
+    for (int i = 0; i < nthreads; ++i) {
+      args[i] = (rq_arg){t, from, to, n * (uint64_t)i / nthreads, n * (uint64_t)(i + 1) / nthreads,
+                         counts, pass ? offs : NULL, out, cpus[i % ncpu]};
+      pthread_create(&th[i], NULL, rq_worker, &args[i]);
+    }
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  }
+  t->mt = 0;
+  if (secs) *secs = now_s() - t0;
+  free(th);
+  free(args);
+  free(offs);
+  return total;
+}
+
+typedef struct {
+  orc_tree *t;
+  uint64_t keyspace;
+  double theta;
+  uint64_t seed;
+  int cpu;
+  volatile int *stop;
+  volatile int *ready;
+  volatile uint64_t *count; /* this thread's op counter (own cache line) */
+} c1_arg;
+static void *c1_worker(void *a_) {
+  c1_arg *a = (c1_arg *)a_;
+  pin_cpu(a->cpu);
+  orc_zipf z;
+  orc_zipf_init(&z, a->keyspace, a->theta, a->seed);
+  __atomic_fetch_add(a->ready, 1, __ATOMIC_RELEASE);
+  uint64_t done = 0;
+  while (!__atomic_load_n(a->stop, __ATOMIC_RELAXED)) {
+    for (int j = 0; j < 256; ++j) {
+      /* key = to_key(zipf_next()), a search (kReadRatio = 100),
+       * test/benchmark.cpp:165-177 */
+      const uint64_t key = orc_to_key(orc_zipf_next(&z), a->keyspace);
+      uint64_t v;
+      (void)orc_search(a->t, key, &v);
+    }
+    done += 256;
+    *a->count = done;  /* tp[id][0] (test/benchmark.cpp:186) */
+  }
+  return NULL;
+}
+
+/* The reference benchmark's measured phase on `nthreads` pinned threads
+ * (test/benchmark.cpp:165-188 with kReadRatio = 100): every thread draws
+ * key = to_key(zipf_next()) over `keyspace` with its own generator (seed
+ * seed_base + thread id) and searches it; the main thread samples the
+ * threads' op counters every window_s seconds (test/benchmark.cpp:302-341)
+ * and writes each window's Mops/s to win_mops[0 .. windows). */
+void orc_c1_bench(orc_tree *t, int nthreads, uint64_t keyspace, double theta,
+                  uint64_t seed_base, int windows, double window_s, double *win_mops) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  static int cpus[1024];
+  const int ncpu = avail_cpus(cpus, 1024);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+  c1_arg *args = (c1_arg *)malloc(sizeof(c1_arg) * nthreads);
+  volatile uint64_t *cnt = (volatile uint64_t *)calloc((size_t)nthreads * 8, 8);
+  volatile int stop = 0, ready = 0;
+  t->mt = 1;
+  for (int i = 0; i < nthreads; ++i) {
+    args[i] = (c1_arg){t, keyspace, theta, (seed_base + (uint64_t)i) & 0xFFFFFFFFFFFFull,
+                       cpus[i % ncpu], &stop, &ready, cnt + 8 * i};
+    pthread_create(&th[i], NULL, c1_worker, &args[i]);
+  }
+  while (__atomic_load_n(&ready, __ATOMIC_ACQUIRE) < nthreads) {
+  }
+  uint64_t prev = 0;
+  double ts = now_s();
+  for (int w = 0; w < windows; ++w) {
+    const double until = ts + window_s;
+    while (now_s() < until) {
+      struct timespec nap = {0, 2000000};
+      nanosleep(&nap, NULL);
+    }
+    const double te = now_s();
+    uint64_t all = 0;
+    for (int i = 0; i < nthreads; ++i) all += cnt[8 * i];
+    win_mops[w] = (double)(all - prev) / (te - ts) / 1e6;
+    prev = all;
+    ts = te;
+  }
+  __atomic_store_n(&stop, 1, __ATOMIC_RELAXED);
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  t->mt = 0;
+  free(th);
+  free(args);
+  free((void *)cnt);
 }

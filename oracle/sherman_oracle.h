@@ -71,6 +71,16 @@ double orc_search_batch_mt(orc_tree *t, const uint64_t *keys, uint64_t n,
                            uint64_t *vals, uint8_t *found, int nthreads);
 /* sequential insert of a batch in batch order (last writer wins);
  * value 0 means delete (kValueNull, Common.h:117). */
+/* the same contents on `nthreads` threads partitioned by page lock word;
+ * returns seconds */
+double orc_apply_batch_mt(orc_tree *t, const uint64_t *keys, const uint64_t *vals, uint64_t n,
+                          int nthreads);
+uint64_t orc_range_query_batch_mt(orc_tree *t, const uint64_t *from, const uint64_t *to,
+                                  uint64_t n, uint64_t *counts, uint64_t *out, uint64_t cap,
+                                  int nthreads, double *secs);
+/* the reference benchmark's read phase (test/benchmark.cpp:165-188, 302-341) */
+void orc_c1_bench(orc_tree *t, int nthreads, uint64_t keyspace, double theta,
+                  uint64_t seed_base, int windows, double window_s, double *win_mops);
 void orc_apply_batch(orc_tree *t, const uint64_t *keys, const uint64_t *vals,
                      uint64_t n);
 

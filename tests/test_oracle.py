@@ -159,3 +159,36 @@ def test_golden_tree_fixture():
     v, f = t.search_batch(probe)
     assert int(f.sum()) == g["found"]
     assert int(np.bitwise_xor.reduce(v)) == g["xor_values"]
+
+
+def test_mt_apply_and_range_match_serial():
+    """The CPU baseline's multi-threaded legs (orc_apply_batch_mt partitioned
+    by page lock word, orc_range_query_batch_mt) leave the same contents and
+    return the same scans as the serial restatement."""
+    import numpy as np
+    from oracle.pyoracle import OracleTree, to_key
+    rng = np.random.default_rng(99)
+    universe = np.array([to_key(i) for i in range(1, 60001)], dtype=np.uint64)
+    a, b = OracleTree(256 << 20), OracleTree(256 << 20)
+    for r in range(6):
+        n = 40000 if r else 50000
+        ks = universe[rng.integers(0, universe.size, n)]
+        vs = rng.integers(1, 1 << 62, n).astype(np.uint64)
+        vs[rng.random(n) < 0.1] = 0
+        a.apply_batch(ks, vs)
+        b.apply_batch_mt(ks, vs, 7)
+        ka, va = a.dump()
+        kb, vb = b.dump()
+        oa, ob = np.argsort(ka), np.argsort(kb)
+        assert np.array_equal(ka[oa], kb[ob]) and np.array_equal(va[oa], vb[ob])
+        assert b.check()[0] == 0
+    lo = rng.integers(0, 1 << 63, 500, dtype=np.uint64) * np.uint64(2)
+    hi = lo + (np.uint64(1) << np.uint64(56))
+    hi[hi < lo] = np.uint64((1 << 64) - 1)
+    ca, xa = b.range_query_batch(lo, hi)
+    cb, xb, _ = b.range_query_batch_mt(lo, hi, 5)
+    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
+    w = b.c1_bench(2, 1 << 20, windows=2, window_s=0.2)
+    assert w.size == 2 and (w > 0).all()
+    a.close()
+    b.close()
