@@ -408,14 +408,9 @@ def main():
     q_per_launch = prof["queries"] / max(prof["calls"], 1)
     achieved = q_per_launch * ALG_BYTES_PER_GET / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_walk.json")
-    if args.workload == "c2" and os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("batch") == batch and pmc.get("keys_log2") == args.keys_log2:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    if args.workload == "c2":
+        traffic = _profile_traffic("pmc_walk.json", "hbm_bytes_per_launch", batch,
+                                   args.keys_log2)
 
     if rank == 0:
         if args.workload == "c2":
@@ -515,18 +510,34 @@ def main():
                 "inserts_per_launch": int(ins_per_launch),
                 "range_ms_per_launch": round(range_ms, 4),
                 "walk_ms_per_launch": None, "order_ms_per_launch": None,
-                "queries_per_launch": None, "alg_bytes_per_get": None})
+                "queries_per_launch": None, "alg_bytes_per_get": None,
+                "traffic": _profile_traffic("pmc_insert.json", "hbm_bytes_per_chunk",
+                                            batch, args.keys_log2)})
         if args.workload == "c3":
             # whole-step algorithmic rate (gets 1040 B, inserts 1074 B per op)
             step_s = elapsed / args.steps
             b0 = mixed[0]
             alg = (b0[0].numel() * ALG_BYTES_PER_GET + b0[1].numel() * ALG_BYTES_PER_INSERT)
             out["roofline"]["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
+            out["roofline"]["step_frac"] = round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
     tree.close()
+
+
+def _profile_traffic(name, field, batch, keys_log2):
+    """HBM bytes per launch measured by the committed PMC passes
+    (profiles/<name>, tools/refresh_profiles.py) when they were taken at this
+    batch and key count, else None."""
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", name)))
+    except (OSError, ValueError):
+        return None
+    if pmc.get("batch") == batch and pmc.get("keys_log2") == keys_log2:
+        return pmc.get(field)
+    return None
 
 
 def make_cshard(tree, world, rank, dist, dev, args, keys_local):

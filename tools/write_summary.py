@@ -14,6 +14,8 @@ import json
 import os
 import sys
 
+INSERT_KERNELS = ("k_tile_dedup", "k_part_coarse", "k_bin_", "k_locate", "k_seg_",
+                  "k_leaf_", "k_upper")
 ANCHOR = {"c3": "k_get<", "c5": "k_range", "c2": "k_get<"}
 
 
@@ -67,6 +69,15 @@ def main(d, wl):
             e["fetch_bytes_x2"] = round(f)
             e["write_bytes"] = round(w)
         out["kernels"][k] = e
+    # the insert chunk's kernels (ordering, locate, segmentation, upsert,
+    # split levels): HBM bytes and kernel time per step
+    ins = {k: e for k, e in out["kernels"].items() if any(p in k for p in INSERT_KERNELS)}
+    out["insert_chunk"] = {
+        "kernels": sorted(ins),
+        "kernel_us_per_step": round(sum(e["us_per_step"] for e in ins.values()), 2),
+        "hbm_bytes_per_step": round(sum(e.get("hbm_bytes_per_launch", 0) * e["calls_per_step"]
+                                        for e in ins.values())),
+    }
     print(json.dumps(out, indent=1))
 
 
