@@ -9,25 +9,31 @@
 // whose per-range new-page counts it accumulated in UpperCtl.
 //
 // k_upper is ONE persistent launch (one block per CU, all resident) that
-// finishes the batch:
-//   leaf level     P2  per block: ordered scan of its segment range's new-page
-//                      counts -> seg_pbase and a dense list of split segments
-//                  --- grid barrier ---
-//                  P3  every wave: build new right siblings (k-way split,
-//                      ceil(T / 36) pages), each emitting its separator and the
-//                      parent it belongs to (a header walk from the root);
-//                      then page 0 of each split segment is rewritten in
-//                      place (set_consistent: front++ , rear = front) once
+// finishes the batch.  Work is split by block range (the upsert kernel
+// assigns segment g to range g * nb / ns and counts its new pages there), so
+// a block finds its global page bases from the per-range counts alone and a
+// grid barrier is needed only where a level hands its separators to the
+// next one:
+//   leaf level     P2  per block: ordered scan of its range's new-page counts
+//                      -> its split segments and their first new page
+//                  P3  the block's waves: build new right siblings (k-way
+//                      split, ceil(T / 36) pages), each emitting its separator
+//                      and the parent it belongs to (a header walk from the
+//                      root); then page 0 of each split segment is rewritten
+//                      in place (set_consistent: front++ , rear = front) once
 //                      every sibling builder has read the old page (a per-
-//                      segment counter), and its lock word released
+//                      segment counter)
 //                  --- grid barrier ---
 //   level L >= 1   I1  per block: segment heads of its separator range, one
 //                      wave per head: lock the page (HBM lock table), plan T
 //                      and P (in place if T <= 60, else ceil((T + 1) / 41))
-//                  --- barrier ---  I2 prefix: dense segment list + page bases
-//                  --- barrier ---  I3 build / rewrite as for leaves
-//                  --- barrier ---  next level while separators remain
+//                  --- grid barrier ---
+//                  I2  per block: its dense segment list and page bases
+//                  I3  the block's waves: build / rewrite as for leaves
+//                  --- grid barrier, only if the level made separators ---
 //   deletes            every wave: Tree::del of the chunk's deletes
+// Lock words are epoch tagged (take_word below): nothing is released page by
+// page; the next chunk's larger tag releases them all.
 // Pages come from a device bump cursor (the superblock's next_page; the
 // reference's LocalAllocator bump, include/LocalAllocator.h:21-43), checked
 // against the arena capacity before each level.  The root page never moves:
@@ -62,9 +68,17 @@ __device__ __forceinline__ uint32_t lock_index(uint64_t page, uint32_t n) {
   return (uint32_t)(cityhash64_u64(page) % n);
 }
 
-__device__ __forceinline__ void release_word(const uint64_t* locks, uint32_t num, uint64_t page) {
-  __hip_atomic_store(const_cast<uint64_t*>(locks) + lock_index(page, num), 0ull,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Lock words (the reference's lock table, Tree.cpp:205-264) are epoch
+// tagged: a chunk takes a word with atomic max of its tag (chunk number << 32;
+// a smaller value is an earlier chunk's hold, released when that chunk
+// retired) and never stores it back.  Every word a chunk holds is released at
+// once when the chunk retires, since the next chunk's tag is larger.  Only
+// the deletes need mutual exclusion inside a chunk: they hold tag | 1 and
+// hand the word back at the chunk's tag.
+__device__ __forceinline__ bool take_word(uint64_t* locks, uint32_t num, uint64_t page,
+                                          uint64_t tag) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(locks) + lock_index(page, num);
+  return atomicMax(w, (unsigned long long)tag) <= (unsigned long long)tag;
 }
 
 // the ops of one segment: keys [st, st + nb) of a sorted unique op array
@@ -320,31 +334,51 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* red, uint32
   return base + incl - v;
 }
 
-// Grid barrier over all resident blocks: every wave's stores performed, one
-// agent-scope release per block, arrive on a monotonic counter, poll it with
-// relaxed agent loads, one agent-scope acquire per block (MI355X_MICROARCH.md
-// "barrier-counter"; the counter is a multiple of nb between launches).
-// Bounded: a spin past kBarrierSpins sets the abort word, which releases every
-// other block too; returns false then.
+// Grid barrier over all resident blocks, XCD-hierarchical
+// (MI355X_MICROARCH.md "barrier-xcd", ≈4 µs at 256 blocks against ≈7 for one
+// counter): every wave's stores performed, then one lane per block: release
+// fence, arrive on its XCD group's counter (blocks are dealt to the 8 XCDs
+// round-robin, b % 8; the grouping only affects speed); the group's last
+// arrival is its leader: it arrives on the top counter, polls it until all
+// groups are in, and publishes the generation to its group, whose other
+// blocks poll that word; acquire fence.  All counters are monotonic, so the
+// generation a barrier completes is derived from the value an arrival
+// returns.  Bounded: a spin past kBarrierSpins sets the abort word, which
+// releases every other block too; returns false then.
 __device__ bool grid_sync(UpperCtl* ctl, uint32_t nb, uint32_t* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    const uint32_t nx = nb < 8u ? nb : 8u;
+    const uint32_t x = blockIdx.x % nx;
+    const uint64_t m = nb / nx + (x < nb % nx ? 1u : 0u);  // blocks of group x
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t old =
-        __hip_atomic_fetch_add(&ctl->bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t target = (old / nb + 1) * nb;
+        __hip_atomic_fetch_add(&ctl->xbar[x][0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t e = old / m + 1;  // the generation this barrier completes
     uint32_t ok = 1;
-    for (uint32_t spin = 0;; ++spin) {
-      if (__hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-          spin > kBarrierSpins) {
-        __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
+    auto spin_until = [&](uint64_t* w, uint64_t want) {
+      for (uint32_t spin = 0;; ++spin) {
+        if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return;
+        if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+            spin > kBarrierSpins) {
+          __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
+    };
+    if (old % m == m - 1) {
+      // leader: the group's releases happened before its arrivals
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      const uint64_t ot =
+          __hip_atomic_fetch_add(&ctl->top[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      spin_until(&ctl->top[0], (ot / nx + 1) * nx);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      __hip_atomic_store(&ctl->gen[x][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      spin_until(&ctl->gen[x][0], e);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -443,9 +477,14 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
     lw = (uint64_t)lock_index(ptr, a.num_locks);
     uint32_t got = 0;
     if (lane == 0) {
+      // free for this delete: any value <= the chunk's tag (an earlier chunk's
+      // hold or this chunk's upserts); tag | 1 = another delete of the chunk
       unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.locks) + lw;
+      const unsigned long long mine = (unsigned long long)(a.tag | 1ull);
       for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-        if (atomicCAS(wd, 0ull, (unsigned long long)a.tag) == 0ull) {
+        const unsigned long long cur =
+            __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur <= (unsigned long long)a.tag && atomicCAS(wd, cur, mine) == cur) {
           got = 1;
           break;
         }
@@ -466,7 +505,7 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
     }
     if (k >= h.highest && h.sibling != 0) {  // Tree.cpp:1028-1032
       if (lane == 0)
-        __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.locks + lw, a.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       locked = false;
       ptr = h.sibling;
       continue;
@@ -484,11 +523,12 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
     break;
   }
   if (locked) {
-    // write_page_and_unlock (Tree.cpp:1049-1052): the entry store first
+    // write_page_and_unlock (Tree.cpp:1049-1052): the entry store first,
+    // then the word back at the chunk's tag
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(a.locks + lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.locks + lw, a.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -508,6 +548,14 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   const uint64_t T = (uint64_t)nb * kUpT, tid = (uint64_t)b * kUpT + (uint64_t)t;
   WaveLds& L = s_l[wv];
   UpperCtl* ctl = a.ctl;
+  uint32_t nstamp = 1;
+  auto stamp = [&]() {
+    if (a.stamps && b == 0 && t == 0 && nstamp < (uint32_t)kUpperStamps) {
+      a.stamps[nstamp++] = wall_clock64();
+      a.stamps[0] = nstamp;
+    }
+  };
+  stamp();
   Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
   uint64_t cursor = sb->next_page;
   uint32_t root_level = (uint32_t)sb->root_level;
@@ -528,11 +576,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   const uint32_t nsplit = block_sum(v_ns, s_red);
   const uint32_t pre_np = block_sum((uint32_t)t < b ? v_np : 0u, s_red);
   const uint32_t pre_ns = block_sum((uint32_t)t < b ? v_ns : 0u, s_red);
-  // in-place segments were written by the upsert kernel: release their words
-  // (write_page_and_unlock's unlock half, Tree.cpp:266-298); split ones stay
-  // held until their page 0 is rewritten below
-  for (uint64_t g = tid; g < ns; g += T)
-    if (a.seg_lk[g] && a.seg_P[g] <= 1) release_word(a.locks, a.num_locks, a.seg_page[g]);
+  (void)nsplit;
   bool ok = true;
   uint32_t nsep = 0;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
@@ -540,10 +584,9 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   if (total && !fits) {
     // arena exhausted: the flagged segments stay unapplied (reported)
     err |= kErrNoMem;
-    for (uint64_t g = tid; g < ns; g += T)
-      if (a.seg_lk[g] && a.seg_P[g] > 1) release_word(a.locks, a.num_locks, a.seg_page[g]);
   } else if (total) {
-    // ---- P2: this block's segment range in order -> seg_pbase, split list --
+    // ---- P2: this block's segment range in order -> its split list, at the
+    // global positions the upsert kernel's per-range counts give ------------
     uint32_t r0, r1;
     block_range(ns, b, nb, r0, r1);
     uint32_t run_np = pre_np, run_ns = pre_ns;
@@ -560,12 +603,14 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       run_np += tnp;
       run_ns += tns;
     }
-    ok = grid_sync(ctl, nb, &s_flag);
-    // ---- P3: new right siblings, then page 0 of every split ----------------
+    __syncthreads();  // the block's split list is complete (workgroup scope)
+    stamp();
+    // ---- P3: this block's new right siblings, then page 0 of its splits ----
     const uint64_t first = cursor;  // arena page of global new page 0
     const uint64_t xroot = cursor + total;  // the root's left half (grow0)
-    for (uint64_t gp = wid; ok && gp < total; gp += W) {
-      const uint32_t k = last_le(a.spl_base, nsplit, (uint32_t)gp);
+    const uint32_t my_ns = run_ns - pre_ns;
+    for (uint32_t gp = pre_np + (uint32_t)wv; gp < run_np; gp += kUpWaves) {
+      const uint32_t k = pre_ns + last_le(a.spl_base + pre_ns, my_ns, gp);
       const uint32_t g = a.spl_seg[k];
       const uint32_t pb = a.spl_base[k];
       const int p = (int)(gp - pb) + 1;
@@ -588,7 +633,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         a.ipage[0][gp] = par_pg;
       }
     }
-    for (uint64_t k = wid; ok && k < nsplit; k += W) {
+    for (uint32_t k = pre_ns + (uint32_t)wv; k < run_ns; k += kUpWaves) {
       const uint32_t g = a.spl_seg[k];
       const uint32_t pb = a.spl_base[k];
       const int P = (int)a.seg_P[g];
@@ -605,17 +650,16 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       const SplitPage sp{0, P, a.seg_T[g], first + pb, dest};
       (void)build_leaf_page(a, L, h, na, o, sp);
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
-      if (lane == 0) {
-        a.leaf_rd[g] = 0;  // for the next batch
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.seg_lk[g]) release_word(a.locks, a.num_locks, page);
-      }
+      if (lane == 0) a.leaf_rd[g] = 0;  // for the next batch
     }
     cursor += total + (grow0 ? 1u : 0u);
     if (grow0) root_level = 1;
     made += total;
     nsep = total;
-    ok = ok && grid_sync(ctl, nb, &s_flag);
+    stamp();
+    // the next level reads every block's separators
+    ok = grid_sync(ctl, nb, &s_flag);
+    stamp();
   }
 
   // ---- internal levels ------------------------------------------------------
@@ -661,18 +705,8 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         if (!ptr_ok(page, a.node, a.arena_bytes)) {
           err |= kErrBadPtr;
         } else {
-          if (lane == 0) {
-            unsigned long long* wd =
-                reinterpret_cast<unsigned long long*>(a.locks) + lock_index(page, a.num_locks);
-            for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-              const unsigned long long old = atomicCAS(wd, 0ull, (unsigned long long)a.tag);
-              if (old == 0ull || old == a.tag) {
-                lk = 1;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-            }
-          }
+          // the parent's word, held until the chunk retires (epoch tags)
+          if (lane == 0) lk = take_word(a.locks, a.num_locks, page, a.tag) ? 1u : 0u;
           lk = rl32(lk, 0);
           if (!lk) err |= kErrLock;
           const u32x4 w = load_page_slice(a.arena, ga_offset(page));
@@ -715,16 +749,24 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         ctl->int_np[b] = bn;
       }
     }
+    stamp();
     ok = grid_sync(ctl, nb, &s_flag);
+    stamp();
     if (!ok) break;
-    // ---- I2: dense segment list and new-page bases, in key order ------------
+    // ---- I2: this block's dense segment list and new-page bases, at global
+    // positions (every block has the per-range counts now) -------------------
     const uint32_t vh = (uint32_t)t < nb ? ctl->int_heads[t] : 0u;
     const uint32_t vp = (uint32_t)t < nb ? ctl->int_np[t] : 0u;
-    const uint32_t nseg = block_sum(vh, s_red);
     const uint32_t tot = block_sum(vp, s_red);
-    uint32_t run_h = block_sum((uint32_t)t < b ? vh : 0u, s_red);
-    uint32_t run_p = block_sum((uint32_t)t < b ? vp : 0u, s_red);
-    const bool fit = cursor + tot + (grow ? 1u : 0u) <= cap;
+    const uint32_t h0 = block_sum((uint32_t)t < b ? vh : 0u, s_red);
+    const uint32_t p0 = block_sum((uint32_t)t < b ? vp : 0u, s_red);
+    if (cursor + tot + (grow ? 1u : 0u) > cap) {
+      // arena exhausted (every block sees the same totals): this level stays
+      // unapplied; B-link keeps every key reachable through the siblings
+      err |= kErrNoMem;
+      break;
+    }
+    uint32_t run_h = h0, run_p = p0;
     for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
       const uint32_t i = c0 + (uint32_t)t;
       const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
@@ -739,22 +781,13 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       run_h += th;
       run_p += tp;
     }
-    if (!fit) {
-      // arena exhausted: this level stays unapplied (B-link keeps every key
-      // reachable through the siblings); release its locks
-      err |= kErrNoMem;
-      for (uint32_t i = r0 + (uint32_t)t; i < r1; i += kUpT)
-        if ((i == 0 || spg[i] != spg[i - 1]) && a.h_lk[i])
-          release_word(a.locks, a.num_locks, spg[i]);
-      break;
-    }
-    ok = grid_sync(ctl, nb, &s_flag);
-    if (!ok) break;
-    // ---- I3: new pages, then page 0 of every segment --------------------------
+    __syncthreads();  // the block's list is complete (workgroup scope)
+    stamp();
+    // ---- I3: this block's new pages, then page 0 of each of its segments ----
     const uint64_t first = cursor;
     const uint64_t xroot = cursor + tot;
-    for (uint64_t gp = wid; gp < tot; gp += W) {
-      const uint32_t s = last_le(a.d_base, nseg, (uint32_t)gp);
+    for (uint32_t gp = p0 + (uint32_t)wv; gp < run_p; gp += kUpWaves) {
+      const uint32_t s = h0 + last_le(a.d_base + h0, run_h - h0, gp);
       const uint32_t hi = a.d_head[s];
       const uint32_t pb = a.d_base[s];
       const int p = (int)(gp - pb) + 1;
@@ -773,7 +806,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         a.ipage[nxt][gp] = par_pg;
       }
     }
-    for (uint64_t s = wid; s < nseg; s += W) {
+    for (uint32_t s = h0 + (uint32_t)wv; s < run_h; s += kUpWaves) {
       const uint32_t hi = a.d_head[s];
       const uint64_t page = spg[hi];
       const int P = (int)a.h_P[hi];
@@ -794,18 +827,18 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
           if (rootsplit) write_new_root(a, L, dest, level + 1, h.fver);
         }
       }
-      if (lane == 0) {
-        a.int_rd[s] = 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.h_lk[hi]) release_word(a.locks, a.num_locks, page);
-      }
+      if (lane == 0) a.int_rd[s] = 0;
     }
     const bool grew = grow && tot > 0;
     cursor += tot + (grew ? 1u : 0u);
     if (grew) root_level = level + 1;
     made += tot;
     nsep = tot;
-    ok = grid_sync(ctl, nb, &s_flag);
+    stamp();
+    if (tot) {  // the next level reads every block's separators
+      ok = grid_sync(ctl, nb, &s_flag);
+      stamp();
+    }
   }
   if (!ok) err |= kErrRounds;
   // the chunk's deletes, after every split (Tree::del, Tree.cpp:542-591):
@@ -813,6 +846,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   const uint64_t n_del = *a.n_del;
   for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
+  stamp();
   if (b == 0 && t == 0) {
     // superblock (device-authoritative) and its host mirror
     sb->next_page = cursor;

@@ -56,7 +56,12 @@ void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, 
 // k_upper runs one block per CU (at most kMaxUpper); its control block.
 constexpr int kMaxUpper = 512;
 struct UpperCtl {
-  uint64_t bar;     // grid-barrier arrivals (monotonic, a multiple of the grid between launches)
+  // XCD-hierarchical grid barrier (insert.hip grid_sync), each word on a
+  // 128 B line of its own: arrivals per XCD group, the XCD leaders' count,
+  // and the generation each leader publishes to its group (all monotonic)
+  uint64_t xbar[8][16];
+  uint64_t top[16];
+  uint64_t gen[8][16];
   uint32_t abort;   // a barrier timed out: every block leaves (sticky)
   uint32_t gate;    // tag of the last chunk rejected by its ordering (kKeyMax)
   // leaf split counts of the upsert kernel per k_upper block range, double
@@ -147,7 +152,11 @@ struct UpperArgs {
   uint64_t dir_lo;
   uint64_t dir_n;
   uint32_t dir_shift;
+  // nullable: block 0 records the wall clock (100 MHz) at each phase end,
+  // stamps[0] = count (tools/upper_stamps.py)
+  uint64_t* stamps;
 };
+constexpr int kUpperStamps = 32;
 uint32_t upper_blocks();
 void launch_upper(const UpperArgs& a, hipStream_t s);
 
@@ -208,9 +217,10 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
 // Segments of a located op list (n_dev: device-side op count <= n) in two
 // launches: per 1024-op tile a head count (bsum), then each tile sums the
 // counts before it and fills its segments, taking each segment's lock word
-// (lane per segment, atomicCAS(0 -> tag) on lock[CityHash64(page) %
-// num_locks], bounded spin; seg_lk[s] = 1 when held; segments sharing a word
-// share the hold).  bsum holds seg_tiles(n) words.
+// (lane per segment, atomic max of the chunk's epoch tag on
+// lock[CityHash64(page) % num_locks]; seg_lk[s] = 1 when held; segments
+// sharing a word share the hold; every word is released when the chunk
+// retires, insert.hip take_word).  bsum holds seg_tiles(n) words.
 struct SegLock {
   uint64_t* locks;
   uint32_t num_locks;

@@ -45,6 +45,7 @@ struct shm_tree {
   uint64_t arena_bytes = 0;
   uint64_t cap_pages = 0;
   uint64_t* locks = nullptr;
+  uint64_t* stamps = nullptr;  // k_upper phase clock (shm__upper_stamps), off when null
   uint32_t* d_err = nullptr;
   uint64_t* d_counts = nullptr;  // 16 words of device scratch
   uint32_t* route_scratch = nullptr;
@@ -556,6 +557,7 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   u.dk = t->dk;
   u.n_del = t->d_counts + 1;
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
+  u.stamps = t->stamps;
   dev::launch_upper(u, s);
   DBG(s, "upper");
   HIP_OK(hipGetLastError());
@@ -592,7 +594,7 @@ void free_all(shm_tree* t) {
   auto F = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  F(t->arena); F(t->locks); F(t->d_err); F(t->d_counts); F(t->route_scratch);
+  F(t->arena); F(t->locks); F(t->stamps); F(t->d_err); F(t->d_counts); F(t->route_scratch);
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
@@ -1131,6 +1133,30 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   a.vals = vals_out;
   a.vals_cap = vals_cap;
   return range_launch(t, s, a);
+}
+
+// Diagnostics, not part of include/sherman_amd.h: enable = 1 turns k_upper's
+// phase clock on, 0 off; out (nullable, kUpperStamps words) receives the last
+// chunk's stamps (out[0] = count, then 100 MHz wall-clock values).
+int shm__upper_stamps(shm_tree* t, int enable, uint64_t* out) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (enable == 1 && !t->stamps) {
+    if (hipMalloc(&t->stamps, sizeof(uint64_t) * dev::kUpperStamps) != hipSuccess)
+      return SHM_ENOMEM;
+    HIP_OK(hipMemset(t->stamps, 0, sizeof(uint64_t) * dev::kUpperStamps));
+  }
+  if (out && t->stamps) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, t->stamps, sizeof(uint64_t) * dev::kUpperStamps,
+                     hipMemcpyDeviceToHost));
+  }
+  if (enable == 0 && t->stamps) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipFree(t->stamps));
+    t->stamps = nullptr;
+  }
+  return SHM_OK;
 }
 
 int shm_stats(shm_tree* t, shm_stats_t* o) {

@@ -103,18 +103,14 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
       seg_start[pos] = (uint32_t)i;
       seg_page[pos] = pg;
       if (lk.locks) {
-        // lock_and_read_page's lock half (Tree.cpp:205-242, 851), as k_seg_fill
+        // lock_and_read_page's lock half (Tree.cpp:205-242, 851) with an
+        // epoch tag (insert.hip take_word): a smaller value is a retired
+        // chunk's hold, the chunk's own tag a shared hold; held until the
+        // chunk retires
         unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
                                 cityhash64_u64(pg) % lk.num_locks;
-        uint32_t ok = 0;
-        for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-          const unsigned long long o = atomicCAS(w, 0ull, (unsigned long long)lk.tag);
-          if (o == 0ull || o == lk.tag) {
-            ok = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
+        const uint32_t ok =
+            atomicMax(w, (unsigned long long)lk.tag) <= (unsigned long long)lk.tag ? 1u : 0u;
         if (!ok) atomicOr(lk.err, kErrLock);
         lk.seg_lk[pos] = ok;
       }

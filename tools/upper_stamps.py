@@ -1,0 +1,56 @@
+"""k_upper phase clock (diagnostic; run on the GPU box):
+    python tools/upper_stamps.py [keys_log2] [batches]
+Builds a tree of 2^keys_log2 keys, then applies C5-like insert batches
+(1 Mi ops, key = to_key(1 + zipf(0.99) over twice the key set)) and C3-like
+ones (zipf over the stored keys: updates only) and prints, per batch, the
+microseconds between k_upper's phase stamps (block 0's view: start, lock
+release, leaf P2, barrier, P3, barrier, then I1 / barrier / I2 / barrier /
+I3 / barrier per internal level, deletes, end)."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import sherman_amd as shm  # noqa: E402
+from sherman_amd.workload import Zipf  # noqa: E402
+
+
+def main():
+    kl = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    nb = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    dev = torch.device("cuda:0")
+    n = 1 << kl
+    t = shm.Tree(arena_bytes=max(2 << 30, n * 1024 // 20), max_batch=1 << 20, device=0)
+    keys = torch.empty(1 << 20, dtype=torch.int64, device=dev)
+    for c in range(0, n, 1 << 20):
+        m = min(1 << 20, n - c)
+        t.gen_keys(1 + c, m, keys[:m])
+        t.insert_batch(keys[:m], torch.arange(1 + c, 1 + c + m, dtype=torch.int64, device=dev) * 2)
+    lib = shm.lib()
+    fn = lib.shm__upper_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    fn(t.h, 1, None)
+    out = (ctypes.c_uint64 * 32)()
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    for name, zn in (("c5", 2 * n), ("c3", n)):
+        z = Zipf(zn, 0.99, dev)
+        for b in range(nb):
+            ids = z.sample(1 << 20, g) + 1
+            k = torch.empty_like(ids)
+            t.hash_keys(ids, k)
+            v = torch.arange(1, (1 << 20) + 1, dtype=torch.int64, device=dev)
+            t.insert_batch(k, v)
+            fn(t.h, 2, out)
+            cnt = int(out[0])
+            ts = [int(out[i]) for i in range(1, cnt)]
+            d = [round((ts[i] - ts[i - 1]) / 100.0, 1) for i in range(1, len(ts))]  # 100 MHz
+            print(name, b, "total %.1f us" % ((ts[-1] - ts[0]) / 100.0), d, flush=True)
+    fn(t.h, 0, None)
+    t.close()
+
+
+if __name__ == "__main__":
+    main()
