@@ -89,6 +89,9 @@ def parse():
                    help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
                         "range partition (the per-GPU work of an N-GPU run, no exchange)")
     p.add_argument("--sim-rank", type=int, default=0)
+    p.add_argument("--start", choices=("dir", "root"), default="dir",
+                   help="where gets and locates start: the leaf directory (default) or the "
+                        "root (a descent through the cached upper levels; A/B for DESIGN §8)")
     p.add_argument("--no-range-hint", action="store_true",
                    help="do not pass the shard key range to the tree (A/B)")
     p.add_argument("--router", choices=("auto", "cabi", "python"), default="auto",
@@ -183,7 +186,8 @@ def main():
     key_lo, key_bits = (0, 64) if args.no_range_hint else shard_range(s_rank, s_world)
     # N > 1: a rank receives ~batch routed keys (+ a few %), keep one chunk
     tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch + (batch >> 2 if world > 1 else 0)), device=local,
-                    node_id=rank, sort_gets={"on": True, "off": False}.get(args.sort, "auto"), key_lo=key_lo, key_bits=key_bits)
+                    node_id=rank, sort_gets={"on": True, "off": False}.get(args.sort, "auto"), key_lo=key_lo, key_bits=key_bits,
+                    leaf_dir=args.start == "dir")
 
     t0 = time.time()
     keys_local, inserted = build_shard(tree, n_keys, s_world, s_rank, dev)
@@ -463,6 +467,7 @@ def main():
                 "streams": (len(outs) if args.workload == "c2" else 1),
                 "rccl_groups": (len(outs) if args.workload == "c2" and world > 1 else None),
                 "router": router_kind,
+                "start": args.start,
                 "build_inserts_per_s": round(inserted / build_s, 1),
                 "hit_rate": round(hit_rate, 4),
                 "splits_in_timed_steps": st_end["splits"] - splits0,

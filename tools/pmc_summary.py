@@ -1,4 +1,5 @@
-"""Average each counter per dispatch for the get-path kernels of a pmc.sh run."""
+"""Average each counter per dispatch for the kernels of a pmc.sh run (all
+kernels the pass collected, keyed by name without the argument list)."""
 import collections
 import csv
 import glob
@@ -10,11 +11,8 @@ d = sys.argv[1]
 agg = collections.defaultdict(list)
 for p in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
-        n = r["Kernel_Name"]
-        for tag in ("k_get<", "k_walk<false", "k_part_coarse_hist", "k_part_coarse_scatter",
-                    "k_part_fine", "k_unpartition"):
-            if tag in n:
-                agg[(tag, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        n = r["Kernel_Name"].split("(")[0]
+        agg[(n, r["Counter_Name"])].append(float(r["Counter_Value"]))
 out = collections.defaultdict(dict)
 for (k, c), v in sorted(agg.items()):
     out[k][c] = sum(v) / len(v)
