@@ -12,8 +12,10 @@
 //   3. k_bin_unique   every bin: last writer per key, sorted (below); a bin
 //                     over 6144 ops (clustered keys) is sorted by the same
 //                     block with a stable LSD radix sort through global
-//                     scratch, so every batch is ordered on the device.
-//   4. k_bin_emit     every bin's survivors at its prefix: uk / uv / dk.
+//                     scratch, so every batch is ordered on the device.  The
+//                     bin then finds its place among the bins (tagged count
+//                     words, bin_prefix) and writes its survivors straight
+//                     to uk / uv / dk.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
     }
   }
   if (bad) {
-    // the chunk is rejected whole (k_bin_emit emits nothing) and reported
+    // the chunk is rejected whole (k_bin_unique emits nothing) and reported
     atomicOr(err, kErrKeyMax);
     *gate = tag;
   }
@@ -174,10 +176,9 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
 //      the whole bin with the LDS bitonic network instead;
 //   d. each survivor's value classifies it as an upsert or a delete (value 0
 //      = kValueNull, Tree.cpp:881); local ranks by one block scan.
-// Survivors go back to the bin's slots of keys1 / pay1 (op index), their
-// local rank to lrank (bit 31 = delete), the bin's (upserts, deletes) to
-// bcnt.  k_bin_emit then places every bin at its prefix: uk / uv (upserts,
-// key order) and dk (deletes), totals in counts[0..1].
+// The bin's (upserts, deletes) give its place among the bins (bin_prefix),
+// and its survivors go straight to uk / uv (upserts, key order) and dk
+// (deletes); the last bin writes the totals to counts[0..1].
 constexpr int kUniqSlots = 8192;  // LDS hash slots (96 KB with the op indices)
 constexpr int kUniqCap = 6144;    // ops per bin handled here (load <= 0.75)
 constexpr int kUniqPer = kUniqCap / kIT;
@@ -195,8 +196,8 @@ constexpr int kUniqPer = kUniqCap / kIT;
 __device__ void big_bin_unique(uint64_t* __restrict__ keys1, uint32_t* __restrict__ pay1,
                                uint64_t* __restrict__ kscr, uint32_t* __restrict__ iscr,
                                uint32_t start, uint32_t cnt, const uint64_t* __restrict__ vals,
-                               uint32_t* __restrict__ lrank, uint32_t* __restrict__ bcnt,
-                               uint32_t b, uint32_t* ldsw) {
+                               uint32_t* __restrict__ lrank, uint32_t* cnt2,
+                               uint32_t* ldsw) {
   constexpr int kW = kIT / kWave;  // 16 waves
   uint32_t* h8 = ldsw;                  // [8][256] digit histograms
   uint32_t* wc = ldsw + 8 * 256;        // [16][256] per-wave digit counts
@@ -293,9 +294,69 @@ __device__ void big_bin_unique(uint64_t* __restrict__ keys1, uint32_t* __restric
     __syncthreads();
   }
   if (t == 0) {
-    bcnt[2 * b] = ru;
-    bcnt[2 * b + 1] = rd;
+    cnt2[0] = ru;
+    cnt2[1] = rd;
   }
+  __syncthreads();
+}
+
+// Bin b's place among the bins: publish its (upserts, deletes) in its
+// tagged word (chunk tag << 48 | upserts << 24 | deletes), then wave 0 waits
+// for the words of bins < b and sums them (the last bin sums all of them into
+// counts[0..1]).  All kCoarse bins are resident together (one block per CU),
+// and a bin waits only on bins of smaller index, dispatched before it.
+__device__ void bin_prefix(uint64_t* lbw, uint32_t b, uint32_t tag, uint32_t ups, uint32_t dels,
+                           uint32_t* red, uint32_t& bu, uint32_t& bd, uint64_t* counts,
+                           uint32_t* err) {
+  const uint64_t tg = (uint64_t)(tag & 0xFFFFu);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lbw + b, (tg << 48) | ((uint64_t)ups << 24) | dels, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < (unsigned)kWave) {
+    const uint32_t lane = threadIdx.x;
+    const bool last = b == (uint32_t)kCoarse - 1;
+    const uint32_t lim = last ? (uint32_t)kCoarse : b;
+    uint64_t su = 0, sd = 0, tu = 0, td = 0;
+    for (uint32_t i = lane; i < lim; i += kWave) {
+      uint64_t w = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        w = __hip_atomic_load(lbw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w >> 48) == tg) break;
+        if (spin > (1u << 24)) {
+          atomicOr(err, kErrRounds);
+          w = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint64_t u = (w >> 24) & 0xFFFFFFu, d = w & 0xFFFFFFu;
+      if (i < b) {
+        su += u;
+        sd += d;
+      }
+      tu += u;
+      td += d;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      su += __shfl_xor(su, o);
+      sd += __shfl_xor(sd, o);
+      tu += __shfl_xor(tu, o);
+      td += __shfl_xor(td, o);
+    }
+    if (lane == 0) {
+      red[0] = (uint32_t)su;
+      red[1] = (uint32_t)sd;
+      if (last) {
+        counts[0] = tu;
+        counts[1] = td;
+      }
+    }
+  }
+  __syncthreads();
+  bu = red[0];
+  bd = red[1];
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1,
@@ -304,9 +365,14 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
                                                    KeyRange kr,
                                                    const uint64_t* __restrict__ vals,
                                                    uint32_t* __restrict__ lrank,
-                                                   uint32_t* __restrict__ bcnt,
+                                                   uint64_t* __restrict__ lbw,
                                                    uint64_t* __restrict__ kscr,
                                                    uint32_t* __restrict__ iscr,
+                                                   uint64_t* __restrict__ uk,
+                                                   uint64_t* __restrict__ uv,
+                                                   uint64_t* __restrict__ dk,
+                                                   uint64_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ err,
                                                    uint32_t* __restrict__ S,
                                                    const uint32_t* gate, uint32_t tag) {
   constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
@@ -315,16 +381,33 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   __shared__ uint32_t hist[kFine];
   __shared__ uint32_t wsum[kIT / kWave];
   __shared__ uint32_t s_big;
+  __shared__ uint32_t s_cnt2[2];
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t b = blockIdx.x;
   // the coarse pass is complete: clear its group sums for the next batch
   if (b == 0)
     for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
-  if (*gate == tag) return;  // rejected chunk (k_bin_emit emits nothing)
+  if (*gate == tag) {  // rejected chunk (kKeyMax): nothing to apply
+    if (b == 0 && t == 0) counts[0] = counts[1] = 0;
+    return;
+  }
   const uint32_t start = bins[2 * b], cnt = bins[2 * b + 1];
   if (cnt > (uint32_t)kUniqCap) {  // block-uniform
-    big_bin_unique(keys1, pay1, kscr, iscr, start, cnt, vals, lrank, bcnt, b,
+    big_bin_unique(keys1, pay1, kscr, iscr, start, cnt, vals, lrank, s_cnt2,
                    reinterpret_cast<uint32_t*>(hkey));
+    uint32_t bu, bd;
+    bin_prefix(lbw, b, tag, s_cnt2[0], s_cnt2[1], wsum, bu, bd, counts, err);
+    const uint32_t u = s_cnt2[0] + s_cnt2[1];
+    for (uint32_t o = (uint32_t)t; o < u; o += kIT) {
+      const uint32_t r = lrank[start + o];
+      const uint64_t k = keys1[start + o];
+      if (r & 0x80000000u) {
+        dk[bd + (r & 0x7FFFFFFFu)] = k;
+      } else {
+        uk[bu + r] = k;
+        uv[bu + r] = vals[pay1[start + o]];
+      }
+    }
     return;
   }
   // a. last writer per key
@@ -405,19 +488,21 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     __syncthreads();
     lds_bitonic<kUniqSlots / kIT>(reinterpret_cast<uint64_t*>(hkey), hidx, m);
   }
-  // d. classify and rank: thread t owns survivors [E t, E t + E)
+  // d. classify and rank: thread t owns survivors [E t, E t + E); then the
+  // bin's place among the bins, and its survivors straight to uk / uv / dk
   constexpr int E = (kUniqCap + kIT - 1) / kIT;
   const uint32_t o0 = (uint32_t)(E * t);
   uint32_t isdel = 0, nloc = 0;  // bit r: survivor o0 + r is a delete
+  uint64_t ok[E], ov[E];
 #pragma unroll
   for (int r = 0; r < E; ++r) {
     const uint32_t o = o0 + (uint32_t)r;
+    ok[r] = 0;
+    ov[r] = 0;
     if (o < u) {
-      const uint64_t k = hkey[o];
-      const uint32_t ix = hidx[o];
-      keys1[start + o] = k;
-      pay1[start + o] = ix;
-      if (vals[ix] == kValueNull) isdel |= 1u << r;
+      ok[r] = hkey[o];
+      ov[r] = vals[hidx[o]];
+      if (ov[r] == kValueNull) isdel |= 1u << r;
       ++nloc;
     }
   }
@@ -425,75 +510,19 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   // one scan of (upserts << 16 | deletes): a bin holds <= 6144 survivors
   uint32_t tot;
   const uint32_t ex = block_scan(((nloc - ndl) << 16) | ndl, wsum, &tot);
-  uint32_t ru = ex >> 16, rd = ex & 0xFFFF;
+  uint32_t bu, bd;
+  bin_prefix(lbw, b, tag, tot >> 16, tot & 0xFFFF, wsum, bu, bd, counts, err);
+  uint32_t ru = bu + (ex >> 16), rd = bd + (ex & 0xFFFF);
 #pragma unroll
   for (int r = 0; r < E; ++r) {
     const uint32_t o = o0 + (uint32_t)r;
-    if (o < u) lrank[start + o] = (isdel >> r) & 1u ? (0x80000000u | rd++) : ru++;
-  }
-  if (t == 0) {
-    bcnt[2 * b] = tot >> 16;
-    bcnt[2 * b + 1] = tot & 0xFFFF;
-  }
-}
-
-// place every bin's survivors at its prefix over the earlier bins
-__global__ __launch_bounds__(256) void k_bin_emit(const uint64_t* __restrict__ keys1,
-                                                 const uint32_t* __restrict__ pay1,
-                                                 const uint32_t* __restrict__ lrank,
-                                                 const uint32_t* __restrict__ bins,
-                                                 const uint32_t* __restrict__ bcnt,
-                                                 const uint64_t* __restrict__ vals,
-                                                 uint64_t* __restrict__ uk,
-                                                 uint64_t* __restrict__ uv,
-                                                 uint64_t* __restrict__ dk,
-                                                 uint64_t* __restrict__ counts,
-                                                 const uint32_t* gate, uint32_t tag) {
-  __shared__ uint32_t su[4], sd[4];
-  const int t = threadIdx.x;
-  const uint32_t b = blockIdx.x;
-  if (*gate == tag) {  // kKeyMax in the chunk: nothing to apply
-    if (b == 0 && t == 0) counts[0] = counts[1] = 0;
-    return;
-  }
-  // prefix over bins < b (and the totals): thread t holds bin t
-  uint32_t cu = bcnt[2 * t], cd = bcnt[2 * t + 1];
-  uint32_t pu = (uint32_t)t < b ? cu : 0u, pd = (uint32_t)t < b ? cd : 0u;
-  for (int off = 32; off > 0; off >>= 1) {
-    pu += (uint32_t)__shfl_xor((int)pu, off);
-    pd += (uint32_t)__shfl_xor((int)pd, off);
-    cu += (uint32_t)__shfl_xor((int)cu, off);
-    cd += (uint32_t)__shfl_xor((int)cd, off);
-  }
-  if (lane_id() == 0) {
-    su[t >> 6] = pu;
-    sd[t >> 6] = pd;
-  }
-  __syncthreads();
-  const uint32_t bu = su[0] + su[1] + su[2] + su[3];
-  const uint32_t bd = sd[0] + sd[1] + sd[2] + sd[3];
-  if (b == gridDim.x - 1) {
-    __syncthreads();
-    if (lane_id() == 0) {
-      su[t >> 6] = cu;
-      sd[t >> 6] = cd;
-    }
-    __syncthreads();
-    if (t == 0) {
-      counts[0] = (uint64_t)su[0] + su[1] + su[2] + su[3];
-      counts[1] = (uint64_t)sd[0] + sd[1] + sd[2] + sd[3];
-    }
-  }
-  const uint32_t start = bins[2 * b];
-  const uint32_t u = bcnt[2 * b] + bcnt[2 * b + 1];
-  for (uint32_t o = (uint32_t)t; o < u; o += 256) {
-    const uint32_t r = lrank[start + o];
-    const uint64_t k = keys1[start + o];
-    if (r & 0x80000000u) {
-      dk[bd + (r & 0x7FFFFFFFu)] = k;
-    } else {
-      uk[bu + r] = k;
-      uv[bu + r] = vals[pay1[start + o]];
+    if (o < u) {
+      if ((isdel >> r) & 1u) {
+        dk[rd++] = ok[r];
+      } else {
+        uk[ru] = ok[r];
+        uv[ru++] = ov[r];
+      }
     }
   }
 }
@@ -510,16 +539,13 @@ void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uin
 }
 
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
-                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
+                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
-                       uint64_t* counts, uint32_t* S, const uint32_t* gate, uint32_t tag,
-                       hipStream_t s) {
+                       uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
+                       uint32_t tag, hipStream_t s) {
   const KeyRange kr{key_lo, key_bits};
   hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
-                     lrank, bcnt, kscr, iscr, S, gate, tag);
-  hipLaunchKernelGGL(k_bin_emit, dim3(kCoarse), dim3(256), 0, s, (const uint64_t*)keys1,
-                     (const uint32_t*)pay1, (const uint32_t*)lrank, bins,
-                     (const uint32_t*)bcnt, vals, uk, uv, dk, counts, gate, tag);
+                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag);
 }
 
 }  // namespace dev

@@ -190,7 +190,7 @@ void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* g
                              uint32_t* bins, hipStream_t s);
 // insert ordering (isort.hip).  Step 1: every 4096-op tile reduced to its
 // last writer per key (LDS hash table, atomic max of the op index); a kKeyMax
-// key rejects the chunk: gate = tag (k_bin_emit then emits nothing) and the
+// key rejects the chunk: gate = tag (k_bin_unique then emits nothing) and the
 // sticky error word gets kErrKeyMax.
 constexpr int kIsortTile = 4096;
 constexpr uint32_t kErrKeyMax = 1u << 31;
@@ -203,12 +203,13 @@ void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uin
 // steps 3-4: per-bin last-writer dedup + sort (bins of <= 6144 ops in LDS,
 // larger ones by an LSD radix sort through global scratch kscr / iscr, n
 // words each), then uk / uv / dk at the bins' prefixes and (upserts, deletes)
-// in counts[0..1]; bcnt = 2 x 256 words, lrank = one u32 per op
+// in counts[0..1]; lbw = kCoarse tagged count words (the bins' look-back),
+// lrank = one u32 per op (bins over 6144 ops)
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,
-                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint32_t* bcnt,
+                       uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
-                       uint64_t* counts, uint32_t* S, const uint32_t* gate, uint32_t tag,
-                       hipStream_t s);
+                       uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
+                       uint32_t tag, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);

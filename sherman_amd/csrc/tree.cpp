@@ -446,7 +446,7 @@ int drain_profile(shm_tree* t) {
 }
 
 // One insert chunk (n <= nmax ops), issued without a host wait:
-//   1. ordering: k_tile_dedup, coarse partition, k_bin_unique + k_bin_emit
+//   1. ordering: k_tile_dedup, coarse partition, k_bin_unique
 //      -> uk / uv (upserts, key order, last writer) and dk (deletes); counts
 //      stay on the device (d_counts[0..1]);
 //   2. k_locate: each upsert's leaf from the leaf directory (header walk);
@@ -468,8 +468,9 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
                                t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
   dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
-                         t->bins + 2 * dev::kCoarse, t->kb, t->ic, t->uk, t->uv, t->dk,
-                         t->d_counts, t->part_S, &t->ctl->gate, tag, s);
+                         reinterpret_cast<uint64_t*>(t->bins + 2 * dev::kCoarse), t->kb, t->ic,
+                         t->uk, t->uv, t->dk, t->d_counts, t->d_err, t->part_S, &t->ctl->gate,
+                         tag, s);
   DBG(s, "ordering");
   // leaves of the upserts
   if (use_leaf_dir(t)) {
@@ -869,7 +870,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
-  rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count), then (upserts, deletes)
+  rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count) per bin, then the bins' tagged counts
   // get workspaces: 0 shares the insert arrays, 1 is its own
   t->gws[0] = {t->kb, t->ka, t->ia, t->ib, t->part_hist, t->part_S, t->part_chunks};
   {
@@ -892,6 +893,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
       hipMemsetAsync(t->ctl, 0, sizeof(dev::UpperCtl), s) ||
+      hipMemsetAsync(t->bins, 0, sizeof(uint32_t) * 4 * dev::kCoarse, s) ||
       hipMemsetAsync(t->leaf_rd, 0, sizeof(uint32_t) * segcap, s) ||
       hipMemsetAsync(t->int_rd, 0, sizeof(uint32_t) * t->sep_cap, s) ||
       hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
