@@ -412,7 +412,7 @@ def main():
     q_per_launch = prof["queries"] / max(prof["calls"], 1)
     achieved = q_per_launch * ALG_BYTES_PER_GET / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
     traffic = None
-    if args.workload == "c2":
+    if args.workload == "c2" and args.start == "dir":
         traffic = _profile_traffic("pmc_walk.json", "hbm_bytes_per_launch", batch,
                                    args.keys_log2)
 
@@ -516,8 +516,9 @@ def main():
                 "range_ms_per_launch": round(range_ms, 4),
                 "walk_ms_per_launch": None, "order_ms_per_launch": None,
                 "queries_per_launch": None, "alg_bytes_per_get": None,
-                "traffic": _profile_traffic("pmc_insert.json", "hbm_bytes_per_chunk",
-                                            batch, args.keys_log2)})
+                "traffic": (_profile_traffic("pmc_insert.json", "hbm_bytes_per_chunk",
+                                             batch, args.keys_log2)
+                            if args.start == "dir" else None)})
         if args.workload == "c3":
             # whole-step algorithmic rate (gets 1040 B, inserts 1074 B per op)
             step_s = elapsed / args.steps
