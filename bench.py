@@ -58,7 +58,9 @@ N_BATCHES = 8                # distinct resident batches the steps cycle over
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=None,
+                   help="timed steps (default 200 for c2 / c3; 20 for c5, whose inserts "
+                        "grow the tree)")
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2")
     p.add_argument("--keys-log2", type=int, default=None,
@@ -98,7 +100,10 @@ def parse():
                    help="N > 1: route gets / inserts through the C-ABI shard (C++ over "
                         "RCCL, shm_shard_*) or the Python exchange; auto = the C-ABI on "
                         "the nccl backend once it matched the Python route on one batch")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.steps is None:
+        a.steps = 20 if a.workload == "c5" else 200
+    return a
 
 
 def log(*a):
