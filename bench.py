@@ -322,11 +322,11 @@ def main():
         del keys_local
 
         def step(i):
-            # the batch's gets, then its inserts, queued without a host wait
-            # (the status of every insert is checked after the timed steps)
+            # one mixed batch (shm_mixed_batch): the gets see the state before
+            # its inserts; queued without a host wait (the status of every
+            # insert is checked after the timed steps)
             gk, pk, pv = mixed[i % N_BATCHES]
-            tree.search_batch(gk, vals[:gk.numel()], found[:gk.numel()])
-            tree.insert_batch_async(pk, pv)
+            tree.mixed_batch(gk, vals[:gk.numel()], found[:gk.numel()], pk, pv)
 
     # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
     cpu = parity = None

@@ -17,6 +17,8 @@
  *   shm_search_batch    Tree::search(const Key&, Value&)  include/Tree.h:49-50, src/Tree.cpp:405-459
  *   shm_insert_batch    Tree::insert(const Key&, const Value&)
  *   shm_insert_batch_async                                include/Tree.h:47-48, src/Tree.cpp:353-403
+ *   shm_mixed_batch     Tree::search + Tree::insert of one mixed op stream
+ *                       (test/benchmark.cpp:165-188)
  *   shm_del_batch       Tree::del(const Key&)             include/Tree.h:51,   src/Tree.cpp:542-591
  *   shm_range_query     Tree::range_query(from, to, Value*)
  *                                                         include/Tree.h:53-54, src/Tree.cpp:461-540
@@ -41,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 4
+#define SHM_ABI_VERSION 5
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -131,6 +133,14 @@ int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
  * handle (shm_synchronize, shm_insert_batch, shm_del_batch) as above. */
 int shm_insert_batch_async(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
                            uint64_t n, void *stream);
+/* One mixed batch of gets and inserts (the reference benchmark's op stream,
+ * test/benchmark.cpp:165-188, cut into batches): the gets see the tree as it
+ * was before the batch's inserts, the inserts apply as shm_insert_batch_async
+ * (the batch's status is reported by the next synchronising call).  Device
+ * pointers; found_out nullable. */
+int shm_mixed_batch(shm_tree *t, const uint64_t *get_keys, uint64_t n_get, uint64_t *vals_out,
+                    uint8_t *found_out, const uint64_t *ins_keys, const uint64_t *ins_vals,
+                    uint64_t n_ins, void *stream);
 /* Tree::del for every key. */
 int shm_del_batch(shm_tree *t, const uint64_t *keys, uint64_t n, void *stream);
 /* Batched inclusive range scans [from[i], to[i]]: values of valid entries in

@@ -94,7 +94,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 4  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 5  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -106,6 +106,7 @@ _SIGNATURES = [
     ("shm_search_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
     ("shm_insert_batch", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_insert_batch_async", ctypes.c_int, [vp, vp, vp, u64, vp]),
+    ("shm_mixed_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp, vp, u64, vp]),
     ("shm_del_batch", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
     ("shm_range_query_batch", ctypes.c_int,
@@ -290,6 +291,14 @@ class Tree:
         raised by the next synchronising call (synchronize, insert_batch)."""
         _check(lib().shm_insert_batch_async(self.h, _ptr(keys), _ptr(vals), keys.numel(),
                                             _stream_ptr(stream)), "insert_batch_async")
+
+    def mixed_batch(self, get_keys, vals_out, found_out, ins_keys, ins_vals, stream=None):
+        """One mixed batch (shm_mixed_batch): the gets see the tree before the
+        batch's inserts; the inserts are queued as insert_batch_async."""
+        _check(lib().shm_mixed_batch(self.h, _ptr(get_keys), get_keys.numel(), _ptr(vals_out),
+                                     _ptr(found_out) if found_out is not None else None,
+                                     _ptr(ins_keys), _ptr(ins_vals), ins_keys.numel(),
+                                     _stream_ptr(stream)), "mixed_batch")
 
     def del_batch(self, keys, stream=None):
         _check(lib().shm_del_batch(self.h, _ptr(keys), keys.numel(),

@@ -2,12 +2,17 @@
 // (include/Tree.h:42-63) over the C-ABI (include/sherman_amd.h).
 //
 //   Reference                                   Here
-//   Tree(DSM*, uint16_t tree_id)                Tree(const shm_config&)
-//   void insert(const Key&, const Value&, ...)  insert(k, v)
-//   bool search(const Key&, Value&, ...)        search(k, v)
-//   void del(const Key&, ...)                   del(k)
-//   uint64_t range_query(from, to, Value* buf)  range_query(from, to, buf)
-//   (new) batched forms on device pointers      search_batch / insert_batch
+//   Tree(DSM*, uint16_t tree_id)                Tree(const shm_config&, uint16_t tree_id = 0)
+//   void insert(const Key&, const Value&, ...)  insert(k, v[, cxt, coro_id])
+//   bool search(const Key&, Value&, ...)        search(k, v[, cxt, coro_id])
+//   void del(const Key&, ...)                   del(k[, cxt, coro_id])
+//   uint64_t range_query(from, to, Value* buf)  range_query(from, to, buf[, cxt, coro_id])
+//   void print_and_check_tree(...)              print_and_check_tree([cxt, coro_id])
+//   (new) batched forms on device pointers      search_batch / insert_batch / mixed_batch
+//
+// The coroutine arguments are accepted and ignored, so call sites of the
+// reference's coroutine path (src/Tree.cpp:1088-1093) compile unchanged: a
+// GPU batch hides latency with occupancy, not with coroutines.
 //
 // Single ops are batches of one, staged through small device buffers; the
 // batched forms are the hot path.  Errors that the reference turns into
@@ -16,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -23,6 +29,10 @@
 #include "../../include/sherman_amd.h"
 
 namespace shm {
+
+// the reference's coroutine context (include/Common.h); only its pointer is
+// ever passed here
+struct CoroContext;
 
 using Key = uint64_t;    // include/Common.h:113
 using Value = uint64_t;  // include/Common.h:114
@@ -40,7 +50,7 @@ inline void check(int s, const char* what) {
 
 class Tree {
  public:
-  explicit Tree(const shm_config& cfg) {
+  explicit Tree(const shm_config& cfg, uint16_t tree_id = 0) : tree_id(tree_id) {
     check(shm_tree_create(&cfg, &t_), "shm_tree_create");
     if (hipSetDevice(cfg.device) != hipSuccess ||
         hipMalloc(&d_keys_, 2 * sizeof(uint64_t)) != hipSuccess ||
@@ -65,12 +75,16 @@ class Tree {
   Tree& operator=(const Tree&) = delete;
 
   // Tree::insert (Tree.cpp:353-403); v == kValueNull deletes
-  void insert(const Key& k, const Value& v) {
+  void insert(const Key& k, const Value& v, CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
     stage(k, &v);
     check(shm_insert_batch(t_, d_keys_, d_vals_, 1, nullptr), "insert");
   }
   // Tree::search (Tree.cpp:405-459)
-  bool search(const Key& k, Value& v) {
+  bool search(const Key& k, Value& v, CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
     stage(k, nullptr);
     check(shm_search_batch(t_, d_keys_, 1, d_vals_, d_found_, nullptr), "search");
     uint8_t f = 0;
@@ -80,13 +94,18 @@ class Tree {
     return f != 0;
   }
   // Tree::del (Tree.cpp:542-591)
-  void del(const Key& k) {
+  void del(const Key& k, CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
     stage(k, nullptr);
     check(shm_del_batch(t_, d_keys_, 1, nullptr), "del");
   }
   // Tree::range_query (Tree.cpp:461-540), intended semantics: values of
   // [from, to] in leaf then slot order; `buffer` must hold every match.
-  uint64_t range_query(const Key& from, const Key& to, Value* buffer) {
+  uint64_t range_query(const Key& from, const Key& to, Value* buffer,
+                       CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
     uint64_t h[2] = {from, to};
     uint64_t *d_from = d_keys_, *d_to = d_keys_ + 1, *d_cnt = d_vals_;
     if (hipMemcpy(d_keys_, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess)
@@ -121,11 +140,29 @@ class Tree {
                     hipStream_t s = nullptr) {
     check(shm_insert_batch(t_, d_keys, d_vals, n, s), "insert_batch");
   }
+  // one mixed batch: the gets see the tree before the batch's inserts
+  void mixed_batch(const Key* d_get, uint64_t n_get, Value* d_vals, uint8_t* d_found,
+                   const Key* d_ins, const Value* d_ins_vals, uint64_t n_ins,
+                   hipStream_t s = nullptr) {
+    check(shm_mixed_batch(t_, d_get, n_get, d_vals, d_found, d_ins, d_ins_vals, n_ins, s),
+          "mixed_batch");
+  }
 
   // Tree::print_and_check_tree (Tree.cpp:151-203) -> structural check
   void check_tree(uint64_t* leaves = nullptr, uint64_t* internal = nullptr,
                   uint64_t* keys = nullptr) {
     check(shm_check(t_, leaves, internal, keys), "check");
+  }
+  // the reference's name: checks the tree and prints its shape
+  void print_and_check_tree(CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
+    uint64_t leaves = 0, internal = 0, keys = 0;
+    check_tree(&leaves, &internal, &keys);
+    const shm_stats_t st = stats();
+    printf("tree %u: height %u, %llu leaves, %llu internal pages, %llu keys\n",
+           (unsigned)tree_id, st.height, (unsigned long long)leaves,
+           (unsigned long long)internal, (unsigned long long)keys);
   }
   shm_stats_t stats() {
     shm_stats_t s;
@@ -133,6 +170,8 @@ class Tree {
     return s;
   }
   shm_tree* handle() { return t_; }
+
+  const uint64_t tree_id;  // include/Tree.h:67 (one tree per handle here)
 
  private:
   void stage(const Key& k, const Value* v) {

@@ -454,15 +454,9 @@ int drain_profile(shm_tree* t) {
 //   4. k_leaf_upsert_pipe: in-place upserts, splits flagged and counted;
 //   5. k_upper: leaf splits, parent levels, root growth, unlocks, the
 //      chunk's deletes, superblock.
-int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
-                 uint64_t n) {
-  const uint32_t tag = ++t->chunks;
-  const uint64_t lock_tag = (uint64_t)tag << 32;
-  shm_tree::ProfRec pr{};
-  if (t->prof_on) {
-    const int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
-    if (rc) return rc;
-  }
+// step 1: it reads only the batch and writes the insert workspace
+int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
+                 uint64_t n, uint32_t tag) {
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
                          t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S, s);
   dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
@@ -472,11 +466,13 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                          t->uk, t->uv, t->dk, t->d_counts, t->d_err, t->part_S, &t->ctl->gate,
                          tag, s);
   DBG(s, "ordering");
-  // leaves of the upserts
-  if (use_leaf_dir(t)) {
-    const int rc = refresh_dir(t, s);
-    if (rc) return rc;
-  }
+  return SHM_OK;
+}
+
+// steps 2-5 on the ordered chunk of tag (the leaf directory is current)
+int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
+                 shm_tree::ProfRec& pr) {
+  const uint64_t lock_tag = (uint64_t)tag << 32;
   dev::WalkArgs w = walk_args(t);
   w.keys = t->uk;
   w.n = n;
@@ -568,6 +564,23 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
     t->prof_pending.push_back(pr);
   }
   return SHM_OK;
+}
+
+int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
+                 uint64_t n) {
+  const uint32_t tag = ++t->chunks;
+  shm_tree::ProfRec pr{};
+  if (t->prof_on) {
+    const int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
+    if (rc) return rc;
+  }
+  if (const int rc = insert_order(t, s, keys, vals, n, tag)) return rc;
+  // leaves of the upserts
+  if (use_leaf_dir(t)) {
+    const int rc = refresh_dir(t, s);
+    if (rc) return rc;
+  }
+  return insert_apply(t, s, n, tag, pr);
 }
 
 // every chunk of one insert call, in order
@@ -925,24 +938,33 @@ int shm_tree_destroy(shm_tree* t) {
   return SHM_OK;
 }
 
+// The batched get on s under ord (the leaf directory is current).
+static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* keys,
+                       uint64_t n, uint64_t* vals_out, uint8_t* found_out);
+
 int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
                      uint64_t* vals_out, uint8_t* found_out, void* stream) {
   if (!t || (n && (!keys || !vals_out))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(stream);
   mirror(t);
-  // Ordering pays when queries share leaves: a batch of q uniform queries
-  // over L leaves reads L(1 - e^(-q/L)) of them sorted, q unsorted (C2, q/L
-  // 0.58: 24 % fewer page reads for ~35 us of partition + gather, +4 %; C3's
-  // get half, q/L 0.29: 13 % fewer, -3 %).  Auto mode orders at q/L >= 0.4.
-  const bool dense = (t->cfg.flags & SHM_FLAG_AUTO_SORT_GETS) && 5 * n >= 2 * t->next_page;
-  const bool ordered = ((t->cfg.flags & SHM_FLAG_SORT_GETS) || dense) && n >= kSortMinGets;
   Order ord(t, s, false);
   if (use_leaf_dir(t)) {
     if (dir_stale(t)) ord.make_exclusive();  // the rebuild rewrites what searches read
     const int rc = ord.rc ? ord.rc : refresh_dir(t, s);
     if (rc) return rc;
   }
+  return search_impl(t, s, ord, keys, n, vals_out, found_out);
+}
+
+static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* keys,
+                       uint64_t n, uint64_t* vals_out, uint8_t* found_out) {
+  // Ordering pays when queries share leaves: a batch of q uniform queries
+  // over L leaves reads L(1 - e^(-q/L)) of them sorted, q unsorted (C2, q/L
+  // 0.58: 24 % fewer page reads for ~35 us of partition + gather, +4 %; C3's
+  // get half, q/L 0.29: 13 % fewer, -3 %).  Auto mode orders at q/L >= 0.4.
+  const bool dense = (t->cfg.flags & SHM_FLAG_AUTO_SORT_GETS) && 5 * n >= 2 * t->next_page;
+  const bool ordered = ((t->cfg.flags & SHM_FLAG_SORT_GETS) || dense) && n >= kSortMinGets;
   for (uint64_t off = 0; off < n; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
     dev::WalkArgs a = walk_args(t);
@@ -1000,6 +1022,31 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   }
   HIP_OK(hipGetLastError());
   return SHM_OK;
+}
+
+int shm_mixed_batch(shm_tree* t, const uint64_t* get_keys, uint64_t n_get, uint64_t* vals_out,
+                    uint8_t* found_out, const uint64_t* ins_keys, const uint64_t* ins_vals,
+                    uint64_t n_ins, void* stream) {
+  if (!t || (n_get && (!get_keys || !vals_out)) || (n_ins && (!ins_keys || !ins_vals)))
+    return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(stream);
+  mirror(t);
+  Order ord(t, s, true);
+  if (ord.rc) return ord.rc;
+  if (use_leaf_dir(t)) {
+    const int rc = refresh_dir(t, s);
+    if (rc) return rc;
+  }
+  // the gets, then the inserts, on s.  (Running the inserts' ordering on a
+  // second stream beside the walk was measured: the walk's blocks hold every
+  // CU, the ordering kernels ran in its tail anyway and the join cost
+  // ~10 us; C3 4125 vs 4160-4188 Mops/s.)
+  int rc = search_impl(t, s, ord, get_keys, n_get, vals_out, found_out);
+  for (uint64_t off = 0; off < n_ins && rc == SHM_OK; off += t->nmax)
+    rc = insert_chunk(t, s, ins_keys + off, ins_vals + off, std::min(t->nmax, n_ins - off));
+  if (rc == SHM_OK && n_ins) t->batches += 1;
+  return rc;
 }
 
 int shm_insert_batch(shm_tree* t, const uint64_t* keys, const uint64_t* vals,

@@ -20,8 +20,9 @@ int main() {
   shm_config cfg = shm::Tree::default_config();
   cfg.arena_bytes = 64ull << 20;
   cfg.max_batch = 1 << 14;
-  shm::Tree tree(cfg);
+  shm::Tree tree(cfg, /*tree_id=*/0);
   shm::Value v;
+  shm::CoroContext* cxt = nullptr;  // the reference's coroutine arguments compile too
   const uint64_t N = 10240;
   for (uint64_t i = 1; i < N; ++i) tree.insert(i, i * 2);
   for (uint64_t i = N - 1; i >= 1; --i) tree.insert(i, i * 3);
@@ -29,7 +30,7 @@ int main() {
     bool res = tree.search(i, v);
     CHECK(res && v == i * 3);
   }
-  for (uint64_t i = 1; i < N; ++i) tree.del(i);
+  for (uint64_t i = 1; i < N; ++i) tree.del(i, cxt, 0);
   for (uint64_t i = 1; i < N; ++i) CHECK(!tree.search(i, v));
   for (uint64_t i = N - 1; i >= 1; --i) tree.insert(i, i * 3);
   for (uint64_t i = 1; i < N; ++i) {
@@ -45,6 +46,7 @@ int main() {
   uint64_t leaves = 0, internal = 0, keys = 0;
   tree.check_tree(&leaves, &internal, &keys);
   CHECK(keys == N - 1);
+  tree.print_and_check_tree(cxt, 0);
   std::printf("tree_test ok: %lu keys, %lu leaves, %lu internal pages, height %u\n",
               (unsigned long)keys, (unsigned long)leaves, (unsigned long)internal,
               tree.stats().height);

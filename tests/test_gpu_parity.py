@@ -481,6 +481,41 @@ def test_mixed_zipf_batches_vs_oracle(lib_ok, sort_gets):
     t.close()
 
 
+@pytest.mark.parametrize("sort_gets", [False, True])
+def test_mixed_batch_gets_see_state_before_its_inserts(lib_ok, sort_gets):
+    """shm_mixed_batch (the C3 step): every get returns the oracle's value
+    BEFORE the batch's inserts, including keys the same batch overwrites,
+    inserts, deletes or never had; the inserts (zipf duplicates, new keys
+    that split leaves, value-0 deletes) then leave the oracle's contents."""
+    n_items, batch = 1 << 16, 1 << 14
+    t = shm.Tree(arena_bytes=128 << 20, max_batch=1 << 15, sort_gets=sort_gets)
+    orc = OracleTree(128 << 20)
+    pre = hashed_keys(1, n_items + 1)
+    pv = np.arange(1, n_items + 1, dtype=U64) * U64(2)
+    gpu_insert(t, pre, pv)
+    orc.apply_batch(pre, pv)
+    splits0 = t.stats()["splits"]
+    for b in range(4):
+        ids = zipf_fill(2 * n_items, 0.99, 0x5EED1000 + b, batch) + U64(1)
+        keys = np.array([to_key(int(i)) for i in ids], dtype=U64)
+        is_get = op_mix(b + 7, 50, batch).astype(bool)
+        op_val = np.arange(b * batch, (b + 1) * batch, dtype=U64) + U64(1)
+        op_val[::97] = 0  # deletes
+        gk, pk, pval = keys[is_get], keys[~is_get], op_val[~is_get]
+        gk = np.concatenate([gk, pk[:512]])  # keys this batch writes
+        ov, of = orc.search_batch(gk)
+        k = dev(gk)
+        v = torch.empty_like(k)
+        f = torch.empty(k.numel(), dtype=torch.uint8, device=k.device)
+        t.mixed_batch(k, v, f, dev(pk), dev(pval))
+        t.synchronize()
+        assert_same(gk, ov, of, host(v), f.cpu().numpy())
+        orc.apply_batch(pk, pval)
+    assert t.stats()["splits"] > splits0, "no leaf split in the mixed stream"
+    compare_contents(t, orc)
+    t.close()
+
+
 def test_leaf_dir_stale_after_splits(lib_ok):
     """The get path starts from the leaf directory (leafdir.hip), built at the
     first search and rebuilt only after the tree grew by 1/32.  Inserts that
