@@ -49,7 +49,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ALG_BYTES_PER_GET = 1040     # 1024 B leaf + 8 B key + 8 B value
+ALG_BYTES_PER_GET = 1040     # 1024 B leaf + 8 B key + 8 B value: the page walk
+# the summary walk (default): three random 128 B HBM lines (directory entry,
+# leaf summary, the matching entry) + 8 B key + 8 B value
+ALG_BYTES_PER_GET_SUM = 3 * 128 + 16
 ALG_BYTES_PER_INSERT = 1074  # 1024 B leaf + 18 B entry + 16 B k/v + 16 B lock
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 N_BATCHES = 8                # distinct resident batches the steps cycle over
@@ -76,8 +79,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline sample length (C1: >= 5 two-second windows)")
     p.add_argument("--sort", choices=("auto", "on", "off"), default="auto",
-                   help="order get batches by key before the walk: always "
-                        "(SHM_FLAG_SORT_GETS), never, or when dense (default)")
+                   help="on: order get batches by key and walk whole pages "
+                        "(SHM_FLAG_SORT_GETS, k_get); auto / off: the leaf-summary walk "
+                        "(k_get_sum, default)")
     p.add_argument("--sync-scans", dest="async_scans", action="store_false",
                    help="c5, N=1: range scans read their total back before the "
                         "batch's inserts are queued (default: async, checked after)")
@@ -415,11 +419,13 @@ def main():
     range_ms = prof["range_ms"] / max(prof["range_calls"], 1)
     order_ms = prof["order_ms"] / max(prof["calls"], 1)
     q_per_launch = prof["queries"] / max(prof["calls"], 1)
-    achieved = q_per_launch * ALG_BYTES_PER_GET / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
+    page_walk = args.sort == "on"  # SHM_FLAG_SORT_GETS: ordered, whole pages (k_get)
+    bpg = ALG_BYTES_PER_GET if page_walk else ALG_BYTES_PER_GET_SUM
+    achieved = q_per_launch * bpg / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
     traffic = None
     if args.workload == "c2" and args.start == "dir":
         traffic = _profile_traffic("pmc_walk.json", "hbm_bytes_per_launch", batch,
-                                   args.keys_log2)
+                                   args.keys_log2, "k_get<" if page_walk else "k_get_sum")
 
     if rank == 0:
         if args.workload == "c2":
@@ -485,8 +491,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_get<4,1,4>",
-                "alg_bytes_per_get": ALG_BYTES_PER_GET,
+                "kernel": "k_get<4,1,4>" if page_walk else "k_get_sum",
+                "alg_bytes_per_get": bpg,
+                # the reference's per-get bytes (a whole 1 KB leaf)
+                # over the same walk time: what reading the page would need
+                "reference_bytes_per_get": ALG_BYTES_PER_GET,
+                "reference_bytes_GBps": round(q_per_launch * ALG_BYTES_PER_GET /
+                                              (walk_ms * 1e-3) / 1e9, 1) if walk_ms else None,
                 "walk_ms_per_launch": round(walk_ms, 4),
                 "order_ms_per_launch": round(order_ms, 4),
                 "queries_per_launch": int(q_per_launch),
@@ -525,10 +536,10 @@ def main():
                                              batch, args.keys_log2)
                             if args.start == "dir" else None)})
         if args.workload == "c3":
-            # whole-step algorithmic rate (gets 1040 B, inserts 1074 B per op)
+            # whole-step algorithmic rate (gets as walked, inserts 1074 B per op)
             step_s = elapsed / args.steps
             b0 = mixed[0]
-            alg = (b0[0].numel() * ALG_BYTES_PER_GET + b0[1].numel() * ALG_BYTES_PER_INSERT)
+            alg = (b0[0].numel() * bpg + b0[1].numel() * ALG_BYTES_PER_INSERT)
             out["roofline"]["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
             out["roofline"]["step_frac"] = round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4)
         print(json.dumps(out), flush=True)
@@ -538,13 +549,15 @@ def main():
     tree.close()
 
 
-def _profile_traffic(name, field, batch, keys_log2):
+def _profile_traffic(name, field, batch, keys_log2, kernel=None):
     """HBM bytes per launch measured by the committed PMC passes
     (profiles/<name>, tools/refresh_profiles.py) when they were taken at this
-    batch and key count, else None."""
+    batch and key count (and of this kernel), else None."""
     try:
         pmc = json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
+        return None
+    if kernel and kernel not in pmc.get("kernel", ""):
         return None
     if pmc.get("batch") == batch and pmc.get("keys_log2") == keys_log2:
         return pmc.get(field)

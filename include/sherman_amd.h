@@ -55,12 +55,14 @@ extern "C" {
 #define SHM_ENOSPC (-28)   /* output buffer too small (size reported) */
 
 /* flags for shm_config.flags */
-#define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key before the walk */
+#define SHM_FLAG_SORT_GETS 0x1u  /* reorder gets by key and walk whole pages
+                                    (k_get) instead of the leaf summaries */
 #define SHM_FLAG_LEAF_DIR 0x2u   /* start gets / leaf locates at the leaf
                                     directory (default on) */
-#define SHM_FLAG_AUTO_SORT_GETS 0x4u /* reorder a get batch by key when it is
-                                    dense enough that queries share leaves
-                                    (>= 0.4 queries per page; default on) */
+#define SHM_FLAG_AUTO_SORT_GETS 0x4u /* accepted; since ABI 5 no batch is
+                                    reordered unless SHM_FLAG_SORT_GETS: the
+                                    leaf-summary walk reads ~3 lines per get
+                                    and ordering never pays */
 
 typedef struct shm_tree shm_tree;
 

@@ -280,5 +280,20 @@ __device__ __forceinline__ uint64_t lower_bound64(const uint64_t* a,
   return lo;
 }
 
+// A leaf's summary line (layout.h) from one wave: lane s < 54 gives slot
+// s's fingerprint (0 = empty), lane 0 the fences; the tag byte last.
+__device__ __forceinline__ void put_leaf_sum(uint8_t* sum, uint64_t page_off, uint64_t highest,
+                                             uint64_t sibling, uint32_t fp) {
+  if (!sum) return;
+  uint8_t* line = sum + (page_off >> 10) * kSumBytes;
+  const int lane = lane_id();
+  if (lane < kLeafCardinality) line[kSumOffFp + lane] = (uint8_t)fp;
+  if (lane == 0) {
+    *reinterpret_cast<uint64_t*>(line + kSumOffHighest) = highest;
+    *reinterpret_cast<uint64_t*>(line + kSumOffSibling) = sibling;
+    line[0] = kSumLeaf;
+  }
+}
+
 }  // namespace dev
 }  // namespace shm

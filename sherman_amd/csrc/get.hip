@@ -297,6 +297,209 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
   }
 }
 
+// ---- the summary walk: lane = query ------------------------------------------
+//
+// Per get, three HBM lines instead of a 1 KB page: the leaf-directory entry,
+// the leaf's summary line (layout.h: fences, one fingerprint byte per slot)
+// and the entries whose fingerprint matches (false positives ~ 53 / 255).
+// A stale directory is fixed by turning right on k >= highest from the
+// summary (B-link).  Pages without a summary (internal pages: a directory
+// miss, or no directory) are walked from their own bytes, lane by lane:
+// check_consistent, fences, binary search of the records (Tree.cpp:593-685).
+// The leaf search keeps Tree.cpp:687-697: the first slot (in slot order) with
+// key == k, value != 0 and f == r.  Batches are serialised against inserts
+// by the call order, so a page is never torn under a get; the entry-level
+// f == r check stays.
+
+namespace {
+
+// leaf entry s of a page (18 B at 44 + 18 s, 2-byte aligned)
+__device__ __forceinline__ void lane_entry(const uint8_t* page, int s, uint64_t& key,
+                                           uint64_t& val, uint32_t& f, uint32_t& r) {
+  const uint32_t off = (uint32_t)(kOffRecords + kLeafEntry * s);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(page + (off & ~3u));
+  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+  const uint32_t sh = off & 3u;  // 0 or 2
+  const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  const uint32_t q3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  const uint32_t q4 = d4 >> (8 * sh);
+  f = q0 & 0xFF;
+  key = (uint64_t)((q0 >> 8) | (q1 << 24)) | ((uint64_t)((q1 >> 8) | (q2 << 24)) << 32);
+  val = (uint64_t)((q2 >> 8) | (q3 << 24)) | ((uint64_t)((q3 >> 8) | (q4 << 24)) << 32);
+  r = (q4 >> 8) & 0xFF;
+}
+
+__device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f, uint32_t r,
+                                          uint64_t k) {
+  return key == k && val != kValueNull && ((f ^ r) & 0xF) == 0;
+}
+
+// 4 bits: the bytes of x equal to the fingerprint pattern fq
+__device__ __forceinline__ uint32_t fp_bytes(uint32_t x, uint32_t fq) {
+  const uint32_t y = x ^ fq;
+  const uint32_t z = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y)) & 0x80808080u;
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+}  // namespace
+
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t k = a.keys[i];
+  uint64_t val = 0;
+  uint32_t err = 0;
+  if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
+    uint64_t ptr = a.root;
+    if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+    int retries = 0;
+    for (int hop = 0;; ++hop) {
+      if (hop > kMaxRounds) {
+        err |= kErrRounds;
+        break;
+      }
+      if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
+        err |= kErrBadPtr;
+        break;
+      }
+      const uint64_t off = ga_offset(ptr);
+      const uint8_t* page = a.arena + off;
+      const u32x4* line = reinterpret_cast<const u32x4*>(a.sum + (off >> 10) * kSumBytes);
+      const u32x4 l0 = line[0];
+      if ((l0.x & 0xFF) == kSumLeaf) {
+        const u32x4 l1 = line[1], l2 = line[2], l3 = line[3], l4 = line[4];
+        const uint64_t highest = (uint64_t)l0.z | ((uint64_t)l0.w << 32);
+        const uint64_t sibling = (uint64_t)l1.x | ((uint64_t)l1.y << 32);
+        if (k >= highest) {  // turn right (Tree.cpp:626-629)
+          if (!sibling) {
+            err |= kErrFence;
+            break;
+          }
+          ptr = sibling;
+          continue;
+        }
+        const uint32_t fq = key_fp(k) * 0x01010101u;
+        const uint32_t dw[14] = {l1.z, l1.w, l2.x, l2.y, l2.z, l2.w, l3.x,
+                                 l3.y, l3.z, l3.w, l4.x, l4.y, l4.z, l4.w};
+        uint64_t cand = 0;
+#pragma unroll
+        for (int d = 0; d < 14; ++d) cand |= (uint64_t)fp_bytes(dw[d], fq) << (4 * d);
+        cand &= (1ull << kLeafCardinality) - 1;
+        while (cand) {
+          uint64_t ek, ev;
+          uint32_t ef, er;
+          lane_entry(page, ctz64(cand), ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            break;
+          }
+          cand &= cand - 1;
+        }
+        break;
+      }
+      // no summary: the page's own bytes
+      const u32x4* pw = reinterpret_cast<const u32x4*>(page);
+      const u32x4 A = pw[0], B = pw[1], C = pw[2];
+      const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
+                                ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
+      const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
+                               ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
+      const uint64_t lowest = (uint64_t)B.w | ((uint64_t)C.x << 32);
+      const uint64_t highest = (uint64_t)C.y | ((uint64_t)C.z << 32);
+      const int cnt = (int)(int16_t)(B.z >> 16) + 1;
+      const bool leaf = leftmost == 0;
+      const uint32_t* pd = reinterpret_cast<const uint32_t*>(page);
+      const uint32_t rver = (leaf ? pd[kOffLeafRear / 4] : pd[kOffInternalRear / 4]) & 0xFF;
+      if ((A.z & 0xFF) != rver) {  // torn page: read it again (Tree.cpp:616-618)
+        if (++retries > kMaxRetries) {
+          err |= kErrInconsistent;
+          break;
+        }
+        continue;
+      }
+      if (k >= highest && sibling) {
+        ptr = sibling;
+        continue;
+      }
+      if (k < lowest || k >= highest) {
+        err |= kErrFence;
+        break;
+      }
+      if (leaf) {  // every slot
+        for (int sl = 0; sl < kLeafCardinality; ++sl) {
+          uint64_t ek, ev;
+          uint32_t ef, er;
+          lane_entry(page, sl, ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            break;
+          }
+        }
+        break;
+      }
+      // internal_page_search (Tree.cpp:665-685): child = #keys <= k
+      int lo = 0, hi = cnt < kInternalCardinality ? cnt : kInternalCardinality;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t km = (uint64_t)pd[11 + 4 * mid] | ((uint64_t)pd[12 + 4 * mid] << 32);
+        if (km <= k)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      ptr = lo == 0 ? leftmost
+                    : ((uint64_t)pd[13 + 4 * (lo - 1)] | ((uint64_t)pd[14 + 4 * (lo - 1)] << 32));
+    }
+  }
+  if (err) atomicOr(a.err, err);
+  a.out_val[i] = val;
+  if (a.out_found) a.out_found[i] = val != kValueNull ? 1 : 0;
+}
+
+void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s) {
+  if (n == 0) return;
+  constexpr int TPB = 256;
+  hipLaunchKernelGGL(k_get_sum<TPB>, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, s, a);
+}
+
+// summaries of a loaded image: one wave per page
+__global__ __launch_bounds__(256) void k_sum_rebuild(const uint8_t* arena, uint64_t pages,
+                                                     uint8_t* sum) {
+  const uint64_t pg = 1 + ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
+  if (pg >= pages) return;  // wave-uniform
+  const int lane = lane_id();
+  const uint8_t* page = arena + pg * kPageSize;
+  const u32x4* pw = reinterpret_cast<const u32x4*>(page);
+  const u32x4 A = pw[0], B = pw[1], C = pw[2];
+  const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
+                            ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
+  const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
+                           ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
+  const uint64_t highest = (uint64_t)C.y | ((uint64_t)C.z << 32);
+  if (leftmost != 0) {  // internal page: no summary
+    if (lane == 0) sum[pg * kSumBytes] = 0;
+    return;
+  }
+  uint32_t fp = 0;
+  if (lane < kLeafCardinality) {
+    uint64_t ek, ev;
+    uint32_t ef, er;
+    lane_entry(page, lane, ek, ev, ef, er);
+    fp = ev != kValueNull ? key_fp(ek) : 0u;
+  }
+  put_leaf_sum(sum, pg * kPageSize, highest, sibling, fp);
+}
+
+void launch_sum_rebuild(const uint8_t* arena, uint64_t pages, uint8_t* sum, hipStream_t s) {
+  if (pages <= 1) return;
+  const uint64_t waves = pages - 1;
+  hipLaunchKernelGGL(k_sum_rebuild, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, arena,
+                     pages, sum);
+}
+
 // G = 4 pages per group, NB = 1 group buffer, 4 waves per block: 16 KB of
 // LDS per block, 24-28 waves per CU (deeper buffers lost
 // occupancy and measured 2-8 % slower)

@@ -194,6 +194,9 @@ __device__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h
   if (lane == 0) L.page[kOffLeafRear / 4] = fver;  // rear_version, byte 1016
   store_page(a.arena, ga_offset(s.dest), L.page);
   if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = (uint8_t)c;  // slots [0, c)
+  // every slot < c is valid (value != 0: deletes never reach a split page)
+  put_leaf_sum(a.sum, ga_offset(s.dest), highest, sibling,
+               (uint32_t)lane < c ? key_fp(key) : 0u);
   return lowest;
 }
 
@@ -256,6 +259,8 @@ __device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint3
   if (lane_id() == 0) L.page[kOffInternalRear / 4] = (old_fver + 1) & 0xFF;
   store_page(a.arena, ga_offset(a.root), L.page);
   if (a.leaf_hw && lane_id() == 0) a.leaf_hw[ga_offset(a.root) >> 10] = kLeafHwFull;
+  // the root page is internal now: its summary no longer describes a leaf
+  if (a.sum && lane_id() == 0) a.sum[(ga_offset(a.root) >> 10) * kSumBytes] = 0;
 }
 
 // The page of `level` whose fences hold k: header walk from the root with
@@ -518,6 +523,7 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
       const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
       put_leaf_entry(reinterpret_cast<uint32_t*>(a.arena + ga_offset(ptr)), lane, k, kValueNull,
                      (e.fraw & 0xF0) | f, (e.rraw & 0xF0) | f);
+      if (a.sum) a.sum[(ga_offset(ptr) >> 10) * kSumBytes + kSumOffFp + lane] = 0;  // empty
     }
     wave_lds_sync();
     break;
@@ -842,8 +848,15 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   }
   if (!ok) err |= kErrRounds;
   // the chunk's deletes, after every split (Tree::del, Tree.cpp:542-591):
-  // the keys are located afresh, so pages that moved right are followed
+  // the keys are located afresh, so pages that moved right are followed.
+  // The last level skipped its barrier; a delete's walk must not meet a page
+  // another block is still rewriting, so wait for every block first.
   const uint64_t n_del = *a.n_del;
+  if (ok && n_del > 0 && total > 0) {
+    stamp();
+    ok = grid_sync(ctl, nb, &s_flag);
+    if (!ok) err |= kErrRounds;
+  }
   for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
   stamp();
@@ -864,12 +877,13 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
 }
 
 // LeafPage() + set_consistent (Tree.cpp:47-52)
-__global__ void k_empty_leaf(uint8_t* arena, uint64_t off) {
+__global__ void k_empty_leaf(uint8_t* arena, uint64_t off, uint8_t* sum) {
   __shared__ __attribute__((aligned(16))) uint32_t lp[kPageDwords + 8];
   init_page_image(lp, 1, 0, 0, 0, -1, kKeyMin, kKeyMax);
   wave_lds_sync();
   if (lane_id() == 0) lp[kOffLeafRear / 4] = 1;
   store_page(arena, off, lp);
+  put_leaf_sum(sum, off, kKeyMax, 0, 0);
 }
 
 __global__ void k_write_superblock(uint8_t* arena, Superblock sb) {
@@ -897,8 +911,8 @@ void launch_upper(const UpperArgs& a, hipStream_t s) {
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s) {
   hipLaunchKernelGGL(k_write_superblock, dim3(1), dim3(kWave), 0, s, arena, sb);
 }
-void launch_empty_leaf(uint8_t* arena, uint64_t off, hipStream_t s) {
-  hipLaunchKernelGGL(k_empty_leaf, dim3(1), dim3(kWave), 0, s, arena, off);
+void launch_empty_leaf(uint8_t* arena, uint64_t off, uint8_t* sum, hipStream_t s) {
+  hipLaunchKernelGGL(k_empty_leaf, dim3(1), dim3(kWave), 0, s, arena, off, sum);
 }
 
 }  // namespace dev

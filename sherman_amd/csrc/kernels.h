@@ -39,10 +39,18 @@ struct WalkArgs {
   // stops after that slot; kLeafHwFull (internal pages, pages of a loaded
   // image) reads the whole page
   const uint8_t* leaf_hw;
+  // leaf summaries (layout.h kSumBytes per page; k_get_sum)
+  const uint8_t* sum;
 };
 
 // batched get walk with grouped page resolution (get.hip)
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
+// batched get over the leaf summaries, lane = query (get.hip): directory
+// entry, summary line, matching entries; results in input order
+void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s);
+// rebuild the summaries of pages [1, pages) from the page bytes (a loaded
+// image), one wave per page
+void launch_sum_rebuild(const uint8_t* arena, uint64_t pages, uint8_t* sum, hipStream_t s);
 // header-only descent, lane = op (locate.hip): out_page[i] = the page of
 // a.target_level holding keys[i]; starts at the leaf directory for level 0
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
@@ -93,8 +101,9 @@ struct SegArgs {
   // (k_upper releases them)
   const uint32_t* seg_lk;
   uint32_t* err;
-  // per-page occupancy bound kept by every leaf writer (see WalkArgs)
+  // per-page occupancy bound and leaf summary kept by every leaf writer
   uint8_t* leaf_hw;
+  uint8_t* sum;
   // split counts for k_upper: segment g adds to range g * up_nb / num_seg
   UpperCtl* ctl;
   uint32_t par;
@@ -109,6 +118,7 @@ struct UpperArgs {
   uint16_t node;
   uint64_t root;             // the root page (fixed: a root split relocates its left half)
   uint8_t* leaf_hw;
+  uint8_t* sum;              // leaf summaries (layout.h)
   uint64_t* locks;
   uint32_t num_locks;
   uint64_t tag;              // lock-word tag of this chunk
@@ -160,7 +170,7 @@ constexpr int kUpperStamps = 32;
 uint32_t upper_blocks();
 void launch_upper(const UpperArgs& a, hipStream_t s);
 
-void launch_empty_leaf(uint8_t* arena, uint64_t page_off, hipStream_t s);
+void launch_empty_leaf(uint8_t* arena, uint64_t page_off, uint8_t* sum, hipStream_t s);
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s);
 
 // ---- ordering (partition.hip, isort.hip) ------------------------------------

@@ -79,6 +79,7 @@ struct shm_tree {
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr, *seg_ver = nullptr;
   uint32_t* seg_lk = nullptr;  // lock words taken ahead per segment (k_seg_fill_scan)
   uint8_t* leaf_hw = nullptr;   // per-page occupancy bound (layout.h kLeafHwFull)
+  uint8_t* sum = nullptr;       // leaf summaries, kSumBytes per page (layout.h)
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
   uint32_t *spl_seg = nullptr, *spl_base = nullptr, *leaf_rd = nullptr;
@@ -250,6 +251,7 @@ dev::WalkArgs walk_args(shm_tree* t) {
   a.root = t->root;
   a.err = t->d_err;
   a.leaf_hw = t->leaf_hw;
+  a.sum = t->sum;
   return a;
 }
 
@@ -505,6 +507,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.seg_lk = t->seg_lk;
   a.err = t->d_err;
   a.leaf_hw = t->leaf_hw;
+  a.sum = t->sum;
   a.ctl = t->ctl;
   a.par = tag & 1u;
   a.up_nb = dev::upper_blocks();
@@ -517,6 +520,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.node = t->cfg.node_id;
   u.root = t->root;
   u.leaf_hw = t->leaf_hw;
+  u.sum = t->sum;
   u.locks = t->locks;
   u.num_locks = t->cfg.num_locks;
   u.tag = lock_tag;
@@ -614,7 +618,7 @@ void free_all(shm_tree* t) {
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->bsum); F(t->bsum64);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw);
+  F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw); F(t->sum);
   F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
@@ -862,6 +866,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->seg_ver, segcap);
   rc |= dalloc(&t->seg_lk, segcap);
   rc |= dalloc(&t->leaf_hw, t->cap_pages);
+  rc |= dalloc(&t->sum, t->cap_pages * kSumBytes);
   rc |= dalloc(&t->ctl, 1);
   rc |= dalloc(&t->spl_seg, segcap);
   rc |= dalloc(&t->spl_base, segcap);
@@ -912,12 +917,13 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->gws[1].S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->arena, 0, kPageSize, s) ||
-      hipMemsetAsync(t->leaf_hw, kLeafHwFull, t->cap_pages, s))
+      hipMemsetAsync(t->leaf_hw, kLeafHwFull, t->cap_pages, s) ||
+      hipMemsetAsync(t->sum, 0, t->cap_pages * kSumBytes, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
   t->next_page = 1;
   const uint64_t root_off = t->next_page * kPageSize;
-  dev::launch_empty_leaf(t->arena, root_off, s);
+  dev::launch_empty_leaf(t->arena, root_off, t->sum, s);
   t->next_page += 1;
   t->root = ga_make(cfg->node_id, root_off);
   t->root_level = 0;
@@ -959,12 +965,13 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
 
 static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* keys,
                        uint64_t n, uint64_t* vals_out, uint8_t* found_out) {
-  // Ordering pays when queries share leaves: a batch of q uniform queries
-  // over L leaves reads L(1 - e^(-q/L)) of them sorted, q unsorted (C2, q/L
-  // 0.58: 24 % fewer page reads for ~35 us of partition + gather, +4 %; C3's
-  // get half, q/L 0.29: 13 % fewer, -3 %).  Auto mode orders at q/L >= 0.4.
-  const bool dense = (t->cfg.flags & SHM_FLAG_AUTO_SORT_GETS) && 5 * n >= 2 * t->next_page;
-  const bool ordered = ((t->cfg.flags & SHM_FLAG_SORT_GETS) || dense) && n >= kSortMinGets;
+  // Unordered batches take the summary walk (k_get_sum: directory entry,
+  // summary line, matching entry: ~3 random lines per get).  Ordering the
+  // batch by key first (SHM_FLAG_SORT_GETS) feeds the page walk (k_get),
+  // which shares a leaf's 1 KB read among the queries that need it; at C2
+  // that is 6.3 G gets/s against 15.4 for the summary walk, so the auto mode
+  // no longer orders.
+  const bool ordered = (t->cfg.flags & SHM_FLAG_SORT_GETS) && n >= kSortMinGets;
   for (uint64_t off = 0; off < n; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
     dev::WalkArgs a = walk_args(t);
@@ -1002,12 +1009,15 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
       a.xcd_remap = 0;
     }
     // leaf DMA policy: an ordered walk reads each leaf once per batch, so
-    // non-temporal loads keep the directory in L2 (C2 +5 %); an unordered walk
-    // reads a leaf once per wave that needs it, and under skew (C3) the
-    // cached policy serves the repeats from L2
+    // non-temporal loads keep the directory in L2 (C2 +5 %)
     a.nt = gathered ? 1 : 0;
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
-    dev::launch_get(a, m, s);
+    // ordered: the page walk (k_get); unordered: the summary walk (k_get_sum,
+    // three lines per get)
+    if (gathered)
+      dev::launch_get(a, m, s);
+    else
+      dev::launch_get_sum(a, m, s);
     DBG(s, "walk(get)");
     if (t->prof_on) {
       HIP_OK(hipEventRecord(pr.e[2], s));
@@ -1270,6 +1280,10 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   HIP_OK(hipMemcpy(t->arena, host_buf, bytes, hipMemcpyHostToDevice));
   // occupancy unknown for the loaded pages: whole-page reads until rewritten
   HIP_OK(hipMemset(t->leaf_hw, kLeafHwFull, t->cap_pages));
+  // leaf summaries from the loaded pages
+  HIP_OK(hipMemset(t->sum, 0, t->cap_pages * kSumBytes));
+  dev::launch_sum_rebuild(t->arena, pages, t->sum, nullptr);
+  HIP_OK(hipDeviceSynchronize());
   t->root = root_ptr;
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;

@@ -165,10 +165,13 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   // ---- write back the changed entries of in-place segments -----------------------
   if (live && !over) {
     uint8_t* pg = a.arena + ga_offset(qpage);
+    uint8_t* fp = a.sum ? a.sum + (ga_offset(qpage) >> 10) * kSumBytes + kSumOffFp : nullptr;
 #pragma unroll
     for (int j = 0; j < E; ++j)
-      if (dirty[j])
+      if (dirty[j]) {
         put_leaf_entry(reinterpret_cast<uint32_t*>(pg), ebase + j, ek[j], ev[j], ef[j], er[j]);
+        if (fp) fp[ebase + j] = (uint8_t)key_fp(ek[j]);  // the leaf summary's slot
+      }
   }
   if (a.leaf_hw) {
     // the page's occupancy bound after the batch: 1 + its last valid slot
