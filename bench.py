@@ -405,10 +405,12 @@ def main():
         dist.all_reduce(lt, op=dist.ReduceOp.MAX)
         lat = lt.tolist()
 
-    # ---- roofline: k_walk timed with HIP events on its launch stream -------
+    # ---- roofline: the walk timed with HIP events on its launch stream.  C2
+    # runs these batches one at a time on one stream, so each launch's
+    # duration is the kernel's own (the timed steps overlap two walks) -----
     tree.profile(True)
     for i in range(args.profile_steps):
-        step(i)
+        (one if args.workload == "c2" else step)(i)
     torch.cuda.synchronize()
     prof = tree.profile_read(reset=True)
     tree.profile(False)
@@ -508,6 +510,9 @@ def main():
                                     if traffic and q_per_launch else None),
                 "traffic_GBps": (round(traffic / (walk_ms * 1e-3) / 1e9, 1)
                                  if traffic and walk_ms else None),
+                # the timed steps: two walks in flight, one batch per step
+                "step_alg_GBps": round(q_per_launch * bpg / (elapsed / args.steps) / 1e9, 1)
+                                 if args.workload == "c2" else None,
                 "full_path_bytes_per_get": 5136,
             },
             "cpu_baseline": cpu,
