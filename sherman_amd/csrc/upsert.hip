@@ -82,13 +82,14 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   uint64_t ek[E], ev[E];
   uint32_t ef[E], er[E];
   chunk_entries<E>(D, ek, ev, ef, er);
-  bool mine[E], valid[E], dirty[E];
+  bool mine[E], valid[E], dirty[E], fresh[E];  // fresh: a new key took the slot
   uint32_t cnt = 0;  // valid entries of slot q (the same in all its lanes)
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     mine[j] = ebase + j >= li * E;
     valid[j] = mine[j] && ev[j] != kValueNull;
     dirty[j] = false;
+    fresh[j] = false;
     cnt += (uint32_t)popc64((ballot(valid[j]) >> (q * L)) & kGroupMask);
   }
 
@@ -129,6 +130,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
       if (valid[j] && ek[j] == kq) hj = j;
     const uint64_t mh = (ballot(go && hj >= 0) >> (q * L)) & kGroupMask;
     bool take = false;
+    const bool isnew = go && !mh;
     int tj = -1;
     if (go && mh) {
       take = li == ctz64(mh);  // the valid slot holding the key
@@ -155,6 +157,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         er[j] = (er[j] & 0xF0) | f;
         valid[j] = true;
         dirty[j] = true;
+        fresh[j] = fresh[j] || isnew;
       }
     }
   }
@@ -170,7 +173,10 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     for (int j = 0; j < E; ++j)
       if (dirty[j]) {
         put_leaf_entry(reinterpret_cast<uint32_t*>(pg), ebase + j, ek[j], ev[j], ef[j], er[j]);
-        if (fp) fp[ebase + j] = (uint8_t)key_fp(ek[j]);  // the leaf summary's slot
+        // the leaf summary: an overwrite keeps its key's fingerprint; a new
+        // key in an empty slot sets it (one partial line write per page
+        // that gained keys, none for pure updates)
+        if (fp && fresh[j]) fp[ebase + j] = (uint8_t)key_fp(ek[j]);
       }
   }
   if (a.leaf_hw) {

@@ -16,7 +16,7 @@ import sys
 
 INSERT_KERNELS = ("k_tile_dedup", "k_part_coarse", "k_bin_", "k_locate", "k_seg_",
                   "k_leaf_", "k_upper")
-ANCHOR = {"c3": "k_get<", "c5": "k_range", "c2": "k_get<"}
+ANCHOR = {"c3": "k_get", "c5": "k_range", "c2": "k_get"}
 
 
 def steps_of(rows, anchor, per):
