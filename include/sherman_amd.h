@@ -241,9 +241,11 @@ int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *p
  * Rank r of P (P <= 16) owns keys [r * 2^64 / P, (r+1) * 2^64 / P) in its own
  * shm_tree (create it with key_lo / key_bits of that slice).  One process per
  * GPU; every rank makes the same calls in the same order (collectives).
- * A routed get: bucket by owner, exchange counts (ncclAllToAll), one host
- * read-back of the split sizes, keys out and values back (grouped
- * ncclSend / ncclRecv), local shm_search_batch, un-permute.  A routed insert:
+ * A routed get: bucket by owner, pack each peer's run into a fixed-size
+ * slot (1.25 n / P + 256 keys, kKeyMax padding), ncclAllToAll of the slots,
+ * local shm_search_batch, results back the same way, unpack; no host wait
+ * (every rank passes the same n; a run longer than its slot is reported as
+ * a device error at the tree's next synchronising call).  A routed insert:
  * the same exchange with the values, then shm_insert_batch_async on the
  * owner (rank-major batch order across ranks).  Device pointers; n <=
  * the local tree's max_batch. */
@@ -259,9 +261,10 @@ int shm_shard_destroy(shm_shard *s);
 /* vals_out / found_out in input order (Tree::search per key) */
 int shm_shard_search(shm_shard *s, const uint64_t *keys, uint64_t n, uint64_t *vals_out,
                      uint8_t *found_out, void *stream);
-/* the same in two halves for pipelining: begin = bucketing + count exchange
- * (no host wait), end = the rest.  Two batches may be begun at once (two
- * slots, each with its own communicator); end them in order. */
+/* the same in two halves for pipelining: begin = bucketing + the keys'
+ * exchange, end = local get + the results' exchange + unpack (neither waits
+ * for the device).  Two batches may be begun at once (two slots, each with
+ * its own communicator); end them in order. */
 int shm_shard_search_begin(shm_shard *s, const uint64_t *keys, uint64_t n, void *stream,
                            uint32_t *ticket);
 int shm_shard_search_end(shm_shard *s, uint32_t ticket, uint64_t *vals_out, uint8_t *found_out);

@@ -264,6 +264,14 @@ void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64
                     hipStream_t s);
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
                       uint64_t* out, uint8_t* found, hipStream_t s);
+// fixed-capacity exchange (shard.cpp): pack a bucketed batch into P runs of
+// cap slots (kKeyMax padding; a longer run sets kErrOverflow in *err), and
+// unpack P runs of results back to input order
+void launch_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P, uint64_t cap,
+                       uint64_t* out, uint32_t* err, hipStream_t s);
+void launch_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P, uint64_t cap,
+                         const uint32_t* perm, uint64_t n, uint64_t* out, uint8_t* found,
+                         hipStream_t s);
 
 // ---- batched range scans (range.hip) -------------------------------------------
 struct RangeArgs {

@@ -8,11 +8,16 @@
 // One exchange each way per batch, over RCCL (xGMI between the GPUs of a
 // node):
 //
-//   search : bucket keys by owner (stable, shm_route_bucket) -> ncclAllToAll
-//            of the P counts -> ONE read-back of both count vectors (the
-//            split sizes) -> grouped ncclSend / ncclRecv of the keys ->
-//            local batched get -> grouped send / recv of the values back ->
-//            un-permute (found = value != 0, Tree.cpp:445-448)
+//   search : bucket keys by owner (stable, shm_route_bucket) -> pack each
+//            peer's run into a fixed-capacity slot (cap = 1.25 n / P + 256,
+//            kKeyMax padding) -> ncclAllToAll of the slots -> local batched
+//            get over all received slots (a kKeyMax finds nothing) ->
+//            ncclAllToAll of the results back -> unpack to input order
+//            (found = value != 0, Tree.cpp:445-448).  No count exchange and no
+//            host wait: the whole routed get is queued on the stream.  A run
+//            longer than its slot (keys far from uniform over the shards) is
+//            cut and reported as kErrOverflow at the tree's next
+//            synchronising call.
 //   insert : the same bucketing, the values permuted alongside, keys and
 //            values exchanged, then a local insert queued without a host
 //            wait; received runs arrive in source-rank order and bucketing
@@ -34,6 +39,10 @@
 #include <vector>
 
 #include "../../include/sherman_amd.h"
+#include "kernels.h"
+
+// library-internal (tree.cpp): the tree's sticky device error word
+extern "C" uint32_t* shm__error_word(shm_tree* t);
 
 namespace {
 
@@ -48,6 +57,15 @@ struct Slot {
   uint64_t* rk = nullptr;     // received keys
   uint64_t* rv = nullptr;     // received insert values / local get results
   uint64_t* back = nullptr;   // results returned to this rank (bucketed order)
+  // fixed-capacity get exchange: P slots of up to pcap keys each way; a
+  // batch of n uses slots of ncap = min(pcap, 1.25 n / P + 256) (every rank
+  // passes the same n: the exchange is a collective)
+  uint64_t pcap = 0;
+  uint64_t ncap = 0;
+  uint64_t* pk = nullptr;     // packed keys to send
+  uint64_t* pr = nullptr;     // keys received
+  uint64_t* pv = nullptr;     // local results for them
+  uint64_t* pb = nullptr;     // results returned
   uint64_t cap = 0;           // send-side capacity (the local max_batch)
   uint64_t rcap = 0;          // receive-side capacity (grows)
   const uint64_t* keys = nullptr;
@@ -94,7 +112,8 @@ int dalloc(T** p, uint64_t count) {
 
 void free_slot(Slot& s, bool own) {
   for (void* p : {(void*)s.cnts, (void*)s.kb, (void*)s.vb, (void*)s.perm, (void*)s.rk,
-                  (void*)s.rv, (void*)s.back})
+                  (void*)s.rv, (void*)s.back, (void*)s.pk, (void*)s.pr, (void*)s.pv,
+                  (void*)s.pb})
     if (p) (void)hipFree(p);
   if (own && s.comm) (void)ncclCommDestroy(s.comm);
   s = Slot{};
@@ -111,6 +130,13 @@ int alloc_slot(Slot& s, uint64_t cap, uint32_t world) {
   rc |= dalloc(&s.back, cap);
   rc |= dalloc(&s.rk, s.rcap);
   rc |= dalloc(&s.rv, s.rcap);
+  // a peer's share of a uniform batch is cap / P; 25 % + 256 of slack
+  s.pcap = world == 1 ? cap : std::min<uint64_t>(cap, (cap + cap / 4) / world + 256);
+  const uint64_t slots = (uint64_t)world * s.pcap;
+  rc |= dalloc(&s.pk, slots);
+  rc |= dalloc(&s.pr, slots);
+  rc |= dalloc(&s.pv, slots);
+  rc |= dalloc(&s.pb, slots);
   return rc ? SHM_ENOMEM : SHM_OK;
 }
 
@@ -250,7 +276,15 @@ int shm_shard_search_begin(shm_shard* h, const uint64_t* keys, uint64_t n, void*
   s.stream = (hipStream_t)stream;
   s.busy = true;
   *ticket = (uint32_t)i;
-  const int rc = begin(h, s);
+  const uint32_t P = h->world;
+  int rc = shm_route_bucket(h->local, s.keys, s.n, P, s.cnts, s.kb, s.perm, s.stream);
+  s.ncap = P == 1 ? n : std::min<uint64_t>(s.pcap, (n + n / 4) / P + 256);
+  if (rc == SHM_OK) {
+    shm::dev::launch_route_pack(s.kb, s.cnts, P, s.ncap, s.pk, shm__error_word(h->local),
+                                s.stream);
+    rc = nccl_ok(ncclAllToAll(s.pk, s.pr, s.ncap, ncclUint64, s.comm, s.stream),
+                 "ncclAllToAll(keys)");
+  }
   if (rc) s.busy = false;
   return rc;
 }
@@ -260,17 +294,14 @@ int shm_shard_search_end(shm_shard* h, uint32_t ticket, uint64_t* vals_out, uint
   Slot& s = h->slot[ticket];
   if (s.n && (!vals_out || !found_out)) return SHM_EINVAL;
   s.busy = false;
-  std::vector<uint64_t> cnt, rcnt, soff, roff;
-  uint64_t nrecv = 0;
-  int rc = counts(h, s, cnt, rcnt, soff, roff, &nrecv);
+  const uint32_t P = h->world;
+  int rc = shm_search_batch(h->local, s.pr, (uint64_t)P * s.ncap, s.pv, nullptr, s.stream);
   if (rc) return rc;
-  if ((rc = ensure_recv(s, nrecv))) return rc;
-  if ((rc = exchange(h, s, s.kb, cnt, soff, s.rk, rcnt, roff))) return rc;
-  if ((rc = shm_search_batch(h->local, s.rk, nrecv, s.rv, nullptr, s.stream))) return rc;
-  // the values go back the way the keys came
-  if ((rc = exchange(h, s, s.rv, rcnt, roff, s.back, cnt, soff))) return rc;
-  return shm_route_unpermute_found(h->local, s.back, s.perm, s.n, vals_out, found_out,
-                                   s.stream);
+  // the results go back the way the keys came, slot for slot
+  NCCL_OK(ncclAllToAll(s.pv, s.pb, s.ncap, ncclUint64, s.comm, s.stream));
+  shm::dev::launch_route_unpack(s.pb, s.cnts, P, s.ncap, s.perm, s.n, vals_out, found_out,
+                                s.stream);
+  return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
 }
 
 int shm_shard_search(shm_shard* h, const uint64_t* keys, uint64_t n, uint64_t* vals_out,

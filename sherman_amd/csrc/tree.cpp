@@ -1194,6 +1194,11 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   return range_launch(t, s, a);
 }
 
+// Library-internal, not part of include/sherman_amd.h: the tree's sticky
+// device error word (shard.cpp's kernels report into it, so the next
+// synchronising call on the tree returns their errors)
+uint32_t* shm__error_word(shm_tree* t) { return t ? t->d_err : nullptr; }
+
 // Diagnostics, not part of include/sherman_amd.h: enable = 1 turns k_upper's
 // phase clock on, 0 off; out (nullable, kUpperStamps words) receives the last
 // chunk's stamps (out[0] = count, then 100 MHz wall-clock values).

@@ -375,5 +375,54 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
   if (n) hipLaunchKernelGGL(k_unpermute, grid1(n), dim3(kT), 0, s, in, perm, n, out, found);
 }
 
+// ---- fixed-capacity exchange (shard.cpp): no host-known counts ----------------
+// peer p's run of a bucketed batch starts at the sum of counts[0..p)
+__device__ __forceinline__ uint64_t peer_off(const uint64_t* counts, uint32_t p) {
+  uint64_t o = 0;
+  for (uint32_t q = 0; q < p; ++q) o += counts[q];
+  return o;
+}
+
+// out[p * cap + j] = kb[off_p + j] for j < counts[p], kKeyMax after (a get
+// of kKeyMax finds nothing); a run longer than cap is cut and reported
+__global__ void k_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P,
+                             uint64_t cap, uint64_t* out, uint32_t* err) {
+  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= (uint64_t)P * cap) return;
+  const uint32_t p = (uint32_t)(x / cap);
+  const uint64_t j = x - (uint64_t)p * cap;
+  const uint64_t c = counts[p];
+  out[x] = j < c ? kb[peer_off(counts, p) + j] : kKeyMax;
+  if (j == 0 && c > cap) atomicOr(err, kErrOverflow);
+}
+void launch_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P, uint64_t cap,
+                       uint64_t* out, uint32_t* err, hipStream_t s) {
+  const uint64_t n = (uint64_t)P * cap;
+  if (n) hipLaunchKernelGGL(k_route_pack, grid1(n), dim3(kT), 0, s, kb, counts, P, cap, out, err);
+}
+
+// bucketed position b (peer p, j = b - off_p): out[perm[b]] = in[p * cap + j]
+__global__ void k_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P,
+                               uint64_t cap, const uint32_t* perm, uint64_t n, uint64_t* out,
+                               uint8_t* found) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  uint32_t p = 0;
+  uint64_t off = 0;
+  while (p + 1 < P && off + counts[p] <= b) off += counts[p++];
+  const uint64_t j = b - off;
+  const uint64_t v = j < cap ? in[(uint64_t)p * cap + j] : kValueNull;
+  const uint32_t o = perm[b];
+  out[o] = v;
+  if (found) found[o] = v != kValueNull ? 1 : 0;
+}
+void launch_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P, uint64_t cap,
+                         const uint32_t* perm, uint64_t n, uint64_t* out, uint8_t* found,
+                         hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_route_unpack, grid1(n), dim3(kT), 0, s, in, counts, P, cap, perm, n, out,
+                       found);
+}
+
 }  // namespace dev
 }  // namespace shm

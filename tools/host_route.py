@@ -93,6 +93,49 @@ print(f"router pipelined, 2 streams: host issue {issue / 50 * 1e6:.1f} us/step, 
       f"wall {total / 50 * 1e6:.1f} us/step", flush=True)
 pend.clear()
 
+# the C-ABI shard (shm_shard_*, C++ over RCCL): plain and pipelined
+cs = shm.CShard(t, 1, 0, dist)
+rc_ = ShardRouter(t, 1, dist, cshard=cs)
+for name, fn in (("cabi search", lambda: rc_.search(q, v, f)),):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        fn()
+    issue = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    print(f"{name}: host issue {issue / 50 * 1e6:.1f} us/step, wall {total / 50 * 1e6:.1f} us/step",
+          flush=True)
+pc = {}
+
+
+def step4(i):
+    if pc.get(i) is None:
+        with torch.cuda.stream(streams[i & 1]):
+            pc[i] = rc_.search_begin(q)
+    with torch.cuda.stream(streams[(i + 1) & 1]):
+        pc[i + 1] = rc_.search_begin(q)
+    with torch.cuda.stream(streams[i & 1]):
+        rc_.search_end(pc.pop(i), *outs[i & 1])
+
+
+for i in range(6):
+    step4(i)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(6, 56):
+    step4(i)
+issue = time.perf_counter() - t0
+torch.cuda.synchronize()
+total = time.perf_counter() - t0
+print(f"cabi pipelined, 2 streams: host issue {issue / 50 * 1e6:.1f} us/step, "
+      f"wall {total / 50 * 1e6:.1f} us/step", flush=True)
+pc.clear()
+torch.cuda.synchronize()
+cs.close()
+
 # per-piece host cost of router.search (no device waits except tolist)
 import collections
 acc = collections.defaultdict(float)
