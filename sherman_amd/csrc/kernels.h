@@ -97,9 +97,10 @@ struct SegArgs {
   uint32_t* seg_P;            // pages after applying (1 = in place)
   uint32_t* seg_newpages;     // P - 1
   uint32_t* seg_ver;          // front_version observed
-  // per segment: 1 = its page's lock word was taken ahead by k_seg_fill_scan
-  // (k_upper releases them)
-  const uint32_t* seg_lk;
+  // the lock table and the chunk's epoch tag (taken with each page's DMA)
+  uint64_t* locks;
+  uint32_t num_locks;
+  uint64_t tag;
   uint32_t* err;
   // per-page occupancy bound and leaf summary kept by every leaf writer
   uint8_t* leaf_hw;
@@ -135,7 +136,6 @@ struct UpperArgs {
   const uint32_t* seg_P;
   const uint32_t* seg_np;
   const uint32_t* seg_ver;
-  const uint32_t* seg_lk;
   const uint32_t* ns_dev;
   uint32_t* spl_seg;         // split segments in key order
   uint32_t* spl_base;        // their first new page (exclusive scan)
@@ -227,23 +227,11 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
 // ---- segmentation (util.hip) --------------------------------------------------
 // Segments of a located op list (n_dev: device-side op count <= n) in two
 // launches: per 1024-op tile a head count (bsum), then each tile sums the
-// counts before it and fills its segments, taking each segment's lock word
-// (lane per segment, atomic max of the chunk's epoch tag on
-// lock[CityHash64(page) % num_locks]; seg_lk[s] = 1 when held; segments
-// sharing a word share the hold; every word is released when the chunk
-// retires, insert.hip take_word).  bsum holds seg_tiles(n) words.
-struct SegLock {
-  uint64_t* locks;
-  uint32_t num_locks;
-  uint64_t tag;
-  uint32_t* seg_lk;
-  uint32_t* err;
-};
+// counts before it and fills its segments.  bsum holds seg_tiles(n) words.
 constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
-                    const SegLock& lk, hipStream_t s);
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
 // exclusive scan of u64 (bsum: seg_tiles(n) words); tot = {total, *err} for
 // the range scan's one read-back
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,

@@ -77,7 +77,6 @@ struct shm_tree {
   uint32_t* seg_start = nullptr;
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr, *seg_ver = nullptr;
-  uint32_t* seg_lk = nullptr;  // lock words taken ahead per segment (k_seg_fill_scan)
   uint8_t* leaf_hw = nullptr;   // per-page occupancy bound (layout.h kLeafHwFull)
   uint8_t* sum = nullptr;       // leaf summaries, kSumBytes per page (layout.h)
   // k_upper state (insert.hip)
@@ -485,9 +484,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  const dev::SegLock lk{t->locks, t->cfg.num_locks, lock_tag, t->seg_lk, t->d_err};
-  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_page, d_ns, lk,
-                      s);
+  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_page, d_ns, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -504,7 +501,9 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.seg_P = t->seg_P;
   a.seg_newpages = t->seg_np;
   a.seg_ver = t->seg_ver;
-  a.seg_lk = t->seg_lk;
+  a.locks = t->locks;
+  a.num_locks = t->cfg.num_locks;
+  a.tag = lock_tag;
   a.err = t->d_err;
   a.leaf_hw = t->leaf_hw;
   a.sum = t->sum;
@@ -536,7 +535,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.seg_P = t->seg_P;
   u.seg_np = t->seg_np;
   u.seg_ver = t->seg_ver;
-  u.seg_lk = t->seg_lk;
   u.ns_dev = d_ns;
   u.spl_seg = t->spl_seg;
   u.spl_base = t->spl_base;
@@ -618,7 +616,7 @@ void free_all(shm_tree* t) {
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->bsum); F(t->bsum64);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_ver); F(t->seg_lk); F(t->leaf_hw); F(t->sum);
+  F(t->seg_ver); F(t->leaf_hw); F(t->sum);
   F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
@@ -864,7 +862,6 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->seg_P, segcap);
   rc |= dalloc(&t->seg_np, segcap);
   rc |= dalloc(&t->seg_ver, segcap);
-  rc |= dalloc(&t->seg_lk, segcap);
   rc |= dalloc(&t->leaf_hw, t->cap_pages);
   rc |= dalloc(&t->sum, t->cap_pages * kSumBytes);
   rc |= dalloc(&t->ctl, 1);

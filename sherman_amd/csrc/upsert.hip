@@ -4,10 +4,10 @@
 //
 // The batch's sorted unique keys are grouped into segments, one per target
 // leaf, and every segment's lock word lock[CityHash64(page) % num_locks] (the
-// reference's on-chip lock word, Tree.cpp:832-842, 205-242) is taken ahead by
-// the segmentation kernel (util.hip k_seg_fill_scan).  A wave takes G = 4
+// reference's on-chip lock word, Tree.cpp:832-842, 205-242) is taken with an
+// epoch tag in the same round trip as the page's DMA.  A wave takes G = 4
 // consecutive segments:
-//   * stage: the G pages by LDS-DMA, read under the locks
+//   * stage: the G pages by LDS-DMA with their lock words
 //     (lock_and_read_page, Tree.cpp:851-852), checked with check_consistent
 //     (front == rear, Tree.cpp:857) and the fences of every key.
 //   * apply: lane group q (16 lanes x 4 consecutive entries) holds slot q's
@@ -16,7 +16,7 @@
 //     f_version++ and r_version = f_version, 4-bit (Tree.cpp:878-912).
 //   * write back only the changed 18 B entries (the reference writes the
 //     entry, not the page: write_page_and_unlock(update_addr, ...),
-//     Tree.cpp:915-920); k_upper releases the words.
+//     Tree.cpp:915-920); the words are released when the chunk retires.
 // A segment whose page would reach 54 entries (the split point,
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
 // k-way split of insert.hip (k_upper), which also learns here how many new
@@ -234,22 +234,30 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   uint32_t err = 0;
 
   // segment record of group gg for lane s < G (raw loads, used later)
-  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en, uint32_t& lk) {
+  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en) {
     const bool sl = gg < ngroups && lane < G && gg * G + (uint64_t)lane < num_seg;
     const uint64_t gs = sl ? gg * G + (uint64_t)lane : 0;
     page = sl ? a.seg_page[gs] : 0;
     st = sl ? a.seg_start[gs] : 0u;
     en = sl ? a.seg_start[gs + 1] : 0u;
-    lk = sl ? a.seg_lk[gs] : 0u;
   };
-  // a loaded record -> page validity, slot ranges, op prefetch, page DMAs
-  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t lk,
-                   uint32_t b, bool& pok, uint32_t& qst, uint32_t& qen, uint64_t& pk,
-                   uint64_t& pv) {
+  // a loaded record -> page validity, the page's lock word, slot ranges, op
+  // prefetch, page DMAs.  lock_and_read_page (Tree.cpp:205-242, 851-852):
+  // the word is taken with an atomic max of the chunk's epoch tag (insert.hip
+  // take_word; a smaller value is a retired chunk's hold, the same tag a
+  // shared hold) in the same round trip as the page DMA; its old value is
+  // checked before the page is used
+  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t b, bool& pok,
+                   uint64_t& lkold, uint32_t& qst, uint32_t& qen, uint64_t& pk, uint64_t& pv) {
     const bool sl = lane < G && gg * G + (uint64_t)lane < num_seg;
     const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
     if (ballot(sl && !pgok)) err |= kErrBadPtr;
-    pok = pgok && lk != 0;
+    pok = pgok;
+    lkold = 0;
+    if (pgok)
+      lkold = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +
+                            cityhash64_u64(page) % a.num_locks,
+                        (unsigned long long)a.tag);
     qst = shfl32(st, q);
     qen = shfl32(en, q);
     const bool pf = (uint32_t)li < qen - qst;
@@ -262,33 +270,39 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
              bufs_lds + (uint32_t)((b * G + s) * kPageSize));
   };
 
-  uint64_t c_page, n_page;
-  uint32_t c_st, c_en, c_lk, n_st, n_en, n_lk;
+  uint64_t c_page, n_page, c_lk;
+  uint32_t c_st, c_en, n_st, n_en;
   bool c_pok;
   uint32_t c_qst, c_qen;
   uint64_t c_pk, c_pv;
-  rec(g, c_page, c_st, c_en, c_lk);
-  stage(g, c_page, c_st, c_en, c_lk, 0, c_pok, c_qst, c_qen, c_pk, c_pv);
-  rec(g + W, n_page, n_st, n_en, n_lk);
+  rec(g, c_page, c_st, c_en);
+  stage(g, c_page, c_st, c_en, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv);
+  rec(g + W, n_page, n_st, n_en);
   for (uint32_t it = 0;; ++it) {
-    wait_vm<0>();  // group g's pages and ops, group g + W's records
+    wait_vm<0>();  // group g's pages, lock words and ops, group g + W's records
     const uint32_t b = it & 1u;
     const uint64_t gn = g + W;
     bool x_pok = false;
+    uint64_t x_lk = 0;
     uint32_t x_qst = 0, x_qen = 0;
     uint64_t x_pk = 0, x_pv = 0;
     uint64_t m_page = 0;
-    uint32_t m_st = 0, m_en = 0, m_lk = 0;
+    uint32_t m_st = 0, m_en = 0;
+    // a word held by a later tag is not this chunk's to take (never in a
+    // serialised tree: reported as a lock failure, the segment left as is)
+    const bool held = c_lk <= a.tag;
+    if (ballot(c_pok && !held)) err |= kErrLock;
     if (gn < ngroups) {  // wave-uniform
-      stage(gn, n_page, n_st, n_en, n_lk, b ^ 1u, x_pok, x_qst, x_qen, x_pk, x_pv);
-      rec(gn + W, m_page, m_st, m_en, m_lk);
+      stage(gn, n_page, n_st, n_en, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv);
+      rec(gn + W, m_page, m_st, m_en);
     }
-    err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok, true,
-                          c_qst, c_qen, c_pk, c_pv);
+    err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
+                          true, c_qst, c_qen, c_pk, c_pv);
     if (gn >= ngroups) break;
     g = gn;
     c_page = n_page;
     c_pok = x_pok;
+    c_lk = x_lk;
     c_qst = x_qst;
     c_qen = x_qen;
     c_pk = x_pk;
@@ -296,7 +310,6 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     n_page = m_page;
     n_st = m_st;
     n_en = m_en;
-    n_lk = m_lk;
   }
   if (err) atomicOr(a.err, err);
 }

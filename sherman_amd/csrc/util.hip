@@ -78,12 +78,11 @@ __global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// seg_start / seg_page of every head; lock words as k_seg_fill
+// seg_start / seg_page of every head
 __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint64_t n,
                                                       const uint64_t* n_dev,
                                                       const uint32_t* bsum, uint32_t* seg_start,
-                                                      uint64_t* seg_page, uint32_t* num_seg,
-                                                      SegLock lk) {
+                                                      uint64_t* seg_page, uint32_t* num_seg) {
   const uint64_t nv = dev_n(n_dev, n);
   const uint32_t prefix = tiles_before<uint32_t>(bsum, blockIdx.x);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
@@ -99,21 +98,8 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = i0 + j;
     if (h[j]) {
-      const uint64_t pg = page[i];
       seg_start[pos] = (uint32_t)i;
-      seg_page[pos] = pg;
-      if (lk.locks) {
-        // lock_and_read_page's lock half (Tree.cpp:205-242, 851) with an
-        // epoch tag (insert.hip take_word): a smaller value is a retired
-        // chunk's hold, the chunk's own tag a shared hold; held until the
-        // chunk retires
-        unsigned long long* w = reinterpret_cast<unsigned long long*>(lk.locks) +
-                                cityhash64_u64(pg) % lk.num_locks;
-        const uint32_t ok =
-            atomicMax(w, (unsigned long long)lk.tag) <= (unsigned long long)lk.tag ? 1u : 0u;
-        if (!ok) atomicOr(lk.err, kErrLock);
-        lk.seg_lk[pos] = ok;
-      }
+      seg_page[pos] = page[i];
     }
     pos += h[j];
     if (i + 1 == nv) {
@@ -128,13 +114,12 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
 }
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
-                    const SegLock& lk, hipStream_t s) {
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg, hipStream_t s) {
   if (!n) return;
   const dim3 g((unsigned)seg_tiles(n));
   hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum);
   hipLaunchKernelGGL(k_seg_fill_scan, g, dim3(kT), 0, s, page, n, n_dev, (const uint32_t*)bsum,
-                     seg_start, seg_page, num_seg, lk);
+                     seg_start, seg_page, num_seg);
 }
 
 template <class T>
