@@ -295,5 +295,51 @@ __device__ __forceinline__ void put_leaf_sum(uint8_t* sum, uint64_t page_off, ui
   }
 }
 
+// ---- per-lane leaf access (the summary walk, the update matcher) --------------
+
+// leaf entry s of a page (18 B at 44 + 18 s, 2-byte aligned)
+__device__ __forceinline__ void lane_entry(const uint8_t* page, int s, uint64_t& key,
+                                           uint64_t& val, uint32_t& f, uint32_t& r) {
+  const uint32_t off = (uint32_t)(kOffRecords + kLeafEntry * s);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(page + (off & ~3u));
+  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+  const uint32_t sh = off & 3u;  // 0 or 2
+  const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  const uint32_t q3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  const uint32_t q4 = d4 >> (8 * sh);
+  f = q0 & 0xFF;
+  key = (uint64_t)((q0 >> 8) | (q1 << 24)) | ((uint64_t)((q1 >> 8) | (q2 << 24)) << 32);
+  val = (uint64_t)((q2 >> 8) | (q3 << 24)) | ((uint64_t)((q3 >> 8) | (q4 << 24)) << 32);
+  r = (q4 >> 8) & 0xFF;
+}
+
+__device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f, uint32_t r,
+                                          uint64_t k) {
+  return key == k && val != kValueNull && ((f ^ r) & 0xF) == 0;
+}
+
+// 4 bits: the bytes of x equal to the fingerprint pattern fq
+__device__ __forceinline__ uint32_t fp_bytes(uint32_t x, uint32_t fq) {
+  const uint32_t y = x ^ fq;
+  const uint32_t z = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y)) & 0x80808080u;
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+
+// the slots of a leaf summary line (dwords 4..19 as l1..l4) whose
+// fingerprint equals k's: bit s for slot s
+__device__ __forceinline__ uint64_t sum_candidates(const u32x4 l1, const u32x4 l2, const u32x4 l3,
+                                                   const u32x4 l4, uint64_t k) {
+  const uint32_t fq = key_fp(k) * 0x01010101u;
+  const uint32_t dw[14] = {l1.z, l1.w, l2.x, l2.y, l2.z, l2.w, l3.x,
+                           l3.y, l3.z, l3.w, l4.x, l4.y, l4.z, l4.w};
+  uint64_t cand = 0;
+#pragma unroll
+  for (int d = 0; d < 14; ++d) cand |= (uint64_t)fp_bytes(dw[d], fq) << (4 * d);
+  return cand & ((1ull << kLeafCardinality) - 1);
+}
+
 }  // namespace dev
 }  // namespace shm

@@ -39,8 +39,14 @@ struct WalkArgs {
   // stops after that slot; kLeafHwFull (internal pages, pages of a loaded
   // image) reads the whole page
   const uint8_t* leaf_hw;
-  // leaf summaries (layout.h kSumBytes per page; k_get_sum)
+  // leaf summaries (layout.h kSumBytes per page; k_get_sum, LOCATE)
   const uint8_t* sum;
+  // LOCATE at level 0 (nullable): the slot of an op whose key its leaf holds
+  // (bit 31 | slot | f byte << 8 | r byte << 16), else 0 and the leaf's
+  // out_new word = out_new_tag (a page with a new key is staged whole)
+  uint32_t* out_slot;
+  uint32_t* out_new;
+  uint32_t out_new_tag;
 };
 
 // batched get walk with grouped page resolution (get.hip)
@@ -97,6 +103,11 @@ struct SegArgs {
   uint32_t* seg_P;            // pages after applying (1 = in place)
   uint32_t* seg_newpages;     // P - 1
   uint32_t* seg_ver;          // front_version observed
+  // per op: the slot it overwrites (k_locate's out_slot: bit 31 | slot |
+  // f << 8 | r << 16), and per segment: 1 = some op is a new key (the page
+  // is staged and applied whole), 0 = overwrites only (written directly)
+  const uint32_t* oslot;
+  const uint8_t* seg_full;
   // the lock table and the chunk's epoch tag (taken with each page's DMA)
   uint64_t* locks;
   uint32_t num_locks;
@@ -230,8 +241,10 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
 // counts before it and fills its segments.  bsum holds seg_tiles(n) words.
 constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
+// seg_full[g] = (pnew[g's page] == tag), the match pass's verdict
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg, hipStream_t s);
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
+                    const uint32_t* pnew, uint32_t tag, uint8_t* seg_full, hipStream_t s);
 // exclusive scan of u64 (bsum: seg_tiles(n) words); tot = {total, *err} for
 // the range scan's one read-back
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,

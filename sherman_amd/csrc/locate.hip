@@ -14,6 +14,13 @@
 //   * internal page above the target: branchless search over its sorted keys
 //     (child = #keys <= k, internal_page_search, Tree.cpp:665-685), 6 dependent
 //     8 B loads from L2-resident upper levels.
+//   * with out_slot (the upsert locate): a leaf that has a summary line
+//     (layout.h) is resolved from it instead of its header -- highest and
+//     sibling for the fence rule, then the entries whose fingerprint matches
+//     the key.  An op whose key the leaf holds (a valid slot: key equal,
+//     value != 0) records that slot and its version bytes; any other op marks
+//     its leaf out_new[page] = tag, and only such pages are staged whole by
+//     the upsert (the rest are overwritten entry by entry, upsert.hip).
 // Op keys arrive sorted, so neighbouring lanes read the same header lines.
 #include "device_common.h"
 #include "kernels.h"
@@ -42,6 +49,8 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   uint32_t err = 0;
   int retries = 0;
   uint64_t out = 0;
+  uint32_t slot = 0;
+  const bool match = a.out_slot != nullptr && a.target_level == 0;
   for (int hop = 0;; ++hop) {
     if (hop > kMaxRounds) {
       err |= kErrRounds;
@@ -51,7 +60,39 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
       err |= kErrBadPtr;
       break;
     }
-    const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + ga_offset(ptr));
+    const uint64_t off = ga_offset(ptr);
+    const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + off);
+    if (match) {
+      const u32x4* line = reinterpret_cast<const u32x4*>(a.sum + (off >> 10) * kSumBytes);
+      const u32x4 l0 = line[0];
+      if ((l0.x & 0xFF) == kSumLeaf) {
+        const u32x4 l1 = line[1], l2 = line[2], l3 = line[3], l4 = line[4];
+        const uint64_t highest = (uint64_t)l0.z | ((uint64_t)l0.w << 32);
+        const uint64_t sibling = (uint64_t)l1.x | ((uint64_t)l1.y << 32);
+        if (k >= highest) {  // turn right (Tree.cpp:626-629)
+          if (!sibling) {
+            err |= kErrFence;
+            break;
+          }
+          ptr = sibling;
+          continue;
+        }
+        out = ptr;
+        uint64_t cand = sum_candidates(l1, l2, l3, l4, k);
+        while (cand) {  // the first valid slot holding k (upsert.hip's rule)
+          const int sl = ctz64(cand);
+          uint64_t ek, ev;
+          uint32_t ef, er;
+          lane_entry(reinterpret_cast<const uint8_t*>(pg), sl, ek, ev, ef, er);
+          if (ek == k && ev != kValueNull) {
+            slot = 0x80000000u | (uint32_t)sl | (ef << 8) | (er << 16);
+            break;
+          }
+          cand &= cand - 1;
+        }
+        break;
+      }
+    }
     const u32x4 A = *reinterpret_cast<const u32x4*>(pg);      // dwords 0..3
     const u32x4 B = *reinterpret_cast<const u32x4*>(pg + 4);  // dwords 4..7
     const u32x4 C = *reinterpret_cast<const u32x4*>(pg + 8);  // dwords 8..11
@@ -98,6 +139,12 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   }
   if (err) atomicOr(a.err, err);
   a.out_page[i] = out;
+  if (match) {
+    a.out_slot[i] = slot;
+    // a new key (or a leaf without a summary): its page is staged whole
+    // (out = 0 after an error marks page 0: staged, rejected as a bad pointer)
+    if (!slot) a.out_new[ga_offset(out) >> 10] = a.out_new_tag;
+  }
 }
 
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {

@@ -79,6 +79,11 @@ struct shm_tree {
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr, *seg_ver = nullptr;
   uint8_t* leaf_hw = nullptr;   // per-page occupancy bound (layout.h kLeafHwFull)
   uint8_t* sum = nullptr;       // leaf summaries, kSumBytes per page (layout.h)
+  // upsert staging verdicts: per op the slot it overwrites (k_locate), per
+  // page the last chunk tag that brought it a new key, per segment staged?
+  uint32_t* oslot = nullptr;
+  uint32_t* pnew = nullptr;
+  uint8_t* seg_full = nullptr;
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
   uint32_t *spl_seg = nullptr, *spl_base = nullptr, *leaf_rd = nullptr;
@@ -450,9 +455,12 @@ int drain_profile(shm_tree* t) {
 //   1. ordering: k_tile_dedup, coarse partition, k_bin_unique
 //      -> uk / uv (upserts, key order, last writer) and dk (deletes); counts
 //      stay on the device (d_counts[0..1]);
-//   2. k_locate: each upsert's leaf from the leaf directory (header walk);
-//   3. segmentation + lock words taken ahead (k_seg_count, k_seg_fill_scan);
-//   4. k_leaf_upsert_pipe: in-place upserts, splits flagged and counted;
+//   2. k_locate: each upsert's leaf from the leaf directory (summary or
+//      header walk), and the slot of each op that overwrites a held key;
+//   3. segmentation (k_seg_count, k_seg_fill_scan): a segment is staged
+//      whole only if its page gets a new key;
+//   4. k_leaf_upsert_pipe: lock words with the page DMAs, in-place upserts,
+//      splits flagged and counted;
 //   5. k_upper: leaf splits, parent levels, root growth, unlocks, the
 //      chunk's deletes, superblock.
 // step 1: it reads only the batch and writes the insert workspace
@@ -480,11 +488,15 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.n_dev = t->d_counts + 0;
   w.out_page = t->pages;
   w.target_level = 0;
+  w.out_slot = t->oslot;
+  w.out_new = t->pnew;
+  w.out_new_tag = tag;
   set_dir(t, &w.dir, &w.dir_lo, &w.dir_shift, &w.dir_n);
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_page, d_ns, s);
+  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_page, d_ns,
+                      t->pnew, tag, t->seg_full, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -501,6 +513,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.seg_P = t->seg_P;
   a.seg_newpages = t->seg_np;
   a.seg_ver = t->seg_ver;
+  a.oslot = t->oslot;
+  a.seg_full = t->seg_full;
   a.locks = t->locks;
   a.num_locks = t->cfg.num_locks;
   a.tag = lock_tag;
@@ -616,7 +630,7 @@ void free_all(shm_tree* t) {
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->bsum); F(t->bsum64);
   F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_ver); F(t->leaf_hw); F(t->sum);
+  F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew); F(t->seg_full);
   F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
@@ -864,6 +878,9 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->seg_ver, segcap);
   rc |= dalloc(&t->leaf_hw, t->cap_pages);
   rc |= dalloc(&t->sum, t->cap_pages * kSumBytes);
+  rc |= dalloc(&t->oslot, n);
+  rc |= dalloc(&t->pnew, t->cap_pages);
+  rc |= dalloc(&t->seg_full, segcap);
   rc |= dalloc(&t->ctl, 1);
   rc |= dalloc(&t->spl_seg, segcap);
   rc |= dalloc(&t->spl_base, segcap);
@@ -915,7 +932,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->gws[1].S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->arena, 0, kPageSize, s) ||
       hipMemsetAsync(t->leaf_hw, kLeafHwFull, t->cap_pages, s) ||
-      hipMemsetAsync(t->sum, 0, t->cap_pages * kSumBytes, s))
+      hipMemsetAsync(t->sum, 0, t->cap_pages * kSumBytes, s) ||
+      hipMemsetAsync(t->pnew, 0, sizeof(uint32_t) * t->cap_pages, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
   t->next_page = 1;

@@ -17,6 +17,9 @@
 //   * write back only the changed 18 B entries (the reference writes the
 //     entry, not the page: write_page_and_unlock(update_addr, ...),
 //     Tree.cpp:915-920); the words are released when the chunk retires.
+// A segment whose ops all overwrite keys the page holds (k_locate's
+// out_slot, seg_full = 0) is not staged: its lanes write the entries at the
+// recorded slots with the recorded versions + 1, the page read skipped.
 // A segment whose page would reach 54 entries (the split point,
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
 // k-way split of insert.hip (k_upper), which also learns here how many new
@@ -46,7 +49,7 @@ namespace {
 template <int G>
 __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t* buf,
                                                 uint64_t g0, uint32_t num_seg, uint64_t page,
-                                                bool pok, bool locked, uint32_t qst,
+                                                bool pok, bool full, bool locked, uint32_t qst,
                                                 uint32_t qen, uint64_t pk, uint64_t pv) {
   constexpr int L = kWave / G;                       // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;  // entries per lane
@@ -65,7 +68,9 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   const uint32_t fver = h2 & 0xFF;
   const uint64_t lowest = (uint64_t)h7 | ((uint64_t)h8 << 32);
   const uint64_t highest = (uint64_t)h9 | ((uint64_t)h10 << 32);
-  const bool qpok = (shfl32(pok ? 1u : 0u, q) != 0) && locked;
+  const bool qown = (shfl32(pok ? 1u : 0u, q) != 0) && locked;
+  const bool qfull = shfl32(full ? 1u : 0u, q) != 0;
+  const bool qpok = qown && qfull;  // a staged page (buf slot q holds it)
   const bool cons = leftmost == 0 && fver == (z & 0xFF);
   if (ballot(qpok && !cons)) err |= kErrInconsistent;
   const uint64_t qpage = shfl64(page, q);
@@ -161,6 +166,22 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
       }
     }
   }
+  // ---- overwrite-only segments: the recorded slots, lane per op ---------------------
+  if (qown && !qfull) {
+    uint32_t* pg = reinterpret_cast<uint32_t*>(a.arena + ga_offset(qpage));
+    for (uint32_t t = (uint32_t)li; t < qen - qst; t += (uint32_t)L) {
+      const uint32_t os = a.oslot[qst + t];
+      const uint64_t kq = t < (uint32_t)L ? pk : a.op_key[qst + t];
+      const uint64_t vq = t < (uint32_t)L ? pv : a.op_val[qst + t];
+      if (!(os >> 31)) {  // a new key in a segment not staged: never by construction
+        bad = true;
+        continue;
+      }
+      const uint32_t f = (os >> 8) & 0xFF, r = (os >> 16) & 0xFF;
+      const uint32_t nf = ((f & 0xF) + 1) & 0xF;
+      put_leaf_entry(pg, (int)(os & 63u), kq, vq, (f & 0xF0) | nf, (r & 0xF0) | nf);
+    }
+  }
   if (ballot(bad)) err |= kErrPlan;
   live = live && !bad;
   const bool over = T > (uint32_t)(kLeafCardinality - 1);
@@ -234,12 +255,13 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   uint32_t err = 0;
 
   // segment record of group gg for lane s < G (raw loads, used later)
-  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en) {
+  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en, uint32_t& fl) {
     const bool sl = gg < ngroups && lane < G && gg * G + (uint64_t)lane < num_seg;
     const uint64_t gs = sl ? gg * G + (uint64_t)lane : 0;
     page = sl ? a.seg_page[gs] : 0;
     st = sl ? a.seg_start[gs] : 0u;
     en = sl ? a.seg_start[gs + 1] : 0u;
+    fl = sl ? (uint32_t)a.seg_full[gs] : 0u;
   };
   // a loaded record -> page validity, the page's lock word, slot ranges, op
   // prefetch, page DMAs.  lock_and_read_page (Tree.cpp:205-242, 851-852):
@@ -247,7 +269,8 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   // take_word; a smaller value is a retired chunk's hold, the same tag a
   // shared hold) in the same round trip as the page DMA; its old value is
   // checked before the page is used
-  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t b, bool& pok,
+  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t fl, uint32_t b,
+                   bool& pok,
                    uint64_t& lkold, uint32_t& qst, uint32_t& qen, uint64_t& pk, uint64_t& pv) {
     const bool sl = lane < G && gg * G + (uint64_t)lane < num_seg;
     const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
@@ -264,20 +287,21 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
     pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer b's reads are done
+    const uint64_t dma = ballot(pgok && fl != 0);  // pages with a new key
 #pragma unroll
     for (int s = 0; s < G; ++s)
-      glds16(a.arena + ga_offset(rl64(pok ? page : 0, s)),
-             bufs_lds + (uint32_t)((b * G + s) * kPageSize));
+      if ((dma >> s) & 1)
+        glds16(a.arena + ga_offset(rl64(page, s)), bufs_lds + (uint32_t)((b * G + s) * kPageSize));
   };
 
   uint64_t c_page, n_page, c_lk;
-  uint32_t c_st, c_en, n_st, n_en;
+  uint32_t c_st, c_en, c_fl, n_st, n_en, n_fl;
   bool c_pok;
   uint32_t c_qst, c_qen;
   uint64_t c_pk, c_pv;
-  rec(g, c_page, c_st, c_en);
-  stage(g, c_page, c_st, c_en, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv);
-  rec(g + W, n_page, n_st, n_en);
+  rec(g, c_page, c_st, c_en, c_fl);
+  stage(g, c_page, c_st, c_en, c_fl, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv);
+  rec(g + W, n_page, n_st, n_en, n_fl);
   for (uint32_t it = 0;; ++it) {
     wait_vm<0>();  // group g's pages, lock words and ops, group g + W's records
     const uint32_t b = it & 1u;
@@ -287,20 +311,21 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     uint32_t x_qst = 0, x_qen = 0;
     uint64_t x_pk = 0, x_pv = 0;
     uint64_t m_page = 0;
-    uint32_t m_st = 0, m_en = 0;
+    uint32_t m_st = 0, m_en = 0, m_fl = 0;
     // a word held by a later tag is not this chunk's to take (never in a
     // serialised tree: reported as a lock failure, the segment left as is)
     const bool held = c_lk <= a.tag;
     if (ballot(c_pok && !held)) err |= kErrLock;
     if (gn < ngroups) {  // wave-uniform
-      stage(gn, n_page, n_st, n_en, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv);
-      rec(gn + W, m_page, m_st, m_en);
+      stage(gn, n_page, n_st, n_en, n_fl, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv);
+      rec(gn + W, m_page, m_st, m_en, m_fl);
     }
     err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
-                          true, c_qst, c_qen, c_pk, c_pv);
+                          c_fl != 0, true, c_qst, c_qen, c_pk, c_pv);
     if (gn >= ngroups) break;
     g = gn;
     c_page = n_page;
+    c_fl = n_fl;
     c_pok = x_pok;
     c_lk = x_lk;
     c_qst = x_qst;
@@ -310,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     n_page = m_page;
     n_st = m_st;
     n_en = m_en;
+    n_fl = m_fl;
   }
   if (err) atomicOr(a.err, err);
 }

@@ -82,7 +82,9 @@ __global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t
 __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint64_t n,
                                                       const uint64_t* n_dev,
                                                       const uint32_t* bsum, uint32_t* seg_start,
-                                                      uint64_t* seg_page, uint32_t* num_seg) {
+                                                      uint64_t* seg_page, uint32_t* num_seg,
+                                                      const uint32_t* pnew, uint32_t tag,
+                                                      uint8_t* seg_full) {
   const uint64_t nv = dev_n(n_dev, n);
   const uint32_t prefix = tiles_before<uint32_t>(bsum, blockIdx.x);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
@@ -98,8 +100,10 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = i0 + j;
     if (h[j]) {
+      const uint64_t pg = page[i];
       seg_start[pos] = (uint32_t)i;
-      seg_page[pos] = page[i];
+      seg_page[pos] = pg;
+      seg_full[pos] = pnew[ga_offset(pg) >> 10] == tag ? 1 : 0;
     }
     pos += h[j];
     if (i + 1 == nv) {
@@ -114,12 +118,13 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
 }
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg, hipStream_t s) {
+                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
+                    const uint32_t* pnew, uint32_t tag, uint8_t* seg_full, hipStream_t s) {
   if (!n) return;
   const dim3 g((unsigned)seg_tiles(n));
   hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum);
   hipLaunchKernelGGL(k_seg_fill_scan, g, dim3(kT), 0, s, page, n, n_dev, (const uint32_t*)bsum,
-                     seg_start, seg_page, num_seg);
+                     seg_start, seg_page, num_seg, pnew, tag, seg_full);
 }
 
 template <class T>

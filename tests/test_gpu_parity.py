@@ -207,6 +207,46 @@ def test_image_conformance_gpu_to_oracle(lib_ok):
     t.close()
 
 
+def test_overwrites_write_the_reference_entry_bytes(lib_ok):
+    """Overwrite-only leaves are written entry by entry at the slot k_locate
+    found, without staging the page (upsert.hip); leaves that also get a new
+    key are staged.  Either way every byte of the page image equals the
+    oracle's after the same batch: the value, f_version + 1 and r_version =
+    f_version per overwritten entry (Tree.cpp:878-912), nothing else moved."""
+    rng = np.random.default_rng(4242)
+    orc = OracleTree(256 << 20)
+    ks = hashed_keys(1, 150001)
+    orc.apply_batch(ks, ks ^ U64(0x77))
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18)
+    t.load_image(orc.image(), orc.root_ptr)
+
+    def same_image():
+        img, root = t.dump_image()
+        ref = orc.image()
+        assert root == orc.root_ptr
+        assert img.size == ref.size, (img.size, ref.size)
+        diff = np.nonzero(img[1024:] != ref[1024:])[0]
+        assert diff.size == 0, f"{diff.size} bytes differ, first at {1024 + int(diff[0])}"
+
+    for r in range(3):  # overwrite-only: every leaf written in place
+        up = rng.choice(ks, 60000, replace=False)
+        vs = rng.integers(1, 1 << 62, up.size).astype(U64)
+        gpu_insert(t, up, vs)
+        orc.apply_batch(up, vs)
+        same_image()
+    # overwrites plus a few new keys (those leaves staged, no split)
+    up = rng.choice(ks, 40000, replace=False)
+    new = hashed_keys(500001, 500301)
+    both = np.concatenate([up, new])
+    vs = rng.integers(1, 1 << 62, both.size).astype(U64)
+    gpu_insert(t, both, vs)
+    orc.apply_batch(both, vs)
+    if t.stats()["splits"] == 0:
+        same_image()
+    compare_contents(t, orc)
+    t.close()
+
+
 @pytest.mark.parametrize("max_batch,cap,leaf_dir", [(1 << 17, None, True),
                                                     (128, 16, True),
                                                     (1 << 17, None, False)])
