@@ -41,12 +41,17 @@ struct WalkArgs {
   const uint8_t* leaf_hw;
   // leaf summaries (layout.h kSumBytes per page; k_get_sum, LOCATE)
   const uint8_t* sum;
-  // LOCATE at level 0 (nullable): the slot of an op whose key its leaf holds
-  // (bit 31 | slot | f byte << 8 | r byte << 16), else 0 and the leaf's
-  // out_new word = out_new_tag (a page with a new key is staged whole)
+  // LOCATE at level 0 (nullable): an op whose key its leaf holds overwrites
+  // that entry in place (vals[i], under the page's lock word taken with
+  // lock_tag) and records out_slot[i] = bit 31 | slot; any other op gets 0
+  // and marks its leaf out_new[page] = out_new_tag (staged whole by the upsert)
   uint32_t* out_slot;
   uint32_t* out_new;
   uint32_t out_new_tag;
+  const uint64_t* vals;
+  uint64_t* locks;
+  uint32_t num_locks;
+  uint64_t lock_tag;
 };
 
 // batched get walk with grouped page resolution (get.hip)
@@ -103,9 +108,9 @@ struct SegArgs {
   uint32_t* seg_P;            // pages after applying (1 = in place)
   uint32_t* seg_newpages;     // P - 1
   uint32_t* seg_ver;          // front_version observed
-  // per op: the slot it overwrites (k_locate's out_slot: bit 31 | slot |
-  // f << 8 | r << 16), and per segment: 1 = some op is a new key (the page
-  // is staged and applied whole), 0 = overwrites only (written directly)
+  // per op: bit 31 = already applied in place by k_locate (out_slot), and
+  // per segment: 1 = some op is a new key (the page is staged and its
+  // remaining ops applied), 0 = overwrites only (nothing left to apply)
   const uint32_t* oslot;
   const uint8_t* seg_full;
   // the lock table and the chunk's epoch tag (taken with each page's DMA)

@@ -17,10 +17,15 @@
 //   * with out_slot (the upsert locate): a leaf that has a summary line
 //     (layout.h) is resolved from it instead of its header -- highest and
 //     sibling for the fence rule, then the entries whose fingerprint matches
-//     the key.  An op whose key the leaf holds (a valid slot: key equal,
-//     value != 0) records that slot and its version bytes; any other op marks
-//     its leaf out_new[page] = tag, and only such pages are staged whole by
-//     the upsert (the rest are overwritten entry by entry, upsert.hip).
+//     the key.  An op whose key the leaf holds (the first valid slot: key
+//     equal, value != 0, upsert.hip's rule) is an update: the lane takes the
+//     page's lock word (epoch atomic max, insert.hip take_word;
+//     lock_and_read_page, Tree.cpp:851-852) and writes the entry -- value,
+//     f_version + 1, r_version = f_version (Tree.cpp:878-912) -- with one
+//     18 B write, the page never read whole (write_page_and_unlock of the
+//     entry, Tree.cpp:915-920).  Any other op marks its leaf out_new[page] =
+//     tag: only such pages are staged by the upsert, which skips the ops
+//     applied here.
 // Op keys arrive sorted, so neighbouring lanes read the same header lines.
 #include "device_common.h"
 #include "kernels.h"
@@ -85,7 +90,17 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
           uint32_t ef, er;
           lane_entry(reinterpret_cast<const uint8_t*>(pg), sl, ek, ev, ef, er);
           if (ek == k && ev != kValueNull) {
-            slot = 0x80000000u | (uint32_t)sl | (ef << 8) | (er << 16);
+            const unsigned long long old = atomicMax(
+                reinterpret_cast<unsigned long long*>(a.locks) + cityhash64_u64(ptr) % a.num_locks,
+                (unsigned long long)a.lock_tag);
+            if (old > a.lock_tag) {  // a later chunk's hold: left to the staged path
+              err |= kErrLock;
+            } else {
+              const uint32_t nf = ((ef & 0xF) + 1) & 0xF;
+              put_leaf_entry(const_cast<uint32_t*>(pg), sl, k, a.vals[i], (ef & 0xF0) | nf,
+                             (er & 0xF0) | nf);
+              slot = 0x80000000u | (uint32_t)sl;
+            }
             break;
           }
           cand &= cand - 1;

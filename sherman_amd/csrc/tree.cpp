@@ -456,7 +456,8 @@ int drain_profile(shm_tree* t) {
 //      -> uk / uv (upserts, key order, last writer) and dk (deletes); counts
 //      stay on the device (d_counts[0..1]);
 //   2. k_locate: each upsert's leaf from the leaf directory (summary or
-//      header walk), and the slot of each op that overwrites a held key;
+//      header walk); an op whose key its leaf holds is applied right there
+//      (lock word, one entry write);
 //   3. segmentation (k_seg_count, k_seg_fill_scan): a segment is staged
 //      whole only if its page gets a new key;
 //   4. k_leaf_upsert_pipe: lock words with the page DMAs, in-place upserts,
@@ -491,6 +492,10 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.out_slot = t->oslot;
   w.out_new = t->pnew;
   w.out_new_tag = tag;
+  w.vals = t->uv;
+  w.locks = t->locks;
+  w.num_locks = t->cfg.num_locks;
+  w.lock_tag = lock_tag;
   set_dir(t, &w.dir, &w.dir_lo, &w.dir_shift, &w.dir_n);
   dev::launch_locate(w, n, s);
   DBG(s, "locate");

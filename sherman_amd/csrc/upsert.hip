@@ -17,9 +17,9 @@
 //   * write back only the changed 18 B entries (the reference writes the
 //     entry, not the page: write_page_and_unlock(update_addr, ...),
 //     Tree.cpp:915-920); the words are released when the chunk retires.
-// A segment whose ops all overwrite keys the page holds (k_locate's
-// out_slot, seg_full = 0) is not staged: its lanes write the entries at the
-// recorded slots with the recorded versions + 1, the page read skipped.
+// Overwrites of keys a page holds were applied in place by k_locate (oslot
+// bit 31); a segment made only of those (seg_full = 0) is neither locked nor
+// staged here, and a staged segment skips them in its op loop.
 // A segment whose page would reach 54 entries (the split point,
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
 // k-way split of insert.hip (k_upper), which also learns here how many new
@@ -50,7 +50,8 @@ template <int G>
 __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t* buf,
                                                 uint64_t g0, uint32_t num_seg, uint64_t page,
                                                 bool pok, bool full, bool locked, uint32_t qst,
-                                                uint32_t qen, uint64_t pk, uint64_t pv) {
+                                                uint32_t qen, uint64_t pk, uint64_t pv,
+                                                uint32_t po) {
   constexpr int L = kWave / G;                       // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;  // entries per lane
   constexpr int CD = kLeafEntry * E / 4;             // dwords per lane chunk
@@ -125,10 +126,14 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     const bool act = t < nloop && !bad;
     const int src = q * L + (t < (uint32_t)L ? (int)t : L - 1);
     const uint64_t sk = shfl64(pk, src), sv = shfl64(pv, src);
+    const uint32_t so = shfl32(po, src);
+    // an op k_locate applied in place: its key is already valid in the page
+    const bool done = (t < (uint32_t)L ? so : (act ? a.oslot[qst + t] : 0u)) >> 31;
     const uint64_t kq = act ? (t < (uint32_t)L ? sk : a.op_key[qst + t]) : 0;
     const uint64_t vq = act ? (t < (uint32_t)L ? sv : a.op_val[qst + t]) : 0;
-    if (act && (kq < lowest || kq >= highest)) bad = true;  // not this page's key
-    const bool go = act && !bad;
+    if (ballot(act && done) == ballot(act)) continue;  // wave-uniform
+    if (act && !done && (kq < lowest || kq >= highest)) bad = true;  // not this page's key
+    const bool go = act && !bad && !done;
     int hj = -1;
 #pragma unroll
     for (int j = E - 1; j >= 0; --j)
@@ -164,22 +169,6 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         dirty[j] = true;
         fresh[j] = fresh[j] || isnew;
       }
-    }
-  }
-  // ---- overwrite-only segments: the recorded slots, lane per op ---------------------
-  if (qown && !qfull) {
-    uint32_t* pg = reinterpret_cast<uint32_t*>(a.arena + ga_offset(qpage));
-    for (uint32_t t = (uint32_t)li; t < qen - qst; t += (uint32_t)L) {
-      const uint32_t os = a.oslot[qst + t];
-      const uint64_t kq = t < (uint32_t)L ? pk : a.op_key[qst + t];
-      const uint64_t vq = t < (uint32_t)L ? pv : a.op_val[qst + t];
-      if (!(os >> 31)) {  // a new key in a segment not staged: never by construction
-        bad = true;
-        continue;
-      }
-      const uint32_t f = (os >> 8) & 0xFF, r = (os >> 16) & 0xFF;
-      const uint32_t nf = ((f & 0xF) + 1) & 0xF;
-      put_leaf_entry(pg, (int)(os & 63u), kq, vq, (f & 0xF0) | nf, (r & 0xF0) | nf);
     }
   }
   if (ballot(bad)) err |= kErrPlan;
@@ -270,14 +259,14 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   // shared hold) in the same round trip as the page DMA; its old value is
   // checked before the page is used
   auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t fl, uint32_t b,
-                   bool& pok,
-                   uint64_t& lkold, uint32_t& qst, uint32_t& qen, uint64_t& pk, uint64_t& pv) {
+                   bool& pok, uint64_t& lkold, uint32_t& qst, uint32_t& qen, uint64_t& pk,
+                   uint64_t& pv, uint32_t& po) {
     const bool sl = lane < G && gg * G + (uint64_t)lane < num_seg;
     const bool pgok = sl && ptr_ok(page, a.node, a.arena_bytes);
     if (ballot(sl && !pgok)) err |= kErrBadPtr;
     pok = pgok;
     lkold = 0;
-    if (pgok)
+    if (pgok && fl)  // overwrite-only segments were locked by k_locate
       lkold = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +
                             cityhash64_u64(page) % a.num_locks,
                         (unsigned long long)a.tag);
@@ -286,6 +275,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     const bool pf = (uint32_t)li < qen - qst;
     pk = pf ? a.op_key[qst + (uint32_t)li] : 0;
     pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
+    po = pf ? a.oslot[qst + (uint32_t)li] : 0u;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer b's reads are done
     const uint64_t dma = ballot(pgok && fl != 0);  // pages with a new key
 #pragma unroll
@@ -299,8 +289,9 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   bool c_pok;
   uint32_t c_qst, c_qen;
   uint64_t c_pk, c_pv;
+  uint32_t c_po;
   rec(g, c_page, c_st, c_en, c_fl);
-  stage(g, c_page, c_st, c_en, c_fl, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv);
+  stage(g, c_page, c_st, c_en, c_fl, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv, c_po);
   rec(g + W, n_page, n_st, n_en, n_fl);
   for (uint32_t it = 0;; ++it) {
     wait_vm<0>();  // group g's pages, lock words and ops, group g + W's records
@@ -310,6 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     uint64_t x_lk = 0;
     uint32_t x_qst = 0, x_qen = 0;
     uint64_t x_pk = 0, x_pv = 0;
+    uint32_t x_po = 0;
     uint64_t m_page = 0;
     uint32_t m_st = 0, m_en = 0, m_fl = 0;
     // a word held by a later tag is not this chunk's to take (never in a
@@ -317,11 +309,11 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     const bool held = c_lk <= a.tag;
     if (ballot(c_pok && !held)) err |= kErrLock;
     if (gn < ngroups) {  // wave-uniform
-      stage(gn, n_page, n_st, n_en, n_fl, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv);
+      stage(gn, n_page, n_st, n_en, n_fl, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv, x_po);
       rec(gn + W, m_page, m_st, m_en, m_fl);
     }
     err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
-                          c_fl != 0, true, c_qst, c_qen, c_pk, c_pv);
+                          c_fl != 0, true, c_qst, c_qen, c_pk, c_pv, c_po);
     if (gn >= ngroups) break;
     g = gn;
     c_page = n_page;
@@ -332,6 +324,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     c_qen = x_qen;
     c_pk = x_pk;
     c_pv = x_pv;
+    c_po = x_po;
     n_page = m_page;
     n_st = m_st;
     n_en = m_en;
