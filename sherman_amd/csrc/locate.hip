@@ -84,15 +84,20 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
         }
         out = ptr;
         uint64_t cand = sum_candidates(l1, l2, l3, l4, k);
+        // a possible update: the page's lock word is taken in the same round
+        // trip as the entry reads (a false candidate leaves a hold of this
+        // chunk's tag, which the upsert shares)
+        unsigned long long old = 0;
+        if (cand)
+          old = atomicMax(
+              reinterpret_cast<unsigned long long*>(a.locks) + cityhash64_u64(ptr) % a.num_locks,
+              (unsigned long long)a.lock_tag);
         while (cand) {  // the first valid slot holding k (upsert.hip's rule)
           const int sl = ctz64(cand);
           uint64_t ek, ev;
           uint32_t ef, er;
           lane_entry(reinterpret_cast<const uint8_t*>(pg), sl, ek, ev, ef, er);
           if (ek == k && ev != kValueNull) {
-            const unsigned long long old = atomicMax(
-                reinterpret_cast<unsigned long long*>(a.locks) + cityhash64_u64(ptr) % a.num_locks,
-                (unsigned long long)a.lock_tag);
             if (old > a.lock_tag) {  // a later chunk's hold: left to the staged path
               err |= kErrLock;
             } else {
