@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       const uint32_t g = a.spl_seg[k];
       const uint32_t pb = a.spl_base[k];
       const int p = (int)(gp - pb) + 1;
-      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_start[g + 1] - a.seg_start[g]};
+      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
       const Hdr h = parse_hdr(w);
       stage_page(L.page, w);
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       const int P = (int)a.seg_P[g];
       const uint64_t page = a.seg_page[g];
       if (!fan_in(a.leaf_rd + g, (uint32_t)(P - 1))) err |= kErrLock;
-      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_start[g + 1] - a.seg_start[g]};
+      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(page));
       const Hdr h = parse_hdr(w);
       if (h.fver != a.seg_ver[g] || h.fver != h.rver_leaf) err |= kErrPlan;

@@ -99,8 +99,10 @@ struct SegArgs {
   // sorted unique operation keys / values
   const uint64_t* op_key;
   const uint64_t* op_val;
-  // segments (runs of ops targeting one page)
-  const uint32_t* seg_start;  // [num_seg + 1]
+  // staged segments (runs of ops targeting one page that gets a new key,
+  // launch_segment): ops [seg_start, seg_end) of page seg_page
+  const uint32_t* seg_start;  // [num_seg]
+  const uint32_t* seg_end;    // [num_seg]
   const uint64_t* seg_page;   // [num_seg]
   uint32_t num_seg;           // an upper bound of *num_seg_dev (grid size)
   const uint32_t* num_seg_dev;  // device-side segment count
@@ -108,11 +110,8 @@ struct SegArgs {
   uint32_t* seg_P;            // pages after applying (1 = in place)
   uint32_t* seg_newpages;     // P - 1
   uint32_t* seg_ver;          // front_version observed
-  // per op: bit 31 = already applied in place by k_locate (out_slot), and
-  // per segment: 1 = some op is a new key (the page is staged and its
-  // remaining ops applied), 0 = overwrites only (nothing left to apply)
+  // per op: bit 31 = already applied in place by k_locate (out_slot)
   const uint32_t* oslot;
-  const uint8_t* seg_full;
   // the lock table and the chunk's epoch tag (taken with each page's DMA)
   uint64_t* locks;
   uint32_t num_locks;
@@ -147,6 +146,7 @@ struct UpperArgs {
   const uint64_t* op_key;
   const uint64_t* op_val;
   const uint32_t* seg_start;
+  const uint32_t* seg_end;
   const uint64_t* seg_page;
   const uint32_t* seg_T;
   const uint32_t* seg_P;
@@ -241,15 +241,16 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);
 
 // ---- segmentation (util.hip) --------------------------------------------------
-// Segments of a located op list (n_dev: device-side op count <= n) in two
-// launches: per 1024-op tile a head count (bsum), then each tile sums the
-// counts before it and fills its segments.  bsum holds seg_tiles(n) words.
+// Staged segments of a located op list (n_dev: device-side op count <= n):
+// the runs of ops on one page whose page k_locate marked (pnew[page] ==
+// tag: it gets a new key); runs of in-place overwrites are left out.  Two
+// launches: per 1024-op tile a staged-head count (bsum), then each tile sums
+// the counts before it and fills its segments.  bsum holds seg_tiles(n) words.
 constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
-// seg_full[g] = (pnew[g's page] == tag), the match pass's verdict
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
-                    const uint32_t* pnew, uint32_t tag, uint8_t* seg_full, hipStream_t s);
+                    uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, hipStream_t s);
 // exclusive scan of u64 (bsum: seg_tiles(n) words); tot = {total, *err} for
 // the range scan's one read-back
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,

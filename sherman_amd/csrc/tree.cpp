@@ -75,15 +75,15 @@ struct shm_tree {
   uint32_t* bsum = nullptr;  // per-tile sums of the segmentation
   uint64_t* bsum64 = nullptr;
   uint32_t* seg_start = nullptr;
+  uint32_t* seg_end = nullptr;
   uint64_t* seg_page = nullptr;
   uint32_t *seg_T = nullptr, *seg_P = nullptr, *seg_np = nullptr, *seg_ver = nullptr;
   uint8_t* leaf_hw = nullptr;   // per-page occupancy bound (layout.h kLeafHwFull)
   uint8_t* sum = nullptr;       // leaf summaries, kSumBytes per page (layout.h)
   // upsert staging verdicts: per op the slot it overwrites (k_locate), per
-  // page the last chunk tag that brought it a new key, per segment staged?
+  // page the last chunk tag that brought it a new key
   uint32_t* oslot = nullptr;
   uint32_t* pnew = nullptr;
-  uint8_t* seg_full = nullptr;
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
   uint32_t *spl_seg = nullptr, *spl_base = nullptr, *leaf_rd = nullptr;
@@ -458,8 +458,8 @@ int drain_profile(shm_tree* t) {
 //   2. k_locate: each upsert's leaf from the leaf directory (summary or
 //      header walk); an op whose key its leaf holds is applied right there
 //      (lock word, one entry write);
-//   3. segmentation (k_seg_count, k_seg_fill_scan): a segment is staged
-//      whole only if its page gets a new key;
+//   3. segmentation (k_seg_count, k_seg_fill_scan): only the runs of ops
+//      on a page that gets a new key are listed (the upsert stages them);
 //   4. k_leaf_upsert_pipe: lock words with the page DMAs, in-place upserts,
 //      splits flagged and counted;
 //   5. k_upper: leaf splits, parent levels, root growth, unlocks, the
@@ -500,8 +500,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_page, d_ns,
-                      t->pnew, tag, t->seg_full, s);
+  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_end,
+                      t->seg_page, d_ns, t->pnew, tag, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -511,6 +511,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.op_key = t->uk;
   a.op_val = t->uv;
   a.seg_start = t->seg_start;
+  a.seg_end = t->seg_end;
   a.seg_page = t->seg_page;
   a.num_seg = (uint32_t)n;
   a.num_seg_dev = d_ns;
@@ -519,7 +520,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.seg_newpages = t->seg_np;
   a.seg_ver = t->seg_ver;
   a.oslot = t->oslot;
-  a.seg_full = t->seg_full;
   a.locks = t->locks;
   a.num_locks = t->cfg.num_locks;
   a.tag = lock_tag;
@@ -549,6 +549,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.op_key = t->uk;
   u.op_val = t->uv;
   u.seg_start = t->seg_start;
+  u.seg_end = t->seg_end;
   u.seg_page = t->seg_page;
   u.seg_T = t->seg_T;
   u.seg_P = t->seg_P;
@@ -634,8 +635,8 @@ void free_all(shm_tree* t) {
     if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->bsum); F(t->bsum64);
-  F(t->seg_start); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
-  F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew); F(t->seg_full);
+  F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
+  F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
   F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
@@ -876,6 +877,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->bsum, dev::seg_tiles(segcap) + 1);
   rc |= dalloc(&t->bsum64, dev::seg_tiles(n) + 1);
   rc |= dalloc(&t->seg_start, segcap + 1);
+  rc |= dalloc(&t->seg_end, segcap);
   rc |= dalloc(&t->seg_page, segcap);
   rc |= dalloc(&t->seg_T, segcap);
   rc |= dalloc(&t->seg_P, segcap);
@@ -885,7 +887,6 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->sum, t->cap_pages * kSumBytes);
   rc |= dalloc(&t->oslot, n);
   rc |= dalloc(&t->pnew, t->cap_pages);
-  rc |= dalloc(&t->seg_full, segcap);
   rc |= dalloc(&t->ctl, 1);
   rc |= dalloc(&t->spl_seg, segcap);
   rc |= dalloc(&t->spl_base, segcap);

@@ -18,8 +18,8 @@
 //     entry, not the page: write_page_and_unlock(update_addr, ...),
 //     Tree.cpp:915-920); the words are released when the chunk retires.
 // Overwrites of keys a page holds were applied in place by k_locate (oslot
-// bit 31); a segment made only of those (seg_full = 0) is neither locked nor
-// staged here, and a staged segment skips them in its op loop.
+// bit 31); the segment list holds only pages that get a new key
+// (launch_segment), and a segment skips the overwrites in its op loop.
 // A segment whose page would reach 54 entries (the split point,
 // Tree.cpp:914) is left untouched and flagged seg_P = ceil(T / 36) for the
 // k-way split of insert.hip (k_upper), which also learns here how many new
@@ -49,7 +49,7 @@ namespace {
 template <int G>
 __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t* buf,
                                                 uint64_t g0, uint32_t num_seg, uint64_t page,
-                                                bool pok, bool full, bool locked, uint32_t qst,
+                                                bool pok, bool locked, uint32_t qst,
                                                 uint32_t qen, uint64_t pk, uint64_t pv,
                                                 uint32_t po) {
   constexpr int L = kWave / G;                       // lanes per page
@@ -69,9 +69,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   const uint32_t fver = h2 & 0xFF;
   const uint64_t lowest = (uint64_t)h7 | ((uint64_t)h8 << 32);
   const uint64_t highest = (uint64_t)h9 | ((uint64_t)h10 << 32);
-  const bool qown = (shfl32(pok ? 1u : 0u, q) != 0) && locked;
-  const bool qfull = shfl32(full ? 1u : 0u, q) != 0;
-  const bool qpok = qown && qfull;  // a staged page (buf slot q holds it)
+  const bool qpok = (shfl32(pok ? 1u : 0u, q) != 0) && locked;  // buf slot q holds it
   const bool cons = leftmost == 0 && fver == (z & 0xFF);
   if (ballot(qpok && !cons)) err |= kErrInconsistent;
   const uint64_t qpage = shfl64(page, q);
@@ -244,13 +242,12 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   uint32_t err = 0;
 
   // segment record of group gg for lane s < G (raw loads, used later)
-  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en, uint32_t& fl) {
+  auto rec = [&](uint64_t gg, uint64_t& page, uint32_t& st, uint32_t& en) {
     const bool sl = gg < ngroups && lane < G && gg * G + (uint64_t)lane < num_seg;
     const uint64_t gs = sl ? gg * G + (uint64_t)lane : 0;
     page = sl ? a.seg_page[gs] : 0;
     st = sl ? a.seg_start[gs] : 0u;
-    en = sl ? a.seg_start[gs + 1] : 0u;
-    fl = sl ? (uint32_t)a.seg_full[gs] : 0u;
+    en = sl ? a.seg_end[gs] : 0u;
   };
   // a loaded record -> page validity, the page's lock word, slot ranges, op
   // prefetch, page DMAs.  lock_and_read_page (Tree.cpp:205-242, 851-852):
@@ -258,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   // take_word; a smaller value is a retired chunk's hold, the same tag a
   // shared hold) in the same round trip as the page DMA; its old value is
   // checked before the page is used
-  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t fl, uint32_t b,
+  auto stage = [&](uint64_t gg, uint64_t page, uint32_t st, uint32_t en, uint32_t b,
                    bool& pok, uint64_t& lkold, uint32_t& qst, uint32_t& qen, uint64_t& pk,
                    uint64_t& pv, uint32_t& po) {
     const bool sl = lane < G && gg * G + (uint64_t)lane < num_seg;
@@ -266,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     if (ballot(sl && !pgok)) err |= kErrBadPtr;
     pok = pgok;
     lkold = 0;
-    if (pgok && fl)  // overwrite-only segments were locked by k_locate
+    if (pgok)
       lkold = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +
                             cityhash64_u64(page) % a.num_locks,
                         (unsigned long long)a.tag);
@@ -277,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     pv = pf ? a.op_val[qst + (uint32_t)li] : 0;
     po = pf ? a.oslot[qst + (uint32_t)li] : 0u;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer b's reads are done
-    const uint64_t dma = ballot(pgok && fl != 0);  // pages with a new key
+    const uint64_t dma = ballot(pgok);
 #pragma unroll
     for (int s = 0; s < G; ++s)
       if ((dma >> s) & 1)
@@ -285,14 +282,14 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   };
 
   uint64_t c_page, n_page, c_lk;
-  uint32_t c_st, c_en, c_fl, n_st, n_en, n_fl;
+  uint32_t c_st, c_en, n_st, n_en;
   bool c_pok;
   uint32_t c_qst, c_qen;
   uint64_t c_pk, c_pv;
   uint32_t c_po;
-  rec(g, c_page, c_st, c_en, c_fl);
-  stage(g, c_page, c_st, c_en, c_fl, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv, c_po);
-  rec(g + W, n_page, n_st, n_en, n_fl);
+  rec(g, c_page, c_st, c_en);
+  stage(g, c_page, c_st, c_en, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv, c_po);
+  rec(g + W, n_page, n_st, n_en);
   for (uint32_t it = 0;; ++it) {
     wait_vm<0>();  // group g's pages, lock words and ops, group g + W's records
     const uint32_t b = it & 1u;
@@ -303,21 +300,20 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     uint64_t x_pk = 0, x_pv = 0;
     uint32_t x_po = 0;
     uint64_t m_page = 0;
-    uint32_t m_st = 0, m_en = 0, m_fl = 0;
+    uint32_t m_st = 0, m_en = 0;
     // a word held by a later tag is not this chunk's to take (never in a
     // serialised tree: reported as a lock failure, the segment left as is)
     const bool held = c_lk <= a.tag;
     if (ballot(c_pok && !held)) err |= kErrLock;
     if (gn < ngroups) {  // wave-uniform
-      stage(gn, n_page, n_st, n_en, n_fl, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv, x_po);
-      rec(gn + W, m_page, m_st, m_en, m_fl);
+      stage(gn, n_page, n_st, n_en, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv, x_po);
+      rec(gn + W, m_page, m_st, m_en);
     }
     err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
-                          c_fl != 0, true, c_qst, c_qen, c_pk, c_pv, c_po);
+                          true, c_qst, c_qen, c_pk, c_pv, c_po);
     if (gn >= ngroups) break;
     g = gn;
     c_page = n_page;
-    c_fl = n_fl;
     c_pok = x_pok;
     c_lk = x_lk;
     c_qst = x_qst;
@@ -328,7 +324,6 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     n_page = m_page;
     n_st = m_st;
     n_en = m_en;
-    n_fl = m_fl;
   }
   if (err) atomicOr(a.err, err);
 }

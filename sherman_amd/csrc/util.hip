@@ -66,25 +66,37 @@ __device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, u
 }
 }  // namespace
 
+// Only segments whose page gets a new key (pnew[page] == tag, set by
+// k_locate) need the upsert and split kernels: the others were applied in
+// place by k_locate.  The list holds just those ("staged" segments), so the
+// later kernels' grids and block ranges cover only them.
+__device__ __forceinline__ bool page_new(const uint32_t* pnew, uint64_t pg, uint32_t tag) {
+  return pnew[ga_offset(pg) >> 10] == tag;
+}
+
 __global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t n,
-                                                  const uint64_t* n_dev, uint32_t* bsum) {
+                                                  const uint64_t* n_dev, uint32_t* bsum,
+                                                  const uint32_t* pnew, uint32_t tag) {
   const uint64_t nv = dev_n(n_dev, n);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint32_t c = 0;
 #pragma unroll
-  for (int j = 0; j < kScanPer; ++j) c += seg_head(page, i0 + j, nv);
+  for (int j = 0; j < kScanPer; ++j)
+    if (seg_head(page, i0 + j, nv)) c += page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
   uint32_t total;
   (void)block_scan<uint32_t>(c, &total);
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// seg_start / seg_page of every head
+// seg_start / seg_end / seg_page of every staged segment: its head writes
+// the start and page, its last op the end (the count of staged heads up to
+// and including it is the segment's position + 1)
 __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint64_t n,
                                                       const uint64_t* n_dev,
                                                       const uint32_t* bsum, uint32_t* seg_start,
-                                                      uint64_t* seg_page, uint32_t* num_seg,
-                                                      const uint32_t* pnew, uint32_t tag,
-                                                      uint8_t* seg_full) {
+                                                      uint32_t* seg_end, uint64_t* seg_page,
+                                                      uint32_t* num_seg, const uint32_t* pnew,
+                                                      uint32_t tag) {
   const uint64_t nv = dev_n(n_dev, n);
   const uint32_t prefix = tiles_before<uint32_t>(bsum, blockIdx.x);
   const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     h[j] = seg_head(page, i0 + j, nv);
+    if (h[j]) h[j] = page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
     c += h[j];
   }
   uint32_t total;
@@ -99,32 +112,28 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = i0 + j;
+    if (i >= nv) break;
+    const uint64_t pg = page[i];
     if (h[j]) {
-      const uint64_t pg = page[i];
       seg_start[pos] = (uint32_t)i;
       seg_page[pos] = pg;
-      seg_full[pos] = pnew[ga_offset(pg) >> 10] == tag ? 1 : 0;
     }
     pos += h[j];
-    if (i + 1 == nv) {
-      *num_seg = pos;
-      seg_start[pos] = (uint32_t)nv;
-    }
+    const bool tail = i + 1 == nv || page[i + 1] != pg;
+    if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
+    if (i + 1 == nv) *num_seg = pos;
   }
-  if (nv == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-    *num_seg = 0;
-    seg_start[0] = 0;
-  }
+  if (nv == 0 && blockIdx.x == 0 && threadIdx.x == 0) *num_seg = 0;
 }
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
-                    uint32_t* seg_start, uint64_t* seg_page, uint32_t* num_seg,
-                    const uint32_t* pnew, uint32_t tag, uint8_t* seg_full, hipStream_t s) {
+                    uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, hipStream_t s) {
   if (!n) return;
   const dim3 g((unsigned)seg_tiles(n));
-  hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum);
+  hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum, pnew, tag);
   hipLaunchKernelGGL(k_seg_fill_scan, g, dim3(kT), 0, s, page, n, n_dev, (const uint32_t*)bsum,
-                     seg_start, seg_page, num_seg, pnew, tag, seg_full);
+                     seg_start, seg_end, seg_page, num_seg, pnew, tag);
 }
 
 template <class T>
