@@ -128,21 +128,31 @@ __device__ __forceinline__ LeafEnt leaf_entry(const uint32_t* lp, int i) {
   e.rraw = (e4 >> 8) & 0xFF;
   return e;
 }
-// write an 18 B entry at its 2-byte aligned slot (9 halfword stores)
+// write an 18 B entry at its 2-byte aligned slot: an even slot starts on a
+// dword (4 dword stores + 1 halfword), an odd one 2 bytes past (1 halfword +
+// 4 dword stores)
 __device__ __forceinline__ void put_leaf_entry(uint32_t* lp, int i,
                                                uint64_t key, uint64_t val,
                                                uint32_t fraw, uint32_t rraw) {
-  uint16_t* h = reinterpret_cast<uint16_t*>(
-      reinterpret_cast<uint8_t*>(lp) + kOffRecords + kLeafEntry * i);
-  h[0] = (uint16_t)((fraw & 0xFF) | ((key & 0xFF) << 8));
-  h[1] = (uint16_t)(key >> 8);
-  h[2] = (uint16_t)(key >> 24);
-  h[3] = (uint16_t)(key >> 40);
-  h[4] = (uint16_t)((key >> 56) | ((val & 0xFF) << 8));
-  h[5] = (uint16_t)(val >> 8);
-  h[6] = (uint16_t)(val >> 24);
-  h[7] = (uint16_t)(val >> 40);
-  h[8] = (uint16_t)((val >> 56) | ((rraw & 0xFF) << 8));
+  uint8_t* b = reinterpret_cast<uint8_t*>(lp) + kOffRecords + kLeafEntry * i;
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  const uint32_t v0 = (uint32_t)val, v1 = (uint32_t)(val >> 32);
+  const uint32_t f = fraw & 0xFF, r = rraw & 0xFF;
+  if ((i & 1) == 0) {  // f k0..k2 | k3..k6 | k7 v0..v2 | v3..v6 | v7 r
+    uint32_t* d = reinterpret_cast<uint32_t*>(b);
+    d[0] = f | (k0 << 8);
+    d[1] = (k0 >> 24) | (k1 << 8);
+    d[2] = (k1 >> 24) | (v0 << 8);
+    d[3] = (v0 >> 24) | (v1 << 8);
+    *reinterpret_cast<uint16_t*>(b + 16) = (uint16_t)((v1 >> 24) | (r << 8));
+  } else {  // f k0 | k1..k4 | k5..k7 v0 | v1..v4 | v5..v7 r
+    *reinterpret_cast<uint16_t*>(b) = (uint16_t)(f | ((k0 & 0xFF) << 8));
+    uint32_t* d = reinterpret_cast<uint32_t*>(b + 2);
+    d[0] = (k0 >> 8) | (k1 << 24);
+    d[1] = (k1 >> 8) | (v0 << 24);
+    d[2] = (v0 >> 8) | (v1 << 24);
+    d[3] = (v1 >> 8) | (r << 24);
+  }
 }
 
 // Header dword d (0..10) of a page image (bytes 0..43); lock word = 0.
@@ -287,12 +297,23 @@ __device__ __forceinline__ void put_leaf_sum(uint8_t* sum, uint64_t page_off, ui
   if (!sum) return;
   uint8_t* line = sum + (page_off >> 10) * kSumBytes;
   const int lane = lane_id();
-  if (lane < kLeafCardinality) line[kSumOffFp + lane] = (uint8_t)fp;
+  if (lane < kLeafCardinality)
+    reinterpret_cast<uint16_t*>(line + kSumOffFp)[lane] = (uint16_t)fp;
   if (lane == 0) {
     *reinterpret_cast<uint64_t*>(line + kSumOffHighest) = highest;
-    *reinterpret_cast<uint64_t*>(line + kSumOffSibling) = sibling;
+    *reinterpret_cast<uint32_t*>(line + kSumOffSibling) = sibling ? dir_page_index(sibling) : 0u;
     line[0] = kSumLeaf;
   }
+}
+// clear slot s's fingerprint (the slot became empty)
+__device__ __forceinline__ void clear_leaf_fp(uint8_t* sum, uint64_t page_off, int s) {
+  if (sum) reinterpret_cast<uint16_t*>(sum + (page_off >> 10) * kSumBytes + kSumOffFp)[s] = 0;
+}
+// set slot s's fingerprint (a new key took the slot)
+__device__ __forceinline__ void set_leaf_fp(uint8_t* sum, uint64_t page_off, int s, uint64_t k) {
+  if (sum)
+    reinterpret_cast<uint16_t*>(sum + (page_off >> 10) * kSumBytes + kSumOffFp)[s] =
+        (uint16_t)key_fp(k);
 }
 
 // ---- per-lane leaf access (the summary walk, the update matcher) --------------
@@ -320,25 +341,32 @@ __device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f
   return key == k && val != kValueNull && ((f ^ r) & 0xF) == 0;
 }
 
-// 4 bits: the bytes of x equal to the fingerprint pattern fq
-__device__ __forceinline__ uint32_t fp_bytes(uint32_t x, uint32_t fq) {
-  const uint32_t y = x ^ fq;
-  const uint32_t z = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y)) & 0x80808080u;
-  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-
-
-// the slots of a leaf summary line (dwords 4..19 as l1..l4) whose
-// fingerprint equals k's: bit s for slot s
-__device__ __forceinline__ uint64_t sum_candidates(const u32x4 l1, const u32x4 l2, const u32x4 l3,
-                                                   const u32x4 l4, uint64_t k) {
-  const uint32_t fq = key_fp(k) * 0x01010101u;
-  const uint32_t dw[14] = {l1.z, l1.w, l2.x, l2.y, l2.z, l2.w, l3.x,
-                           l3.y, l3.z, l3.w, l4.x, l4.y, l4.z, l4.w};
+// A leaf's summary line read whole (one 128 B request): false if it does not
+// describe a current leaf; else its highest fence, sibling and the slots
+// whose 16-bit fingerprint equals k's (bit s for slot s)
+struct SumLine {
+  uint64_t highest, sibling, cand;
+};
+__device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, uint16_t node,
+                                         uint64_t k, SumLine& o) {
+  const u32x4* line = reinterpret_cast<const u32x4*>(sum + (page_off >> 10) * kSumBytes);
+  u32x4 l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) l[j] = line[j];
+  if ((l[0].x & 0xFF) != kSumLeaf) return false;
+  o.sibling = l[0].y ? dir_page_ga(l[0].y, node) : 0;
+  o.highest = (uint64_t)l[0].z | ((uint64_t)l[0].w << 32);
+  const uint32_t fq = key_fp(k);
   uint64_t cand = 0;
 #pragma unroll
-  for (int d = 0; d < 14; ++d) cand |= (uint64_t)fp_bytes(dw[d], fq) << (4 * d);
-  return cand & ((1ull << kLeafCardinality) - 1);
+  for (int d = 0; d < kLeafCardinality / 2; ++d) {  // dwords 4..30: two slots each
+    const u32x4 v = l[1 + d / 4];
+    const uint32_t x = (d & 3) == 0 ? v.x : (d & 3) == 1 ? v.y : (d & 3) == 2 ? v.z : v.w;
+    cand |= (uint64_t)((x & 0xFFFFu) == fq) << (2 * d);
+    cand |= (uint64_t)((x >> 16) == fq) << (2 * d + 1);
+  }
+  o.cand = cand;
+  return true;
 }
 
 }  // namespace dev

@@ -300,8 +300,8 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 // ---- the summary walk: lane = query ------------------------------------------
 //
 // Per get, three HBM lines instead of a 1 KB page: the leaf-directory entry,
-// the leaf's summary line (layout.h: fences, one fingerprint byte per slot)
-// and the entries whose fingerprint matches (false positives ~ 53 / 255).
+// the leaf's summary line (layout.h: fences, a 16-bit fingerprint per slot)
+// and the entries whose fingerprint matches (false positives ~ 53 / 65535).
 // A stale directory is fixed by turning right on k >= highest from the
 // summary (B-link).  Pages without a summary (internal pages: a directory
 // miss, or no directory) are walked from their own bytes, lane by lane:
@@ -333,21 +333,17 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
       }
       const uint64_t off = ga_offset(ptr);
       const uint8_t* page = a.arena + off;
-      const u32x4* line = reinterpret_cast<const u32x4*>(a.sum + (off >> 10) * kSumBytes);
-      const u32x4 l0 = line[0];
-      if ((l0.x & 0xFF) == kSumLeaf) {
-        const u32x4 l1 = line[1], l2 = line[2], l3 = line[3], l4 = line[4];
-        const uint64_t highest = (uint64_t)l0.z | ((uint64_t)l0.w << 32);
-        const uint64_t sibling = (uint64_t)l1.x | ((uint64_t)l1.y << 32);
-        if (k >= highest) {  // turn right (Tree.cpp:626-629)
-          if (!sibling) {
+      SumLine sl;
+      if (sum_read(a.sum, off, a.node, k, sl)) {
+        if (k >= sl.highest) {  // turn right (Tree.cpp:626-629)
+          if (!sl.sibling) {
             err |= kErrFence;
             break;
           }
-          ptr = sibling;
+          ptr = sl.sibling;
           continue;
         }
-        uint64_t cand = sum_candidates(l1, l2, l3, l4, k);
+        uint64_t cand = sl.cand;
         while (cand) {
           uint64_t ek, ev;
           uint32_t ef, er;

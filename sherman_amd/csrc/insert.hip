@@ -523,7 +523,7 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
       const uint32_t f = ((e.fraw & 0xF) + 1) & 0xF;
       put_leaf_entry(reinterpret_cast<uint32_t*>(a.arena + ga_offset(ptr)), lane, k, kValueNull,
                      (e.fraw & 0xF0) | f, (e.rraw & 0xF0) | f);
-      if (a.sum) a.sum[(ga_offset(ptr) >> 10) * kSumBytes + kSumOffFp + lane] = 0;  // empty
+      clear_leaf_fp(a.sum, ga_offset(ptr), lane);  // empty
     }
     wave_lds_sync();
     break;

@@ -67,18 +67,20 @@ SHM_HD int hw_dma_lanes(uint32_t hw) {
 // Leaf summary (a side line per arena page, 128 B, not part of the page
 // bytes): what a get needs of a leaf in one HBM line instead of the page's
 // 1 KB.  Byte 0 = kSumLeaf while the line describes the current leaf (0 for
-// internal pages and pages never written as leaves); highest fence and
-// sibling pointer at 8 / 16; fp[slot] at 24 + slot = key_fp of the slot's key
-// for a valid slot (value != 0), 0 for an empty one.  A get reads the line,
-// turns right on k >= highest, and reads only the entries whose fp matches
-// (false positives ~ 53 / 255 per leaf); every leaf writer keeps the line.
+// internal pages and pages never written as leaves); the sibling as a page
+// index (u32, 0 = none: page 0 is the superblock) at 4, the highest fence at
+// 8; fp[slot] (u16) at 16 + 2 slot = key_fp of the slot's key for a valid
+// slot (value != 0), 0 for an empty one.  A get reads the line, turns right
+// on k >= highest, and reads only the entries whose fp matches (false
+// positives ~ 53 / 65535 per leaf); every leaf writer keeps the line.
 constexpr uint32_t kSumBytes = 128;
+constexpr uint32_t kSumOffSibling = 4;
 constexpr uint32_t kSumOffHighest = 8;
-constexpr uint32_t kSumOffSibling = 16;
-constexpr uint32_t kSumOffFp = 24;
+constexpr uint32_t kSumOffFp = 16;
 constexpr uint8_t kSumLeaf = 0xA5;
+static_assert(kSumOffFp + 2 * kLeafCardinality <= kSumBytes, "summary line");
 SHM_HD uint32_t key_fp(uint64_t k) {
-  const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56);
+  const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 48);
   return f ? f : 1u;
 }
 

@@ -48,6 +48,8 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   const uint64_t n = a.n_dev ? *a.n_dev : a.n;
   if (i >= n) return;
   const uint64_t k = a.keys[i];
+  const bool match = a.out_slot != nullptr && a.target_level == 0;
+  const uint64_t v = match ? a.vals[i] : 0;  // with the key: the update needs no later load
   uint64_t ptr = a.root;
   if (a.dir && a.target_level == 0)
     ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
@@ -55,7 +57,6 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   int retries = 0;
   uint64_t out = 0;
   uint32_t slot = 0;
-  const bool match = a.out_slot != nullptr && a.target_level == 0;
   for (int hop = 0;; ++hop) {
     if (hop > kMaxRounds) {
       err |= kErrRounds;
@@ -68,22 +69,18 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
     const uint64_t off = ga_offset(ptr);
     const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + off);
     if (match) {
-      const u32x4* line = reinterpret_cast<const u32x4*>(a.sum + (off >> 10) * kSumBytes);
-      const u32x4 l0 = line[0];
-      if ((l0.x & 0xFF) == kSumLeaf) {
-        const u32x4 l1 = line[1], l2 = line[2], l3 = line[3], l4 = line[4];
-        const uint64_t highest = (uint64_t)l0.z | ((uint64_t)l0.w << 32);
-        const uint64_t sibling = (uint64_t)l1.x | ((uint64_t)l1.y << 32);
-        if (k >= highest) {  // turn right (Tree.cpp:626-629)
-          if (!sibling) {
+      SumLine sl;
+      if (sum_read(a.sum, off, a.node, k, sl)) {
+        if (k >= sl.highest) {  // turn right (Tree.cpp:626-629)
+          if (!sl.sibling) {
             err |= kErrFence;
             break;
           }
-          ptr = sibling;
+          ptr = sl.sibling;
           continue;
         }
         out = ptr;
-        uint64_t cand = sum_candidates(l1, l2, l3, l4, k);
+        uint64_t cand = sl.cand;
         // a possible update: the page's lock word is taken in the same round
         // trip as the entry reads (a false candidate leaves a hold of this
         // chunk's tag, which the upsert shares)
@@ -102,7 +99,7 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
               err |= kErrLock;
             } else {
               const uint32_t nf = ((ef & 0xF) + 1) & 0xF;
-              put_leaf_entry(const_cast<uint32_t*>(pg), sl, k, a.vals[i], (ef & 0xF0) | nf,
+              put_leaf_entry(const_cast<uint32_t*>(pg), sl, k, v, (ef & 0xF0) | nf,
                              (er & 0xF0) | nf);
               slot = 0x80000000u | (uint32_t)sl;
             }

@@ -5,101 +5,240 @@
 // The count pass stages each scan's first stage_cap values; the fill pass
 // then copies the scans that fit and walks only the longer ones again.
 //
-// One wave per scan.  The start leaf comes from the leaf directory (or a
-// descent from the covering internal page / the root with a ballot child
-// select); B-link right turns fix a stale start.  Along the leaf chain the
-// sibling page is loaded into registers as soon as the current header says
-// the scan continues, so its HBM latency overlaps the current leaf's compare
-// and store.  offsets == nullptr -> count only.
+// Four scans per wave, 16 lanes per scan.  A scan is a chain of dependent
+// page reads (start leaf, then its siblings), so a wave that walks one scan
+// waits on one page at a time; four independent chains per wave put four
+// times the page reads in flight at the same occupancy.  Lane li of scan
+// group q reads 16 B chunks li, li + 16, li + 32, li + 48 of the group's
+// page (256 B coalesced per group per load), stages them in the group's
+// 1 KB LDS slot, and compares 4 consecutive 18 B entries (leaf_chunk.h).
+// The start leaf comes from the leaf directory (or a descent from the
+// covering internal page / the root: 4 separators per lane, the child is
+// the count of separators <= from); B-link right turns fix a stale start.
+// Along the leaf chain the sibling page is loaded into registers as soon as
+// the current header says the scan continues, so its HBM latency overlaps
+// the current leaf's compare and stores.  offsets == nullptr -> count only.
 #include "device_common.h"
 #include "kernels.h"
+#include "leaf_chunk.h"
 
 namespace shm {
 namespace dev {
 
 namespace {
 constexpr int kRangeWaves = 4;
+constexpr int kRG = 4;                        // scans per wave
+constexpr int kRL = kWave / kRG;              // lanes per scan
+constexpr int kRE = 4;                        // leaf entries per lane
+constexpr int kRCD = kLeafEntry * kRE / 4;    // dwords of a lane's entry chunk
+constexpr int kRChunks = kPageSize / 16 / kRL;  // 16 B page chunks per lane
+static_assert(kRL * kRE >= kLeafCardinality, "entries per group");
+
+struct RPage {
+  u32x4 c[kRChunks];
+};
+
+__device__ __forceinline__ void rload(const uint8_t* arena, uint64_t p, int li, RPage& w) {
+  const uint8_t* b = arena + ga_offset(p) + 16 * li;
+#pragma unroll
+  for (int k = 0; k < kRChunks; ++k) w.c[k] = *reinterpret_cast<const u32x4*>(b + 16 * kRL * k);
 }
+__device__ __forceinline__ void rstage(uint32_t* lp, int li, const RPage& w) {
+#pragma unroll
+  for (int k = 0; k < kRChunks; ++k) *reinterpret_cast<u32x4*>(lp + 4 * (li + kRL * k)) = w.c[k];
+}
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* lp, int d) {
+  return (uint64_t)lp[d] | ((uint64_t)lp[d + 1] << 32);
+}
+// header fields of a staged page (Tree.h:130-160; bytes 9..43)
+__device__ __forceinline__ uint64_t hdr_leftmost(const uint32_t* lp) {
+  const uint32_t a2 = lp[2], a3 = lp[3], b0 = lp[4];
+  return (uint64_t)((a2 >> 8) | (a3 << 24)) | ((uint64_t)((a3 >> 8) | (b0 << 24)) << 32);
+}
+__device__ __forceinline__ uint64_t hdr_sibling(const uint32_t* lp) {
+  const uint32_t b0 = lp[4], b1 = lp[5], b2 = lp[6];
+  return (uint64_t)((b0 >> 8) | (b1 << 24)) | ((uint64_t)((b1 >> 8) | (b2 << 24)) << 32);
+}
+// exclusive prefix of v over the 16 lanes of each scan group; *tot = group sum
+__device__ __forceinline__ uint32_t group_scan(uint32_t v, int li, uint32_t* tot) {
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < kRL; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, off, kRL);
+    if (li >= off) incl += y;
+  }
+  *tot = (uint32_t)__shfl((int)incl, kRL - 1, kRL);
+  return incl - v;
+}
+}  // namespace
 
 __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_page[kRangeWaves][kPageDwords + 8];
+  __shared__ __attribute__((aligned(16))) uint32_t s_page[kRangeWaves][kRG * kPageDwords];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const uint64_t q = (uint64_t)blockIdx.x * kRangeWaves + wv;
-  if (q >= a.n) return;  // wave-uniform
-  uint32_t* lp = s_page[wv];
-  const uint64_t lo = a.from[q], hi = a.to[q];
-  uint64_t cnt = 0;
-  const uint64_t out = a.offsets ? a.offsets[q] : 0;
+  const int q = lane / kRL, li = lane % kRL;
+  const uint64_t Q = ((uint64_t)blockIdx.x * kRangeWaves + (uint64_t)wv) * kRG + (uint64_t)q;
+  const bool has = Q < a.n;
+  if (!ballot(has)) return;  // wave-uniform
+  uint32_t* lp = s_page[wv] + q * kPageDwords;
+  uint64_t lo = 0, hi = 0, out = 0;
+  if (has) {
+    lo = a.from[Q];
+    hi = a.to[Q];
+    if (a.offsets) out = a.offsets[Q];
+  }
   uint32_t err = 0;
-  uint64_t* stq = a.stage ? a.stage + q * (uint64_t)a.stage_cap : nullptr;
-  if (a.offsets && stq && a.counts[q] <= a.stage_cap) {
+  uint64_t cnt = 0;
+  uint64_t* stq = (a.stage && has) ? a.stage + Q * (uint64_t)a.stage_cap : nullptr;
+  bool act = has && lo <= hi;
+  bool copied = false;
+  if (a.offsets && stq) {
     // fill pass, staged scan: copy its values out, no second walk
-    const uint64_t c = a.counts[q];
-    for (uint64_t i = (uint64_t)lane; i < c && out + i < a.vals_cap; i += kWave)
-      a.vals[out + i] = stq[i];
-    return;
-  }
-  if (lo <= hi) {
-    uint64_t p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
-    int hops = 0;
-    u32x4 w;
-    // descend to the leaf whose fences hold lo
-    for (;;) {
-      if (++hops > kMaxRounds || !ptr_ok(p, a.node, a.arena_bytes)) {
-        err |= kErrBadPtr;
-        p = 0;
-        break;
-      }
-      w = load_page_slice(a.arena, ga_offset(p));
-      const Hdr h = parse_hdr(w);
-      if (lo >= h.highest && h.sibling) {
-        p = h.sibling;
-        continue;
-      }
-      if (h.leftmost == 0) break;
-      const IntRec r = internal_record(w);
-      const int c = popc64(ballot(lane >= 3 && lane - 3 < h.last_index + 1 && r.key <= lo));
-      p = c == 0 ? h.leftmost : rl64(r.ptr, c + 2);
-    }
-    // scan the leaf chain; w holds leaf p
-    while (p) {
-      const Hdr h = parse_hdr(w);
-      const bool more = h.sibling != 0 && h.highest <= hi;
-      u32x4 wn = w;
-      if (more) {
-        if (++hops > (1 << 24) || !ptr_ok(h.sibling, a.node, a.arena_bytes)) {
-          err |= kErrBadPtr;
-          break;
+    const uint64_t c = a.counts[Q];
+    copied = c <= a.stage_cap;
+    if (copied) {
+      for (uint64_t b = 0; b < c; b += kRL * 4) {
+        uint64_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t i = b + (uint64_t)(li + kRL * u);
+          v[u] = i < c ? stq[i] : 0;
         }
-        wn = load_page_slice(a.arena, ga_offset(h.sibling));  // in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t i = b + (uint64_t)(li + kRL * u);
+          if (i < c && out + i < a.vals_cap) a.vals[out + i] = v[u];
+        }
       }
-      stage_page(lp, w);
-      wave_lds_sync();
-      const LeafEnt e = leaf_entry(lp, lane < kLeafCardinality ? lane : 0);
-      const bool hit = lane < kLeafCardinality && e.val != kValueNull &&
-                       (e.fraw & 0xF) == (e.rraw & 0xF) && e.key >= lo && e.key <= hi;
-      const uint64_t m = ballot(hit);
-      const uint64_t slot = cnt + popc64(m & lanemask_lt());
-      if (a.offsets && hit && out + slot < a.vals_cap) a.vals[out + slot] = e.val;
-      if (!a.offsets && stq && hit && slot < a.stage_cap) stq[slot] = e.val;
-      cnt += popc64(m);
-      wave_lds_sync();  // LDS reads done before the next stage
-      if (!more) break;
-      p = h.sibling;
-      w = wn;
+      act = false;
     }
   }
-  if (lane == 0) {
-    if (err) atomicOr(a.err, err);
-    a.counts[q] = cnt;
+
+  // ---- descend to the leaf whose fences hold lo ------------------------------
+  RPage w;
+  uint64_t p = 0;
+  int hops = 0;
+  if (act) {
+    p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
+    if (!ptr_ok(p, a.node, a.arena_bytes)) {
+      err |= kErrBadPtr;
+      act = false;
+    } else {
+      rload(a.arena, p, li, w);
+    }
   }
+  bool desc = act;
+  while (ballot(desc)) {
+    if (desc) rstage(lp, li, w);
+    wave_lds_sync();
+    if (desc) {
+      const uint64_t sibling = hdr_sibling(lp);
+      const uint64_t highest = lds_u64(lp, 9);
+      const uint64_t leftmost = hdr_leftmost(lp);
+      uint64_t np = 0;
+      if (lo >= highest && sibling) {
+        np = sibling;
+      } else if (leftmost != 0) {
+        // internal page (Tree.cpp:665-685): child = number of keys <= lo
+        const int last = (int)(int16_t)(lp[6] >> 16);
+        uint32_t c = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int j = li + kRL * m;
+          c += (j <= last && j < kInternalCardinality && lds_u64(lp, 11 + 4 * j) <= lo) ? 1u : 0u;
+        }
+        uint32_t tot;
+        (void)group_scan(c, li, &tot);
+        np = tot == 0 ? leftmost : lds_u64(lp, 13 + 4 * ((int)tot - 1));
+      }
+      if (np) {
+        if (++hops > kMaxRounds || !ptr_ok(np, a.node, a.arena_bytes)) {
+          err |= kErrBadPtr;
+          act = false;
+          desc = false;
+        } else {
+          p = np;
+        }
+      } else {
+        desc = false;  // a leaf: w holds it
+      }
+    }
+    wave_lds_sync();  // LDS reads done before the next stage
+    if (desc) rload(a.arena, p, li, w);
+  }
+
+  // ---- scan the leaf chain; w holds leaf p ------------------------------------
+  const int ebase = chunk_base<kRE>(li);
+  while (ballot(act)) {
+    if (act) rstage(lp, li, w);
+    wave_lds_sync();
+    bool more = false;
+    uint64_t sibling = 0;
+    RPage wn = w;
+    bool hit[kRE];
+    uint64_t ev[kRE];
+#pragma unroll
+    for (int j = 0; j < kRE; ++j) {
+      hit[j] = false;
+      ev[j] = 0;
+    }
+    if (act) {
+      sibling = hdr_sibling(lp);
+      const uint64_t highest = lds_u64(lp, 9);
+      more = sibling != 0 && highest <= hi;
+      if (more) {
+        if (++hops > (1 << 24) || !ptr_ok(sibling, a.node, a.arena_bytes)) {
+          err |= kErrBadPtr;
+          more = false;
+        } else {
+          rload(a.arena, sibling, li, wn);  // in flight
+        }
+      }
+      uint32_t D[kRCD];
+      const uint32_t* ep = lp + (kOffRecords + kLeafEntry * ebase) / 4;
+#pragma unroll
+      for (int i = 0; i < kRCD; ++i) D[i] = ep[i];
+      uint64_t ek[kRE];
+      uint32_t ef[kRE], er[kRE];
+      chunk_entries<kRE>(D, ek, ev, ef, er);
+#pragma unroll
+      for (int j = 0; j < kRE; ++j)
+        hit[j] = ebase + j >= li * kRE && ev[j] != kValueNull && ((ef[j] ^ er[j]) & 0xF) == 0 &&
+                 ek[j] >= lo && ek[j] <= hi;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kRE; ++j) c += hit[j] ? 1u : 0u;
+    uint32_t tot;
+    uint64_t slot = cnt + group_scan(c, li, &tot);
+#pragma unroll
+    for (int j = 0; j < kRE; ++j) {
+      if (hit[j]) {
+        if (a.offsets && out + slot < a.vals_cap) a.vals[out + slot] = ev[j];
+        if (!a.offsets && stq && slot < a.stage_cap) stq[slot] = ev[j];
+        ++slot;
+      }
+    }
+    cnt += tot;
+    wave_lds_sync();  // LDS reads done before the next stage
+    if (act) {
+      if (more) {
+        p = sibling;
+        w = wn;
+      } else {
+        act = false;
+      }
+    }
+  }
+  if (has && !copied && li == 0) a.counts[Q] = cnt;
+  if (err) atomicOr(a.err, err);
 }
 
 void launch_range(const RangeArgs& a, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(k_range, dim3((unsigned)((a.n + kRangeWaves - 1) / kRangeWaves)),
-                     dim3(kRangeWaves * kWave), 0, s, a);
+  const uint64_t per = (uint64_t)kRangeWaves * kRG;
+  hipLaunchKernelGGL(k_range, dim3((unsigned)((a.n + per - 1) / per)), dim3(kRangeWaves * kWave),
+                     0, s, a);
 }
 
 // zero-copy read-back (tree.cpp readback): one wave copies the words into

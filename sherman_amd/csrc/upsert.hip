@@ -176,7 +176,6 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   // ---- write back the changed entries of in-place segments -----------------------
   if (live && !over) {
     uint8_t* pg = a.arena + ga_offset(qpage);
-    uint8_t* fp = a.sum ? a.sum + (ga_offset(qpage) >> 10) * kSumBytes + kSumOffFp : nullptr;
 #pragma unroll
     for (int j = 0; j < E; ++j)
       if (dirty[j]) {
@@ -184,7 +183,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         // the leaf summary: an overwrite keeps its key's fingerprint; a new
         // key in an empty slot sets it (one partial line write per page
         // that gained keys, none for pure updates)
-        if (fp && fresh[j]) fp[ebase + j] = (uint8_t)key_fp(ek[j]);
+        if (fresh[j]) set_leaf_fp(a.sum, ga_offset(qpage), ebase + j, ek[j]);
       }
   }
   if (a.leaf_hw) {
