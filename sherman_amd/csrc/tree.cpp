@@ -825,7 +825,10 @@ int shm_config_init(shm_config* c) {
   c->flags = SHM_FLAG_LEAF_DIR | SHM_FLAG_AUTO_SORT_GETS;
   c->arena_bytes = 1ull << 30;
   c->max_batch = 1ull << 20;
-  c->num_locks = 1u << 22;  // 32 MB: rare false sharing between waves
+  // the reference's kNumOfLock (Common.h:87-93): 128 KB of lock words stay
+  // cached at the memory side, where the atomics run (C5 locate 76 -> 69 us
+  // against 4 Mi words; 2^17 measured the same as 2^14)
+  c->num_locks = 16384;
   c->sort_bits = kDefaultSortBits;
   c->key_lo = 0;
   c->key_bits = 64;
