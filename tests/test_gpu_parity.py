@@ -247,6 +247,36 @@ def test_overwrites_write_the_reference_entry_bytes(lib_ok):
     t.close()
 
 
+def test_range_query_async_long_scans_match_sync(lib_ok):
+    """The async scans' one-pass placement (launch_range_place): thousands of
+    scans over many placement blocks, with scans longer than their staging
+    (> 160 values: walked again from the overflow list) mixed with short and
+    empty ones; counts, offsets and values equal the synchronous call's."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 14)
+    ks = hashed_keys(1, 60001)
+    gpu_insert(t, ks, ks + U64(5))
+    rng = np.random.default_rng(23)
+    n = 3000
+    lo = rng.integers(0, 1 << 63, n, dtype=np.uint64) * U64(2)
+    # ~0-60 keys per scan, every 97th scan ~ 200-600 keys, a few whole-space
+    span = (U64(1) << U64(52)) * rng.integers(0, 16, n).astype(U64)
+    span[::97] = (U64(1) << U64(57)) * rng.integers(1, 4, span[::97].size).astype(U64)
+    hi = lo + span
+    hi[hi < lo] = U64((1 << 64) - 1)
+    lo[5], hi[5] = U64(0), U64((1 << 64) - 1)
+    lo[6], hi[6] = U64(9), U64(8)  # empty
+    sc, sv = t.range_query_batch(dev(lo), dev(hi))
+    scn = sc.cpu().numpy()
+    assert (scn > 160).sum() >= 20 and scn[5] == ks.size
+    pend = t.range_query_batch_async(dev(lo), dev(hi))
+    assert pend.tot is not None
+    ac, av = pend.result()
+    assert np.array_equal(ac.cpu().numpy(), scn)
+    assert np.array_equal(host(av), host(sv))
+    t.check()
+    t.close()
+
+
 @pytest.mark.parametrize("max_batch,cap,leaf_dir", [(1 << 17, None, True),
                                                     (128, 16, True),
                                                     (1 << 17, None, False)])
