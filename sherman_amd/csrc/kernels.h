@@ -271,14 +271,15 @@ void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64
                     hipStream_t s);
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
                       uint64_t* out, uint8_t* found, hipStream_t s);
-// fixed-capacity exchange (shard.cpp): pack a bucketed batch into P runs of
-// cap slots (kKeyMax padding; a longer run sets kErrOverflow in *err), and
-// unpack P runs of results back to input order
-void launch_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P, uint64_t cap,
-                       uint64_t* out, uint32_t* err, hipStream_t s);
-void launch_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P, uint64_t cap,
-                         const uint32_t* perm, uint64_t n, uint64_t* out, uint8_t* found,
-                         hipStream_t s);
+// fixed-capacity get exchange (shard.cpp): keys straight into P runs of cap
+// slots (kKeyMax padding; spos[i] = input i's slot, ~0 and kErrOverflow in
+// *err when its run is full; cursor = P words of scratch), and the results
+// gathered back to input order
+void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
+                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint32_t* err,
+                        hipStream_t s);
+void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
+                         uint8_t* found, hipStream_t s);
 
 // ---- batched range scans (range.hip) -------------------------------------------
 struct RangeArgs {

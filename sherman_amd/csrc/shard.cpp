@@ -8,16 +8,16 @@
 // One exchange each way per batch, over RCCL (xGMI between the GPUs of a
 // node):
 //
-//   search : bucket keys by owner (stable, shm_route_bucket) -> pack each
-//            peer's run into a fixed-capacity slot (cap = 1.25 n / P + 256,
-//            kKeyMax padding) -> ncclAllToAll of the slots -> local batched
-//            get over all received slots (a kKeyMax finds nothing) ->
-//            ncclAllToAll of the results back -> unpack to input order
-//            (found = value != 0, Tree.cpp:445-448).  No count exchange and no
-//            host wait: the whole routed get is queued on the stream.  A run
-//            longer than its slot (keys far from uniform over the shards) is
-//            cut and reported as kErrOverflow at the tree's next
-//            synchronising call.
+//   search : every key straight into its owner's run of fixed-capacity
+//            slots (cap = 1.25 n / P + 256, kKeyMax padding; a per-peer
+//            cursor places it, spos records where) -> ncclAllToAll of the
+//            slots -> local batched get over all received slots (a kKeyMax
+//            finds nothing) -> ncclAllToAll of the results back -> gather to
+//            input order through spos (found = value != 0, Tree.cpp:445-448).
+//            No count exchange, no bucketing pass and no host wait: the whole
+//            routed get is queued on the stream.  A key whose run is full
+//            (keys far from uniform over the shards) finds nothing and is
+//            reported as kErrOverflow at the tree's next synchronising call.
 //   insert : the same bucketing, the values permuted alongside, keys and
 //            values exchanged, then a local insert queued without a host
 //            wait; received runs arrive in source-rank order and bucketing
@@ -53,7 +53,7 @@ struct Slot {
   uint64_t* cnts = nullptr;   // device: send counts [P], receive counts [P]
   uint64_t* kb = nullptr;     // keys bucketed by owner
   uint64_t* vb = nullptr;     // insert values, permuted alongside
-  uint32_t* perm = nullptr;   // source position of kb[i]
+  uint32_t* perm = nullptr;   // insert: source position of kb[i]; get: slot of input i
   uint64_t* rk = nullptr;     // received keys
   uint64_t* rv = nullptr;     // received insert values / local get results
   uint64_t* back = nullptr;   // results returned to this rank (bucketed order)
@@ -277,14 +277,13 @@ int shm_shard_search_begin(shm_shard* h, const uint64_t* keys, uint64_t n, void*
   s.busy = true;
   *ticket = (uint32_t)i;
   const uint32_t P = h->world;
-  int rc = shm_route_bucket(h->local, s.keys, s.n, P, s.cnts, s.kb, s.perm, s.stream);
   s.ncap = P == 1 ? n : std::min<uint64_t>(s.pcap, (n + n / 4) / P + 256);
-  if (rc == SHM_OK) {
-    shm::dev::launch_route_pack(s.kb, s.cnts, P, s.ncap, s.pk, shm__error_word(h->local),
-                                s.stream);
+  shm::dev::launch_route_slots(s.keys, s.n, P, s.ncap, reinterpret_cast<uint32_t*>(s.cnts), s.pk,
+                               s.perm, shm__error_word(h->local), s.stream);
+  int rc = hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+  if (rc == SHM_OK)
     rc = nccl_ok(ncclAllToAll(s.pk, s.pr, s.ncap, ncclUint64, s.comm, s.stream),
                  "ncclAllToAll(keys)");
-  }
   if (rc) s.busy = false;
   return rc;
 }
@@ -299,8 +298,7 @@ int shm_shard_search_end(shm_shard* h, uint32_t ticket, uint64_t* vals_out, uint
   if (rc) return rc;
   // the results go back the way the keys came, slot for slot
   NCCL_OK(ncclAllToAll(s.pv, s.pb, s.ncap, ncclUint64, s.comm, s.stream));
-  shm::dev::launch_route_unpack(s.pb, s.cnts, P, s.ncap, s.perm, s.n, vals_out, found_out,
-                                s.stream);
+  shm::dev::launch_route_gather(s.pb, s.perm, s.n, vals_out, found_out, s.stream);
   return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
 }
 

@@ -252,15 +252,15 @@ __global__ __launch_bounds__(1024) void k_route_scan(uint32_t* __restrict__ cm, 
   for (uint32_t b = b0; b < b1; ++b) sum += cm[(uint64_t)b * shards + sh];
   if (live) part[q * shards + sh] = sum;
   __syncthreads();
-  if (t < shards) {
-    uint32_t acc = 0;
-    for (uint32_t x = 0; x < Q; ++x) {
-      const uint32_t v = part[x * shards + t];
-      part[x * shards + t] = acc;
-      acc += v;
-    }
-    off[t] = acc;  // shard total for now
+  // per shard, inclusive scan of the slice sums over q (log2 Q steps)
+  uint32_t incl = sum;
+  for (uint32_t d = 1; d < Q; d <<= 1) {
+    const uint32_t add = (live && q >= d) ? part[(q - d) * shards + sh] : 0u;
+    __syncthreads();
+    if (live) part[q * shards + sh] = (incl += add);
+    __syncthreads();
   }
+  if (live && q == Q - 1) off[sh] = incl;  // shard total for now
   __syncthreads();
   if (t == 0) {
     uint32_t acc = 0;
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(1024) void k_route_scan(uint32_t* __restrict__ cm, 
   }
   __syncthreads();
   if (live) {
-    uint32_t run = off[sh] + part[q * shards + sh];
+    uint32_t run = off[sh] + incl - sum;
     for (uint32_t b = b0; b < b1; ++b) {
       const uint64_t o = (uint64_t)b * shards + sh;
       const uint32_t v = cm[o];
@@ -374,53 +374,118 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
   if (n) hipLaunchKernelGGL(k_unpermute, grid1(n), dim3(kT), 0, s, in, perm, n, out, found);
 }
 
-// ---- fixed-capacity exchange (shard.cpp): no host-known counts ----------------
-// peer p's run of a bucketed batch starts at the sum of counts[0..p)
-__device__ __forceinline__ uint64_t peer_off(const uint64_t* counts, uint32_t p) {
-  uint64_t o = 0;
-  for (uint32_t q = 0; q < p; ++q) o += counts[q];
-  return o;
+// ---- fixed-capacity get exchange (shard.cpp): no host-known counts ------------
+// Peer p's keys go to slot run [p * cap, (p + 1) * cap) of the send buffer,
+// the rest of the run kKeyMax (a get of kKeyMax finds nothing).  A key's
+// place in its run comes from a per-peer cursor (one atomic per peer present
+// in a wave), so no bucketing pass, scan or pack is needed; the order inside
+// a run does not matter, since spos[i] records where input i went and the
+// results are gathered back from the same places.
+__global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t n, uint32_t* cursor,
+                                                   uint32_t P) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i == 0)
+    for (uint32_t p = 0; p < P; ++p) cursor[p] = 0;
+  if (2 * i + 1 < n) {
+    *reinterpret_cast<u32x4*>(out + 2 * i) = u32x4{~0u, ~0u, ~0u, ~0u};
+  } else if (2 * i < n) {
+    out[2 * i] = kKeyMax;
+  }
 }
 
-// out[p * cap + j] = kb[off_p + j] for j < counts[p], kKeyMax after (a get
-// of kKeyMax finds nothing); a run longer than cap is cut and reported
-__global__ void k_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P,
-                             uint64_t cap, uint64_t* out, uint32_t* err) {
-  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= (uint64_t)P * cap) return;
-  const uint32_t p = (uint32_t)(x / cap);
-  const uint64_t j = x - (uint64_t)p * cap;
-  const uint64_t c = counts[p];
-  out[x] = j < c ? kb[peer_off(counts, p) + j] : kKeyMax;
-  if (j == 0 && c > cap) atomicOr(err, kErrOverflow);
-}
-void launch_route_pack(const uint64_t* kb, const uint64_t* counts, uint32_t P, uint64_t cap,
-                       uint64_t* out, uint32_t* err, hipStream_t s) {
-  const uint64_t n = (uint64_t)P * cap;
-  if (n) hipLaunchKernelGGL(k_route_pack, grid1(n), dim3(kT), 0, s, kb, counts, P, cap, out, err);
+// A block places 4096 keys (16 per thread): per round and wave, ranks among
+// the lanes of one owner by ballots (as k_route_scatter); per owner, ONE
+// global cursor claim for the whole block (a cursor word claimed per wave
+// serialises ~16 K atomics on one address per batch: 270 us at world 1)
+constexpr int kSlotPer = 16;
+constexpr int kSlotTile = kT * kSlotPer;
+
+__global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__ keys, uint64_t n,
+                                                    uint32_t P, uint64_t cap,
+                                                    uint32_t* __restrict__ cursor,
+                                                    uint64_t* __restrict__ out,
+                                                    uint32_t* __restrict__ spos, uint32_t* err) {
+  constexpr int kW = kT / kWave;
+  __shared__ uint32_t wc[kSlotPer][kW][kRouteMaxShards];
+  const int t = threadIdx.x, w = t >> 6, lane = lane_id();
+  for (int j = t; j < kSlotPer * kW * kRouteMaxShards; j += kT) (&wc[0][0][0])[j] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kSlotTile;
+  uint64_t kk[kSlotPer];
+  uint32_t own[kSlotPer], rank[kSlotPer];
+#pragma unroll
+  for (int r = 0; r < kSlotPer; ++r) {
+    const uint64_t i = base + (uint64_t)r * kT + t;
+    const bool valid = i < n;
+    kk[r] = valid ? keys[i] : 0;
+    own[r] = valid ? owner_of(kk[r], P) : ~0u;
+    rank[r] = 0;
+    uint64_t pending = ballot(valid);
+    while (pending) {  // one pass per owner present in this wave
+      const uint32_t o = rl32(own[r], ctz64(pending));
+      const uint64_t m = ballot(own[r] == o);
+      if (own[r] == o) rank[r] = popc64(m & lanemask_lt());
+      if (lane == 0) wc[r][w][o] = popc64(m);
+      pending &= ~m;
+    }
+  }
+  __syncthreads();
+  if ((uint32_t)t < P) {  // the block's claim on owner t's run, then (round, wave) bases
+    uint32_t tot = 0;
+    for (int r = 0; r < kSlotPer; ++r)
+      for (int x = 0; x < kW; ++x) tot += wc[r][x][t];
+    uint32_t run = tot ? atomicAdd(cursor + t, tot) : 0u;
+    for (int r = 0; r < kSlotPer; ++r)
+      for (int x = 0; x < kW; ++x) {
+        const uint32_t v = wc[r][x][t];
+        wc[r][x][t] = run;
+        run += v;
+      }
+  }
+  __syncthreads();
+  bool over = false;
+#pragma unroll
+  for (int r = 0; r < kSlotPer; ++r) {
+    if (own[r] == ~0u) continue;
+    const uint64_t i = base + (uint64_t)r * kT + t;
+    const uint32_t pos = wc[r][w][own[r]] + rank[r];
+    if (pos < cap) {
+      const uint64_t x = (uint64_t)own[r] * cap + pos;
+      out[x] = kk[r];
+      spos[i] = (uint32_t)x;
+    } else {  // this peer's run is full: reported, the key finds nothing
+      spos[i] = ~0u;
+      over = true;
+    }
+  }
+  if (over) atomicOr(err, kErrOverflow);
 }
 
-// bucketed position b (peer p, j = b - off_p): out[perm[b]] = in[p * cap + j]
-__global__ void k_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P,
-                               uint64_t cap, const uint32_t* perm, uint64_t n, uint64_t* out,
-                               uint8_t* found) {
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  uint32_t p = 0;
-  uint64_t off = 0;
-  while (p + 1 < P && off + counts[p] <= b) off += counts[p++];
-  const uint64_t j = b - off;
-  const uint64_t v = j < cap ? in[(uint64_t)p * cap + j] : kValueNull;
-  const uint32_t o = perm[b];
-  out[o] = v;
-  if (found) found[o] = v != kValueNull ? 1 : 0;
-}
-void launch_route_unpack(const uint64_t* in, const uint64_t* counts, uint32_t P, uint64_t cap,
-                         const uint32_t* perm, uint64_t n, uint64_t* out, uint8_t* found,
-                         hipStream_t s) {
+void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
+                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint32_t* err,
+                        hipStream_t s) {
+  const uint64_t slots = (uint64_t)P * cap;
+  hipLaunchKernelGGL(k_route_fill, grid1((slots + 1) / 2 + 1), dim3(kT), 0, s, out, slots, cursor,
+                     P);
   if (n)
-    hipLaunchKernelGGL(k_route_unpack, grid1(n), dim3(kT), 0, s, in, counts, P, cap, perm, n, out,
-                       found);
+    hipLaunchKernelGGL(k_route_slots, grid1(n, kSlotTile), dim3(kT), 0, s, keys, n, P, cap, cursor,
+                       out, spos, err);
+}
+
+// out[i] = in[spos[i]] (0 for a key cut by a full run), found[i] = out[i] != 0
+// (Tree.cpp:445-448)
+__global__ void k_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n,
+                               uint64_t* out, uint8_t* found) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = spos[i];
+  const uint64_t v = x != ~0u ? in[x] : kValueNull;
+  out[i] = v;
+  if (found) found[i] = v != kValueNull ? 1 : 0;
+}
+void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
+                         uint8_t* found, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_route_gather, grid1(n), dim3(kT), 0, s, in, spos, n, out, found);
 }
 
 }  // namespace dev
