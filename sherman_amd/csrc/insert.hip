@@ -564,6 +564,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   stamp();
   Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
   uint64_t cursor = sb->next_page;
+  const uint64_t cursor0 = cursor;
   uint32_t root_level = (uint32_t)sb->root_level;
   const uint64_t cap = sb->capacity_pages;
   uint64_t made = 0;  // pages created by splits
@@ -866,7 +867,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     sb->root_level = root_level;
     sb->splits += made;
     sb->batches = a.batch;
-    if (a.pub) {
+    if (a.pub && cursor != cursor0) {  // the host mirror changes only with new pages
       __hip_atomic_store(a.pub + 1, cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.pub + 2, (uint64_t)root_level, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
