@@ -333,4 +333,24 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   return shm_insert_batch_async(h->local, s.rk, s.rv, nrecv, s.stream);
 }
 
+// Library-internal test hooks, not part of include/sherman_amd.h: the routed
+// get's slot placement and result gather for P shards, so the P > 1 path can
+// be checked on one GPU (tests/test_gpu_shard.py) without P ranks.  cursor:
+// P u32 of device scratch; the overflow bit goes to t's error word.
+int shm__route_slots(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
+                     uint32_t* cursor, uint64_t* slots, uint32_t* spos, void* stream) {
+  if (!t || !cursor || !slots || !spos || P == 0 || P > 64 || (n && !keys) ||
+      (uint64_t)P * cap >= ~0u)
+    return SHM_EINVAL;
+  shm::dev::launch_route_slots(keys, n, P, cap, cursor, slots, spos, shm__error_word(t),
+                               (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+}
+int shm__route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* vals_out,
+                      uint8_t* found_out, void* stream) {
+  if (n && (!in || !spos || !vals_out)) return SHM_EINVAL;
+  shm::dev::launch_route_gather(in, spos, n, vals_out, found_out, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+}
+
 }  // extern "C"

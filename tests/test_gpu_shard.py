@@ -110,3 +110,89 @@ def test_routed_gpu_shards_match_unsharded_oracle(backend, world, cabi):
         mp.spawn(gpu_worker, args=(world, free_port(), d, backend, cabi), nprocs=world,
                  join=True)
         verify_against_unsharded(d, world)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_slot_routed_get_p_shards_on_one_gpu(P):
+    """The C-ABI shard's get placement for P > 1 without P ranks: P trees on
+    cuda:0 (each with its shard's key-range hint), one batch of queries
+    (hits, misses, a duplicate, key 0) placed into P runs of fixed-capacity
+    slots (shm__route_slots), run p searched by tree p -- what the
+    ncclAllToAll hands each rank -- and the results gathered back
+    (shm__route_gather).  Every key lands in its owner's run, the runs'
+    tails are kKeyMax, and the gathered values equal the unsharded dict.  A
+    too-small capacity cuts the overflowing keys (they find nothing) and
+    reports kErrOverflow."""
+    import ctypes
+
+    import sherman_amd as shm
+    from sherman_amd.shard import owner_of, shard_range
+
+    L = shm.lib()
+    L.shm__route_slots.restype = ctypes.c_int
+    L.shm__route_slots.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                   ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.shm__route_gather.restype = ctypes.c_int
+    L.shm__route_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(100 + P)
+    keys = np.unique(rng.integers(1, (1 << 64) - 2, 30000, dtype=np.uint64))
+    vals = keys ^ U64(0x5555)
+    trees = []
+    own = owner_of(torch.from_numpy(keys.view(np.int64)), P).numpy()
+    for p in range(P):
+        lo, bits = shard_range(p, P)
+        t = shm.Tree(arena_bytes=32 << 20, max_batch=1 << 15, node_id=p, key_lo=lo,
+                     key_bits=bits)
+        kp = keys[own == p]
+        t.insert_batch(torch.from_numpy(kp.view(np.int64)).to(dev),
+                       torch.from_numpy(vals[own == p].view(np.int64)).to(dev))
+        trees.append(t)
+    q = np.concatenate([keys[rng.integers(0, keys.size, 20000)],
+                        rng.integers(1, (1 << 64) - 2, 5000, dtype=np.uint64),  # misses
+                        keys[:1], keys[:1], np.array([0], dtype=U64)])
+    rng.shuffle(q)
+    n = q.size
+    qd = torch.from_numpy(q.view(np.int64)).to(dev)
+    want = dict(zip(keys.tolist(), vals.tolist()))
+    exp = np.array([want.get(int(x), 0) for x in q], dtype=U64)
+
+    for cap, overflow in (((n + n // 4) // P + 256, False), (n // (2 * P), True)):
+        cursor = torch.zeros(P, dtype=torch.int32, device=dev)
+        slots = torch.empty(P * cap, dtype=torch.int64, device=dev)
+        spos = torch.empty(n, dtype=torch.int32, device=dev)
+        rc = L.shm__route_slots(trees[0].h, qd.data_ptr(), n, P, cap, cursor.data_ptr(),
+                                slots.data_ptr(), spos.data_ptr(), None)
+        assert rc == 0
+        res = torch.empty_like(slots)
+        for p in range(P):
+            fp = torch.empty(cap, dtype=torch.uint8, device=dev)
+            trees[p].search_batch(slots[p * cap:(p + 1) * cap], res[p * cap:(p + 1) * cap], fp)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        fnd = torch.empty(n, dtype=torch.uint8, device=dev)
+        assert L.shm__route_gather(res.data_ptr(), spos.data_ptr(), n, out.data_ptr(),
+                                   fnd.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        sl = slots.cpu().numpy().view(U64).reshape(P, cap)
+        sp = spos.cpu().numpy().view(np.uint32)
+        qo = owner_of(qd.cpu(), P).numpy()
+        o = out.cpu().numpy().view(U64)
+        f = fnd.cpu().numpy()
+        placed = sp != 0xFFFFFFFF
+        assert bool(placed.all()) != overflow
+        # every placed key sits in its owner's run at the recorded slot
+        assert np.array_equal(sl.reshape(-1)[sp[placed]], q[placed])
+        assert np.array_equal(sp[placed] // cap, qo[placed])
+        for p in range(P):
+            c = int((placed & (qo == p)).sum())
+            assert np.all(sl[p, c:] == U64((1 << 64) - 1))  # kKeyMax padding
+        assert np.array_equal(o[placed], exp[placed])
+        assert np.all(o[~placed] == 0) and np.array_equal(f, (o != 0).astype(np.uint8))
+        if overflow:
+            with pytest.raises(shm.ShermanError):
+                trees[0].synchronize()  # kErrOverflow reported by the next sync
+    for t in trees:
+        t.close()
