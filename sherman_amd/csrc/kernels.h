@@ -307,6 +307,9 @@ struct RangeArgs {
   // fill pass: values at output index >= vals_cap are dropped (the async
   // batch call writes before the host knows the total; it reports the total)
   uint64_t vals_cap;
+  // per-page occupancy bound (nullable, layout.h): a sibling leaf's bytes
+  // past its last possibly valid slot are not read
+  const uint8_t* leaf_hw;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // x[i] += c for i < n

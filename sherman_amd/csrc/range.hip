@@ -43,6 +43,20 @@ __device__ __forceinline__ void rload(const uint8_t* arena, uint64_t p, int li, 
 #pragma unroll
   for (int k = 0; k < kRChunks; ++k) w.c[k] = *reinterpret_cast<const u32x4*>(b + 16 * kRL * k);
 }
+// chunks 0..2 (bytes 0..767: the header and slots 0..39); chunk 3 (slots
+// 40..53 and the rear version) only when the leaf's occupancy bound says a
+// valid slot may lie there (layout.h leaf_hw: every slot >= hw is empty)
+constexpr uint32_t kChunk3Hw = 41;  // slot 40 ends past byte 767
+__device__ __forceinline__ void rload3(const uint8_t* arena, uint64_t p, int li, RPage& w) {
+  const uint8_t* b = arena + ga_offset(p) + 16 * li;
+#pragma unroll
+  for (int k = 0; k < kRChunks - 1; ++k)
+    w.c[k] = *reinterpret_cast<const u32x4*>(b + 16 * kRL * k);
+}
+__device__ __forceinline__ void rload_last(const uint8_t* arena, uint64_t p, int li, RPage& w) {
+  w.c[kRChunks - 1] =
+      *reinterpret_cast<const u32x4*>(arena + ga_offset(p) + 16 * li + 16 * kRL * (kRChunks - 1));
+}
 __device__ __forceinline__ void rstage(uint32_t* lp, int li, const RPage& w) {
 #pragma unroll
   for (int k = 0; k < kRChunks; ++k) *reinterpret_cast<u32x4*>(lp + 4 * (li + kRL * k)) = w.c[k];
@@ -168,12 +182,15 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
   }
 
   // ---- scan the leaf chain; w holds leaf p ------------------------------------
+  // (the start leaf whole; a sibling's bytes past slot hw - 1 are not read)
   const int ebase = chunk_base<kRE>(li);
+  uint32_t hw = kLeafCardinality;  // slots of the current leaf that may be valid
   while (ballot(act)) {
     if (act) rstage(lp, li, w);
     wave_lds_sync();
     bool more = false;
     uint64_t sibling = 0;
+    uint32_t hwn = kLeafHwFull;
     RPage wn = w;
     bool hit[kRE];
     uint64_t ev[kRE];
@@ -191,7 +208,10 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
           err |= kErrBadPtr;
           more = false;
         } else {
-          rload(a.arena, sibling, li, wn);  // in flight
+          // in flight: the sibling's bound (a 1.8 MB array, L2-resident) and
+          // its first 768 bytes
+          if (a.leaf_hw) hwn = a.leaf_hw[ga_offset(sibling) >> 10];
+          rload3(a.arena, sibling, li, wn);
         }
       }
       uint32_t D[kRCD];
@@ -203,8 +223,8 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
       chunk_entries<kRE>(D, ek, ev, ef, er);
 #pragma unroll
       for (int j = 0; j < kRE; ++j)
-        hit[j] = ebase + j >= li * kRE && ev[j] != kValueNull && ((ef[j] ^ er[j]) & 0xF) == 0 &&
-                 ek[j] >= lo && ek[j] <= hi;
+        hit[j] = ebase + j >= li * kRE && (uint32_t)(ebase + j) < hw && ev[j] != kValueNull &&
+                 ((ef[j] ^ er[j]) & 0xF) == 0 && ek[j] >= lo && ek[j] <= hi;
     }
     uint32_t c = 0;
 #pragma unroll
@@ -223,6 +243,8 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
     wave_lds_sync();  // LDS reads done before the next stage
     if (act) {
       if (more) {
+        if (hwn >= kChunk3Hw) rload_last(a.arena, sibling, li, wn);
+        hw = hwn < (uint32_t)kLeafCardinality ? hwn : (uint32_t)kLeafCardinality;
         p = sibling;
         w = wn;
       } else {

@@ -752,6 +752,7 @@ dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to,
   a.vals = vals;
   a.err = t->d_err;
   a.vals_cap = ~0ull;
+  a.leaf_hw = t->leaf_hw;
   set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
   return a;
 }
