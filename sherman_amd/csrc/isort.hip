@@ -3,7 +3,7 @@
 // leaves it (src/Tree.cpp:353-403, 878-889: a later insert of a key
 // overwrites the earlier one).
 //
-//   1. k_tile_dedup   every 4096-op tile: an LDS hash table keeps each key's
+//   1. k_tile_dedup   every 2048-op tile: an LDS hash table keeps each key's
 //                     last op (atomic max of the op index), and the tile's
 //                     survivors are compacted to its front (gcount).  Heavy
 //                     hitters (zipf) shrink to one op per tile here.
@@ -189,7 +189,7 @@ constexpr int kUniqPer = kUniqCap / kIT;
 // one block, ping-ponging between the bin's slots of keys1 / pay1 and the
 // same slots of the scratch arrays; digits on which every key agrees are
 // skipped (clustered keys need few passes).  Equal keys stay in op-index
-// order (the input holds at most one op per key per 4096-op tile, tiles in
+// order (the input holds at most one op per key per 2048-op tile, tiles in
 // order), so the last of each run is the batch's last writer.  Survivors
 // are then compacted to the bin's front with their ranks, as in the LDS path.
 // ldsw: >= 8 x 256 + 16 x 256 + 256 + 16 words of LDS.

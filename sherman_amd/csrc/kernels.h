@@ -197,10 +197,10 @@ void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s
 // partition_chunk_slots(n) words.
 constexpr int kCoarse = 256;
 constexpr int kFine = 256;
-constexpr int kMaxTiles = 256;
+constexpr int kMaxTiles = 512;
 constexpr int kFineCap = 8192;
 constexpr int kPartHistWords = kMaxTiles * kCoarse;
-constexpr int kPartGroupWords = 16 * kCoarse;
+constexpr int kPartGroupWords = kMaxTiles / 16 * kCoarse;
 uint32_t partition_chunk_slots(uint64_t n);
 // get ordering by the top 16 bits of the key's offset in the shard's range
 // [key_lo, key_lo + 2^key_bits) (keys outside clamp to the first/last bucket)
@@ -208,17 +208,17 @@ void launch_partition(const uint64_t* keys, uint64_t n, uint64_t key_lo, uint32_
                       uint32_t* M, uint32_t* S, uint32_t* chunks, uint64_t* keys1,
                       uint32_t* pos1, uint64_t* keys_out, uint32_t* src, hipStream_t s);
 // insert ordering, step 2: the coarse pass alone over per-group
-// de-duplicated runs (group gi = keys [gi * 4096, ...) holds gcount[gi]
+// de-duplicated runs (group gi = keys [gi * kIsortTile, ...) holds gcount[gi]
 // keys), carrying a u32 payload; bins = 2 x 256 words of (start, count)
 void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* gcount,
                              const uint32_t* pay_in, uint64_t key_lo, uint32_t key_bits,
                              uint32_t* M, uint32_t* S, uint64_t* keys1, uint32_t* pay1,
                              uint32_t* bins, hipStream_t s);
-// insert ordering (isort.hip).  Step 1: every 4096-op tile reduced to its
+// insert ordering (isort.hip).  Step 1: every 2048-op tile reduced to its
 // last writer per key (LDS hash table, atomic max of the op index); a kKeyMax
 // key rejects the chunk: gate = tag (k_bin_unique then emits nothing) and the
 // sticky error word gets kErrKeyMax.
-constexpr int kIsortTile = 4096;
+constexpr int kIsortTile = 2048;
 constexpr uint32_t kErrKeyMax = 1u << 31;
 // For batches of <= kMaxTiles tiles it also writes the coarse pass's tile
 // histograms M and group sums S (launch_partition_coarse then skips its own).

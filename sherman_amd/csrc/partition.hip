@@ -30,8 +30,8 @@ namespace dev {
 
 namespace {
 constexpr int kPT = 1024;                 // threads per block
-constexpr int kGrp = 4;                   // keys per thread per group
-constexpr int kGrpKeys = kPT * kGrp;      // 4096 keys per group
+constexpr int kGrp = 2;                   // keys per thread per group
+constexpr int kGrpKeys = kPT * kGrp;      // 2048 keys per group
 constexpr int kFinePer = kFineCap / kPT;  // keys per thread in the fine pass
 constexpr int kTileGroup = 16;            // tiles per S row
 constexpr int kGroups = kMaxTiles / kTileGroup;
@@ -120,20 +120,24 @@ __global__ __launch_bounds__(kPT) void k_part_coarse_scatter(
     k[r] = part_valid(i, n, gcount) ? keys[i] : 0;
   }
   {
-    // thread (bin b, quarter q): q 0/1 sum S rows [8q, 8q+8) -> both the bin
-    // total and (rows before this tile's group) the group prefix; q 2/3 sum
-    // this group's M rows before this tile.  All loads issue at once.
+    // thread (bin b, quarter q): q 0/1 sum S rows [SR q, SR q + SR) -> both
+    // the bin total and (rows before this tile's group) the group prefix;
+    // q 2/3 sum this group's M rows before this tile (8 each).  All loads
+    // issue at once.
+    constexpr int SR = kGroups / 2;
+    static_assert(SR >= 8 && kTileGroup == 16, "quarter layout");
     const int b = t & (kCoarse - 1), q = t >> 8;
     const uint32_t g = tile / kTileGroup;
-    const uint32_t u0 = q < 2 ? 8 * q : g * kTileGroup + 8 * (q - 2);
+    const uint32_t u0 = q < 2 ? SR * q : g * kTileGroup + 8 * (q - 2);
     const uint32_t* src = q < 2 ? S : M;
-    uint32_t v[8];
+    const int rows = q < 2 ? SR : 8;
+    uint32_t v[SR];
 #pragma unroll
-    for (int x = 0; x < 8; ++x)
-      v[x] = (q < 2 || u0 + x < tile) ? src[(uint64_t)(u0 + x) * kCoarse + b] : 0;
+    for (int x = 0; x < SR; ++x)
+      v[x] = (x < rows && (q < 2 || u0 + x < tile)) ? src[(uint64_t)(u0 + x) * kCoarse + b] : 0;
     uint32_t all = 0, pre = 0;
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
+    for (int x = 0; x < SR; ++x) {
       all += v[x];
       pre += (u0 + x) < g ? v[x] : 0;
     }
