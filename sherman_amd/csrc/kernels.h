@@ -243,14 +243,16 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
 // ---- segmentation (util.hip) --------------------------------------------------
 // Staged segments of a located op list (n_dev: device-side op count <= n):
 // the runs of ops on one page whose page k_locate marked (pnew[page] ==
-// tag: it gets a new key); runs of in-place overwrites are left out.  Two
-// launches: per 1024-op tile a staged-head count (bsum), then each tile sums
-// the counts before it and fills its segments.  bsum holds seg_tiles(n) words.
+// tag: it gets a new key); runs of in-place overwrites are left out.  One
+// launch: per 1024-op tile a staged-head count published in a tagged word
+// (lbw: seg_tiles(n) u64, zero at creation), the counts of the tiles before
+// it summed, its segments filled.
 constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
-void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
+void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, hipStream_t s);
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, uint32_t* err,
+                    hipStream_t s);
 // exclusive scan of u64 (bsum: seg_tiles(n) words); tot = {total, *err} for
 // the range scan's one read-back
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,

@@ -72,7 +72,7 @@ struct shm_tree {
   uint32_t *ia = nullptr, *ib = nullptr, *ic = nullptr;
   uint64_t *uk = nullptr, *uv = nullptr, *dk = nullptr;
   uint64_t* pages = nullptr;
-  uint32_t* bsum = nullptr;  // per-tile sums of the segmentation
+  uint64_t* seg_lb = nullptr;  // tagged per-tile staged-head counts (launch_segment)
   uint64_t* bsum64 = nullptr;
   uint32_t* seg_start = nullptr;
   uint32_t* seg_end = nullptr;
@@ -500,8 +500,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_segment(t->pages, n, t->d_counts + 0, t->bsum, t->seg_start, t->seg_end,
-                      t->seg_page, d_ns, t->pnew, tag, s);
+  dev::launch_segment(t->pages, n, t->d_counts + 0, t->seg_lb, t->seg_start, t->seg_end,
+                      t->seg_page, d_ns, t->pnew, tag, t->d_err, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -634,7 +634,7 @@ void free_all(shm_tree* t) {
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
   F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
-  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->bsum); F(t->bsum64);
+  F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->seg_lb); F(t->bsum64);
   F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
   F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
@@ -878,7 +878,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->uv, n);
   rc |= dalloc(&t->dk, n);
   rc |= dalloc(&t->pages, segcap);
-  rc |= dalloc(&t->bsum, dev::seg_tiles(segcap) + 1);
+  rc |= dalloc(&t->seg_lb, dev::seg_tiles(segcap) + 1);
   rc |= dalloc(&t->bsum64, dev::seg_tiles(n) + 1);
   rc |= dalloc(&t->seg_start, segcap + 1);
   rc |= dalloc(&t->seg_end, segcap);
@@ -934,6 +934,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   hipStream_t s = t->stream;
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
+      hipMemsetAsync(t->seg_lb, 0, sizeof(uint64_t) * (dev::seg_tiles(segcap) + 1), s) ||
       hipMemsetAsync(t->ctl, 0, sizeof(dev::UpperCtl), s) ||
       hipMemsetAsync(t->bins, 0, sizeof(uint32_t) * 4 * dev::kCoarse, s) ||
       hipMemsetAsync(t->leaf_rd, 0, sizeof(uint32_t) * segcap, s) ||

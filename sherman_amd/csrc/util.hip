@@ -74,32 +74,23 @@ __device__ __forceinline__ bool page_new(const uint32_t* pnew, uint64_t pg, uint
   return pnew[ga_offset(pg) >> 10] == tag;
 }
 
-__global__ __launch_bounds__(kT) void k_seg_count(const uint64_t* page, uint64_t n,
-                                                  const uint64_t* n_dev, uint32_t* bsum,
-                                                  const uint32_t* pnew, uint32_t tag) {
+// One launch: every 1024-op tile counts its staged heads, publishes the
+// count in its tagged word (chunk tag << 32 | count), sums the words of the
+// tiles before it (a tile waits only on tiles of smaller index, dispatched
+// before it, so nothing waits on a tile that is not running), and fills its
+// segments: seg_start / seg_page at each staged head, seg_end at its run's
+// last op (the count of staged heads up to and including that op is the
+// segment's position + 1).
+__global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t n,
+                                                 const uint64_t* n_dev, uint64_t* lbw,
+                                                 uint32_t* seg_start, uint32_t* seg_end,
+                                                 uint64_t* seg_page, uint32_t* num_seg,
+                                                 const uint32_t* pnew, uint32_t tag,
+                                                 uint32_t* err) {
+  __shared__ uint32_t s_pre[kT / kWave];
   const uint64_t nv = dev_n(n_dev, n);
-  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j)
-    if (seg_head(page, i0 + j, nv)) c += page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
-  uint32_t total;
-  (void)block_scan<uint32_t>(c, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-// seg_start / seg_end / seg_page of every staged segment: its head writes
-// the start and page, its last op the end (the count of staged heads up to
-// and including it is the segment's position + 1)
-__global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint64_t n,
-                                                      const uint64_t* n_dev,
-                                                      const uint32_t* bsum, uint32_t* seg_start,
-                                                      uint32_t* seg_end, uint64_t* seg_page,
-                                                      uint32_t* num_seg, const uint32_t* pnew,
-                                                      uint32_t tag) {
-  const uint64_t nv = dev_n(n_dev, n);
-  const uint32_t prefix = tiles_before<uint32_t>(bsum, blockIdx.x);
-  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  const uint32_t b = blockIdx.x;
+  const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint32_t h[kScanPer], c = 0;
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
@@ -108,7 +99,33 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
     c += h[j];
   }
   uint32_t total;
-  uint32_t pos = prefix + block_scan<uint32_t>(c, &total);
+  const uint32_t local = block_scan<uint32_t>(c, &total);
+  const uint64_t tg = (uint64_t)tag << 32;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the counts of the tiles before this one
+  uint32_t v = 0;
+  for (uint32_t x = threadIdx.x; x < b; x += kT) {
+    uint64_t w = 0;
+    for (uint32_t spin = 0;; ++spin) {
+      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & ~0xFFFFFFFFull) == tg) break;
+      if (spin > (1u << 24)) {
+        atomicOr(err, kErrRounds);
+        w = tg;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    v += (uint32_t)w;
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = v;
+  __syncthreads();
+  uint32_t pos = local;
+#pragma unroll
+  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = i0 + j;
@@ -123,17 +140,16 @@ __global__ __launch_bounds__(kT) void k_seg_fill_scan(const uint64_t* page, uint
     if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
     if (i + 1 == nv) *num_seg = pos;
   }
-  if (nv == 0 && blockIdx.x == 0 && threadIdx.x == 0) *num_seg = 0;
+  if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
 }
 
-void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint32_t* bsum,
+void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, hipStream_t s) {
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, uint32_t* err,
+                    hipStream_t s) {
   if (!n) return;
-  const dim3 g((unsigned)seg_tiles(n));
-  hipLaunchKernelGGL(k_seg_count, g, dim3(kT), 0, s, page, n, n_dev, bsum, pnew, tag);
-  hipLaunchKernelGGL(k_seg_fill_scan, g, dim3(kT), 0, s, page, n, n_dev, (const uint32_t*)bsum,
-                     seg_start, seg_end, seg_page, num_seg, pnew, tag);
+  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev, lbw,
+                     seg_start, seg_end, seg_page, num_seg, pnew, tag, err);
 }
 
 template <class T>
