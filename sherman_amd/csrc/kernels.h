@@ -253,10 +253,12 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, uint32_t* err,
                     hipStream_t s);
-// exclusive scan of u64 (bsum: seg_tiles(n) words); tot = {total, *err} for
-// the range scan's one read-back
-void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,
-                           const uint32_t* err, uint64_t* tot, hipStream_t s);
+// exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
+// at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
+// wraps); tot = {total, *err} for the range scan's one read-back
+void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* lbw,
+                           uint32_t tag, const uint32_t* err, uint64_t* tot, uint32_t* err_out,
+                           hipStream_t s);
 
 // ---- generators and multi-GPU routing (util.hip) -------------------------------
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,

@@ -73,7 +73,8 @@ struct shm_tree {
   uint64_t *uk = nullptr, *uv = nullptr, *dk = nullptr;
   uint64_t* pages = nullptr;
   uint64_t* seg_lb = nullptr;  // tagged per-tile staged-head counts (launch_segment)
-  uint64_t* bsum64 = nullptr;
+  uint64_t* bsum64 = nullptr;  // tagged tile words of launch_scan_u64_total
+  uint32_t scan_seq = 0;
   uint32_t* seg_start = nullptr;
   uint32_t* seg_end = nullptr;
   uint64_t* seg_page = nullptr;
@@ -757,6 +758,17 @@ dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to,
   return a;
 }
 
+// a fresh tag for launch_scan_u64_total's tile words (16 bits: the words
+// are zeroed again when the tag wraps, so no stale word can match)
+uint32_t scan_tag(shm_tree* t, hipStream_t s) {
+  uint32_t tag = ++t->scan_seq & 0xFFFFu;
+  if (tag == 0) {
+    (void)hipMemsetAsync(t->bsum64, 0, sizeof(uint64_t) * (dev::seg_tiles(t->nmax) + 1), s);
+    tag = ++t->scan_seq & 0xFFFFu;
+  }
+  return tag;
+}
+
 // one timed k_range launch
 int range_launch(shm_tree* t, hipStream_t s, const dev::RangeArgs& a) {
   shm_tree::ProfRec pr{};
@@ -935,6 +947,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (hipMemsetAsync(t->locks, 0, sizeof(uint64_t) * cfg->num_locks, s) ||
       hipMemsetAsync(t->d_err, 0, 16, s) ||
       hipMemsetAsync(t->seg_lb, 0, sizeof(uint64_t) * (dev::seg_tiles(segcap) + 1), s) ||
+      hipMemsetAsync(t->bsum64, 0, sizeof(uint64_t) * (dev::seg_tiles(n) + 1), s) ||
       hipMemsetAsync(t->ctl, 0, sizeof(dev::UpperCtl), s) ||
       hipMemsetAsync(t->bins, 0, sizeof(uint32_t) * 4 * dev::kCoarse, s) ||
       hipMemsetAsync(t->leaf_rd, 0, sizeof(uint32_t) * segcap, s) ||
@@ -1158,8 +1171,8 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
     const uint64_t m = std::min(t->nmax, n - off);
     int rc = range_launch(t, s, rargs(off, m, nullptr, nullptr));
     if (rc) return rc;
-    dev::launch_scan_u64_total(counts_out + off, offsets_out + off, m, t->bsum64, t->d_err,
-                               t->d_counts + 12, s);
+    dev::launch_scan_u64_total(counts_out + off, offsets_out + off, m, t->bsum64,
+                               scan_tag(t, s), t->d_err, t->d_counts + 12, t->d_err, s);
     rc = readback(t, s, t->d_counts + 12, 2 * sizeof(uint64_t));
     if (rc) return rc;
     if (t->h_pin[1]) return check_err(t, s);
@@ -1212,7 +1225,8 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   if (rc) return rc;
   // count pass -> offsets and (total, error word) into total_dev, then the
   // fill pass bounded by vals_cap; no host synchronisation
-  dev::launch_scan_u64_total(counts_out, offsets_out, n, t->bsum64, t->d_err, total_dev, s);
+  dev::launch_scan_u64_total(counts_out, offsets_out, n, t->bsum64, scan_tag(t, s), t->d_err,
+                             total_dev, t->d_err, s);
   if (!vals_cap) return SHM_OK;
   a.offsets = offsets_out;
   a.vals = vals_out;

@@ -51,16 +51,6 @@ __device__ __forceinline__ T block_scan(T v, T* total) {
   return base + incl - v;
 }
 
-// sum of bsum[0, b) by the whole block
-template <class T>
-__device__ __forceinline__ T tiles_before(const T* bsum, uint32_t b) {
-  T v = 0;
-  for (uint32_t j = threadIdx.x; j < b; j += kT) v += bsum[j];
-  T total;
-  (void)block_scan(v, &total);
-  return total;
-}
-
 __device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, uint64_t nv) {
   return i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
 }
@@ -152,50 +142,69 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                      seg_start, seg_end, seg_page, num_seg, pnew, tag, err);
 }
 
-template <class T>
-__global__ __launch_bounds__(kT) void k_tile_sum(const T* in, uint64_t n, T* bsum) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  T c = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) c += i0 + j < n ? in[i0 + j] : T(0);
-  T total;
-  (void)block_scan(c, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-// tot (nullable): {out[n-1] + in[n-1], *err} from the thread holding n - 1
-template <class T>
-__global__ __launch_bounds__(kT) void k_tile_scan(const T* in, uint64_t n, const T* bsum, T* out,
-                                                  const uint32_t* err, uint64_t* tot) {
-  const T prefix = tiles_before(bsum, blockIdx.x);
-  const uint64_t i0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  T v[kScanPer], c = 0;
+// Exclusive scan of u64 counts in one launch: every 1024-element tile
+// publishes its sum in a tagged word (tag << 48 | sum: a range scan's
+// counts total < 2^48), sums the words of the tiles before it (as
+// k_seg_fill) and writes its offsets; the thread holding n - 1 writes
+// tot = {total, *err} (nullable).
+__global__ __launch_bounds__(kT) void k_scan_u64(const uint64_t* in, uint64_t n, uint64_t* lbw,
+                                                 uint32_t tag, uint64_t* out,
+                                                 const uint32_t* err, uint64_t* tot,
+                                                 uint32_t* err_out) {
+  __shared__ uint64_t s_pre[kT / kWave];
+  const uint32_t b = blockIdx.x;
+  const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
+  uint64_t v[kScanPer], c = 0;
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
-    v[j] = i0 + j < n ? in[i0 + j] : T(0);
+    v[j] = i0 + j < n ? in[i0 + j] : 0;
     c += v[j];
   }
-  T total;
-  T pos = prefix + block_scan(c, &total);
+  uint64_t total;
+  const uint64_t local = block_scan<uint64_t>(c, &total);
+  constexpr uint64_t kMask = (1ull << 48) - 1;
+  const uint64_t tg = (uint64_t)(tag & 0xFFFFu) << 48;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lbw + b, tg | (total & kMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t pre = 0;
+  for (uint32_t x = threadIdx.x; x < b; x += kT) {
+    uint64_t w = 0;
+    for (uint32_t spin = 0;; ++spin) {
+      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & ~kMask) == tg) break;
+      if (spin > (1u << 24)) {
+        atomicOr(err_out, kErrRounds);
+        w = tg;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    pre += w & kMask;
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = pre;
+  __syncthreads();
+  uint64_t pos = local;
+#pragma unroll
+  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     if (i0 + j < n) out[i0 + j] = pos;
     pos += v[j];
     if (tot && i0 + j + 1 == n) {
-      tot[0] = (uint64_t)pos;
+      tot[0] = pos;
       tot[1] = *err;
     }
   }
 }
 
-void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bsum,
-                           const uint32_t* err, uint64_t* tot, hipStream_t s) {
+void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* lbw,
+                           uint32_t tag, const uint32_t* err, uint64_t* tot, uint32_t* err_out,
+                           hipStream_t s) {
   if (!n) return;
-  const dim3 g((unsigned)seg_tiles(n));
-  using U = unsigned long long;
-  hipLaunchKernelGGL(k_tile_sum<U>, g, dim3(kT), 0, s, (const U*)in, n, (U*)bsum);
-  hipLaunchKernelGGL(k_tile_scan<U>, g, dim3(kT), 0, s, (const U*)in, n, (const U*)bsum,
-                     (U*)out, err, tot);
+  hipLaunchKernelGGL(k_scan_u64, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, in, n, lbw, tag, out,
+                     err, tot, err_out);
 }
 
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
