@@ -583,7 +583,6 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   const uint32_t nsplit = block_sum(v_ns, s_red);
   const uint32_t pre_np = block_sum((uint32_t)t < b ? v_np : 0u, s_red);
   const uint32_t pre_ns = block_sum((uint32_t)t < b ? v_ns : 0u, s_red);
-  (void)nsplit;
   bool ok = true;
   uint32_t nsep = 0;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
@@ -612,12 +611,17 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     }
     __syncthreads();  // the block's split list is complete (workgroup scope)
     stamp();
-    // ---- P3: this block's new right siblings, then page 0 of its splits ----
+    // ---- P3: every wave of the grid takes new right siblings, then pages 0,
+    // from the whole split list: the splits of a block range vary (a few
+    // per block on average, several times that on some), and the slowest
+    // block held every other at the next barrier (block-local P3: 13 us of
+    // work, 19 us of barrier wait per C5 chunk, phase clock)
+    ok = grid_sync(ctl, nb, &s_flag);
+    stamp();
     const uint64_t first = cursor;  // arena page of global new page 0
     const uint64_t xroot = cursor + total;  // the root's left half (grow0)
-    const uint32_t my_ns = run_ns - pre_ns;
-    for (uint32_t gp = pre_np + (uint32_t)wv; gp < run_np; gp += kUpWaves) {
-      const uint32_t k = pre_ns + last_le(a.spl_base + pre_ns, my_ns, gp);
+    for (uint32_t gp = (uint32_t)wid; ok && gp < total; gp += (uint32_t)W) {
+      const uint32_t k = last_le(a.spl_base, nsplit, gp);
       const uint32_t g = a.spl_seg[k];
       const uint32_t pb = a.spl_base[k];
       const int p = (int)(gp - pb) + 1;
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         a.ipage[0][gp] = par_pg;
       }
     }
-    for (uint32_t k = pre_ns + (uint32_t)wv; k < run_ns; k += kUpWaves) {
+    for (uint32_t k = (uint32_t)wid; ok && k < nsplit; k += (uint32_t)W) {
       const uint32_t g = a.spl_seg[k];
       const uint32_t pb = a.spl_base[k];
       const int P = (int)a.seg_P[g];
@@ -665,7 +669,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     nsep = total;
     stamp();
     // the next level reads every block's separators
-    ok = grid_sync(ctl, nb, &s_flag);
+    ok = ok && grid_sync(ctl, nb, &s_flag);
     stamp();
   }
 

@@ -796,7 +796,9 @@ int range_stage(shm_tree* t, hipStream_t s, uint64_t n, bool* staged) {
       t->rstage = nullptr;
       t->rstage_words = 0;
     }
-    const uint64_t words = std::max<uint64_t>(n, 1u << 14) * kRangeStage;
+    // headroom: batches of similar size must not each reallocate (a
+    // reallocation waits for the stream)
+    const uint64_t words = std::max<uint64_t>(n + n / 4, 1u << 14) * kRangeStage;
     if (dalloc(&t->rstage, words)) return SHM_ENOMEM;
     t->rstage_words = words;
   }
