@@ -279,14 +279,20 @@ def main():
         n_glob = n_keys * world
         span = (1 << 64) // n_glob * args.scan_keys
         zipf = Zipf(2 * n_glob, args.theta, dev)  # ids > n_glob: new keys
+        # a fresh batch for every step the run applies (CPU-baseline parity
+        # pair, warmup, timed, latency and profile steps): a batch applied a
+        # second time would find its new keys already stored and turn their
+        # inserts into updates, leaving the timed steps with few splits
+        n_c5 = 2 + args.warmup + args.steps + args.profile_steps + (
+            args.latency_steps if args.latency_steps is not None else args.steps)
         mixed = []
-        for b in range(N_BATCHES):
+        for b in range(n_c5):
             ids = zipf.sample(batch, g) + 1
             k = torch.empty_like(ids)
             tree.hash_keys(ids, k)
             is_scan = op_is_get(batch, args.scan_ratio, dev, g)
             op_idx = torch.arange(b * batch, (b + 1) * batch, dtype=torch.int64, device=dev)
-            op_idx += (rank * N_BATCHES) * batch
+            op_idx += (rank * n_c5) * batch
             lo = k[is_scan].contiguous()
             hi = lo + span  # wraps past 2^64 - 1 ...
             hi = torch.where((hi ^ (-(1 << 63))) < (lo ^ (-(1 << 63))),
@@ -296,9 +302,11 @@ def main():
         del keys_local
         route = ShardRouter(tree, world, dist, cshard=cshard) if world > 1 else None
         scan_out = {}
+        applied = [0]  # batches applied so far (all step loops)
 
         def step(i):
-            lo, hi, pk, pv = mixed[i % N_BATCHES]
+            lo, hi, pk, pv = mixed[applied[0] % n_c5]
+            applied[0] += 1
             if route is None and args.async_scans:
                 # scans queued without a host wait; the batch's inserts queue
                 # behind them; every step's total is checked after the run
@@ -750,9 +758,9 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     parity = True
     done, secs, b = 0, 0.0, 0
     while secs < args.cpu_seconds or b < 2:
-        lo, hi, pk, pv = mixed[b % N_BATCHES]
+        lo, hi, pk, pv = mixed[b % len(mixed)]
         if b < 2:
-            step(b)
+            step(b)  # applies mixed[b]: the first two batches of the run
             torch.cuda.synchronize()
             gc, gv = scan_out["r"].result()
             gc = gc.cpu().numpy()
