@@ -210,6 +210,11 @@ __device__ __forceinline__ void store_page(uint8_t* arena, uint64_t off,
 // keys); count 0: pg0 is the deepest internal page covering the prefix.
 // Leaf i is taken only when t_i < t(k), which proves k > sep_i; on a tie the
 // walk starts one leaf to the left and moves right (B-link, Tree.cpp:626-629).
+// k lies inside the directory's key range (and is not kKeyMax)
+__device__ __forceinline__ bool dir_covers(uint64_t dir_lo, uint32_t dir_shift, uint64_t dir_n,
+                                           uint64_t k) {
+  return k >= dir_lo && ((k - dir_lo) >> dir_shift) < dir_n && k != kKeyMax;
+}
 __device__ __forceinline__ uint64_t dir_start(const uint64_t* dir, uint64_t dir_lo,
                                               uint32_t dir_shift, uint64_t dir_n,
                                               uint16_t node, uint64_t k, uint64_t fallback) {

@@ -268,6 +268,18 @@ __device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint3
 // (665-685), one wave.  0 on an inconsistency (error bits in *err).
 __device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err) {
   uint64_t ptr = a.root;
+  // start at the level's page on the path of k's directory prefix (a page
+  // keeps its lowest fence when it splits, so a stale hint is still a valid
+  // B-link start); a hint whose page is no longer at `level` (the root page
+  // grew a level) restarts from the root
+  bool hinted = false;
+  if (a.dir_hint && level >= 1 && level <= 2 && dir_covers(a.dir_lo, a.dir_shift, a.dir_n, k)) {
+    const uint32_t pg = a.dir_hint[(uint64_t)(level - 1) * a.dir_n + ((k - a.dir_lo) >> a.dir_shift)];
+    if (pg) {
+      ptr = dir_page_ga(pg, a.node);
+      hinted = true;
+    }
+  }
   int retries = 0;
   for (int hop = 0; hop < kMaxRounds; ++hop) {
     if (!ptr_ok(ptr, a.node, a.arena_bytes)) {
@@ -282,6 +294,11 @@ __device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, ui
         *err |= kErrInconsistent;
         return 0;
       }
+      continue;
+    }
+    if (hinted && (h.level != level || k < h.lowest)) {  // not this level's page any more
+      hinted = false;
+      ptr = a.root;
       continue;
     }
     if (k >= h.highest && h.sibling != 0) {  // turn right (Tree.cpp:626-629)

@@ -67,9 +67,11 @@ void launch_sum_rebuild(const uint8_t* arena, uint64_t pages, uint8_t* sum, hipS
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
 // leaf directory (leafdir.hip): n_ent entries of 8 u32 from dir_lo, 2^shift
 // keys each
+// hint (nullable): 2 x n_ent u32, the level-1 and level-2 pages (page
+// indices, 0 = none) on the root-to-leaf path of each prefix's first key
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* err, hipStream_t s);
+                     uint32_t* hint, uint32_t* err, hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.
@@ -178,6 +180,9 @@ struct UpperArgs {
   uint64_t dir_lo;
   uint64_t dir_n;
   uint32_t dir_shift;
+  // nullable: the directory's level-1 / level-2 path pages (launch_leaf_dir),
+  // start pages of parent_of walks
+  const uint32_t* dir_hint;
   // nullable: block 0 records the wall clock (100 MHz) at each phase end,
   // stamps[0] = count (tools/upper_stamps.py)
   uint64_t* stamps;

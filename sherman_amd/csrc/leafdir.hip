@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
                                                   uint64_t arena_bytes, uint16_t node,
                                                   uint64_t root, uint64_t dir_lo,
                                                   uint32_t shift, uint64_t n_ent,
-                                                  uint64_t* __restrict__ dir, uint32_t* err) {
+                                                  uint64_t* __restrict__ dir,
+                                                  uint32_t* __restrict__ hint, uint32_t* err) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_ent) return;
   const uint64_t lo = dir_lo + (p << shift);
@@ -61,6 +62,7 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
   const uint64_t hi = lo > ~0ull - span ? ~0ull : lo + span;
   uint64_t ptr = root, cover = root;
   uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t h1 = 0, h2 = 0;  // level-1 / level-2 pages on lo's path
   bool ok = false;
   for (int it = 0; it < 4096; ++it) {
     if (!ptr_ok(ptr, node, arena_bytes)) break;
@@ -74,6 +76,9 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
       continue;
     }
     if (leftmost != 0) {  // internal: descend towards lo
+      const uint32_t lv = pg[kOffLevel];
+      if (lv == 1) h1 = dir_page_index(ptr);
+      if (lv == 2) h2 = dir_page_index(ptr);
       const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
       const int c = keys_le(pg, cnt, lo);
       if (hi < highest && keys_le(pg, cnt, hi) == c) cover = ptr;  // whole prefix below
@@ -115,6 +120,10 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
   uint32_t t[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) t[i] = (uint32_t)((out[4 + i] - lo) >> sh);
+  if (hint) {
+    hint[p] = ok ? h1 : 0u;
+    hint[n_ent + p] = ok ? h2 : 0u;
+  }
   u32x4* e = reinterpret_cast<u32x4*>(dir + 4 * p);
   e[0] = u32x4{dir_page_index(out[0]), dir_page_index(out[1]), dir_page_index(out[2]),
                dir_page_index(out[3])};
@@ -123,10 +132,10 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
 
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* err, hipStream_t s) {
+                     uint32_t* hint, uint32_t* err, hipStream_t s) {
   if (!n_ent) return;
   hipLaunchKernelGGL(k_leaf_dir, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s, arena,
-                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, err);
+                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, err);
 }
 
 }  // namespace dev

@@ -103,6 +103,7 @@ struct shm_tree {
   bool err_pending = false;  // kernels ran since d_err was last read back
   uint64_t* dir = nullptr;
   uint32_t dir_bits = 0;
+  uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
   uint64_t dir_np = 0;
   bool dir_valid = false;
   std::mutex mu;
@@ -294,13 +295,17 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
     if (t->dir) {
       HIP_OK(hipStreamSynchronize(s));
       HIP_OK(hipFree(t->dir));
+      HIP_OK(hipFree(t->dir_hint));
       t->dir = nullptr;
+      t->dir_hint = nullptr;
     }
     if (dalloc(&t->dir, 4ull << bits)) return SHM_ENOMEM;  // 32 B per entry
+    if (dalloc(&t->dir_hint, 2ull << bits)) return SHM_ENOMEM;  // levels 1, 2
     t->dir_bits = bits;
   }
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
-                       t->cfg.key_bits - bits, 1ull << bits, t->dir, t->d_err, s);
+                       t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint, t->d_err,
+                       s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
   return SHM_OK;
@@ -577,6 +582,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.dk = t->dk;
   u.n_del = t->d_counts + 1;
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
+  if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
   dev::launch_upper(u, s);
   DBG(s, "upper");
@@ -642,7 +648,7 @@ void free_all(shm_tree* t) {
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
-  F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->dir); F(t->gcount); F(t->bins);
+  F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->dir); F(t->dir_hint); F(t->gcount); F(t->bins);
   for (auto& r : t->prof_pending)
     for (hipEvent_t e : r.e)
       if (e) t->event_pool.push_back(e);
