@@ -48,6 +48,9 @@ struct WalkArgs {
   uint32_t* out_slot;
   uint32_t* out_new;
   uint32_t out_new_tag;
+  // nullable: set to out_new_tag when any op marked a page (a wave stores
+  // it once): the segmentation skips a chunk of updates only
+  uint32_t* any_new;
   const uint64_t* vals;
   uint64_t* locks;
   uint32_t num_locks;
@@ -254,10 +257,12 @@ void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
 // it summed, its segments filled.
 constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
+// any_new (nullable): the locate's any-page-marked word (== tag: some page
+// gets a new key; otherwise there are no staged segments)
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, uint32_t* err,
-                    hipStream_t s);
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag,
+                    const uint32_t* any_new, uint32_t* err, hipStream_t s);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
 // wraps); tot = {total, *err} for the range scan's one read-back

@@ -162,6 +162,10 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
     // (out = 0 after an error marks page 0: staged, rejected as a bad pointer)
     if (!slot) a.out_new[ga_offset(out) >> 10] = a.out_new_tag;
   }
+  if (match && a.any_new) {
+    const uint64_t m = ballot(!slot);
+    if (m && lane_id() == ctz64(m)) *a.any_new = a.out_new_tag;  // one store per wave
+  }
 }
 
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {

@@ -498,6 +498,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.out_slot = t->oslot;
   w.out_new = t->pnew;
   w.out_new_tag = tag;
+  w.any_new = reinterpret_cast<uint32_t*>(t->d_counts + 10);
   w.vals = t->uv;
   w.locks = t->locks;
   w.num_locks = t->cfg.num_locks;
@@ -507,7 +508,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
   dev::launch_segment(t->pages, n, t->d_counts + 0, t->seg_lb, t->seg_start, t->seg_end,
-                      t->seg_page, d_ns, t->pnew, tag, t->d_err, s);
+                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};

@@ -76,10 +76,14 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  uint32_t* seg_start, uint32_t* seg_end,
                                                  uint64_t* seg_page, uint32_t* num_seg,
                                                  const uint32_t* pnew, uint32_t tag,
-                                                 uint32_t* err) {
+                                                 const uint32_t* any_new, uint32_t* err) {
   __shared__ uint32_t s_pre[kT / kWave];
-  const uint64_t nv = dev_n(n_dev, n);
   const uint32_t b = blockIdx.x;
+  if (any_new && *any_new != tag) {  // no op of this chunk marked a page
+    if (b == 0 && threadIdx.x == 0) *num_seg = 0;
+    return;
+  }
+  const uint64_t nv = dev_n(n_dev, n);
   const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint32_t h[kScanPer], c = 0;
 #pragma unroll
@@ -135,11 +139,11 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag, uint32_t* err,
-                    hipStream_t s) {
+                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag,
+                    const uint32_t* any_new, uint32_t* err, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev, lbw,
-                     seg_start, seg_end, seg_page, num_seg, pnew, tag, err);
+                     seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err);
 }
 
 // Exclusive scan of u64 counts in one launch: every 1024-element tile
