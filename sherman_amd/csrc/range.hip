@@ -86,48 +86,17 @@ __device__ __forceinline__ uint32_t group_scan(uint32_t v, int li, uint32_t* tot
 }
 }  // namespace
 
-__global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_page[kRangeWaves][kRG * kPageDwords];
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const int q = lane / kRL, li = lane % kRL;
-  const uint64_t Q = ((uint64_t)blockIdx.x * kRangeWaves + (uint64_t)wv) * kRG + (uint64_t)q;
-  const bool has = Q < a.n;
-  if (!ballot(has)) return;  // wave-uniform
-  uint32_t* lp = s_page[wv] + q * kPageDwords;
-  uint64_t lo = 0, hi = 0, out = 0;
-  if (has) {
-    lo = a.from[Q];
-    hi = a.to[Q];
-    if (a.offsets) out = a.offsets[Q];
-  }
-  uint32_t err = 0;
+// Walks one scan per group of the wave (act: the group has one) from the
+// leaf directory / root down to lo's leaf and along the sibling chain to hi;
+// its hit values in key order go to dst0[slot] for slot < cap0, then to
+// dst1[slot - cap0] for the next cap1 slots (either nullable with cap 0).
+// Returns the scan's value count.  Wave-uniform call (ballot loops); lp =
+// the group's 1 KB LDS page slot.
+__device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uint64_t lo,
+                                               uint64_t hi, uint32_t* lp, int li, uint64_t* dst0,
+                                               uint64_t cap0, uint64_t* dst1, uint64_t cap1,
+                                               uint32_t& err) {
   uint64_t cnt = 0;
-  uint64_t* stq = (a.stage && has) ? a.stage + Q * (uint64_t)a.stage_cap : nullptr;
-  bool act = has && lo <= hi;
-  bool copied = false;
-  if (a.offsets && stq) {
-    // fill pass, staged scan: copy its values out, no second walk
-    const uint64_t c = a.counts[Q];
-    copied = c <= a.stage_cap;
-    if (copied) {
-      for (uint64_t b = 0; b < c; b += kRL * 4) {
-        uint64_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint64_t i = b + (uint64_t)(li + kRL * u);
-          v[u] = i < c ? stq[i] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint64_t i = b + (uint64_t)(li + kRL * u);
-          if (i < c && out + i < a.vals_cap) a.vals[out + i] = v[u];
-        }
-      }
-      act = false;
-    }
-  }
-
   // ---- descend to the leaf whose fences hold lo ------------------------------
   RPage w;
   uint64_t p = 0;
@@ -234,8 +203,10 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
 #pragma unroll
     for (int j = 0; j < kRE; ++j) {
       if (hit[j]) {
-        if (a.offsets && out + slot < a.vals_cap) a.vals[out + slot] = ev[j];
-        if (!a.offsets && stq && slot < a.stage_cap) stq[slot] = ev[j];
+        if (slot < cap0)
+          dst0[slot] = ev[j];
+        else if (slot - cap0 < cap1)
+          dst1[slot - cap0] = ev[j];
         ++slot;
       }
     }
@@ -252,6 +223,57 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
       }
     }
   }
+  return cnt;
+}
+
+__global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_page[kRangeWaves][kRG * kPageDwords];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const int q = lane / kRL, li = lane % kRL;
+  const uint64_t Q = ((uint64_t)blockIdx.x * kRangeWaves + (uint64_t)wv) * kRG + (uint64_t)q;
+  const bool has = Q < a.n;
+  if (!ballot(has)) return;  // wave-uniform
+  uint32_t* lp = s_page[wv] + q * kPageDwords;
+  uint64_t lo = 0, hi = 0, out = 0;
+  if (has) {
+    lo = a.from[Q];
+    hi = a.to[Q];
+    if (a.offsets) out = a.offsets[Q];
+  }
+  uint32_t err = 0;
+  uint64_t* stq = (a.stage && has) ? a.stage + Q * (uint64_t)a.stage_cap : nullptr;
+  bool act = has && lo <= hi;
+  bool copied = false;
+  if (a.offsets && stq) {
+    // fill pass, staged scan: copy its values out, no second walk
+    const uint64_t c = a.counts[Q];
+    copied = c <= a.stage_cap;
+    if (copied) {
+      for (uint64_t b = 0; b < c; b += kRL * 4) {
+        uint64_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t i = b + (uint64_t)(li + kRL * u);
+          v[u] = i < c ? stq[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t i = b + (uint64_t)(li + kRL * u);
+          if (i < c && out + i < a.vals_cap) a.vals[out + i] = v[u];
+        }
+      }
+      act = false;
+    }
+  }
+
+  uint64_t* dst = stq;
+  uint64_t cap = stq ? a.stage_cap : 0;
+  if (a.offsets) {
+    dst = a.vals + out;
+    cap = out < a.vals_cap ? a.vals_cap - out : 0;
+  }
+  const uint64_t cnt = range_walk(a, act, lo, hi, lp, li, dst, cap, nullptr, 0, err);
   if (has && !copied && li == 0) a.counts[Q] = cnt;
   if (err) atomicOr(a.err, err);
 }
