@@ -50,8 +50,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 ALG_BYTES_PER_GET = 1040     # 1024 B leaf + 8 B key + 8 B value: the page walk
-# the summary walk (default): three random 128 B HBM lines (directory entry,
-# leaf summary, the matching entry) + 8 B key + 8 B value
+# the summary walk (default): three random reads, each served as a 128 B
+# L2 line (directory entry, the 64 B leaf summary, the matching entry) + 8 B
+# key + 8 B value
 ALG_BYTES_PER_GET_SUM = 3 * 128 + 16
 ALG_BYTES_PER_INSERT = 1074  # 1024 B leaf + 18 B entry + 16 B k/v + 16 B lock
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)

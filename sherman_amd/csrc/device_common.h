@@ -296,29 +296,29 @@ __device__ __forceinline__ uint64_t lower_bound64(const uint64_t* a,
 }
 
 // A leaf's summary line (layout.h) from one wave: lane s < 54 gives slot
-// s's fingerprint (0 = empty), lane 0 the fences; the tag byte last.
+// s's fingerprint (0 = empty), lane 0 the highest fence; the tag byte last.
 __device__ __forceinline__ void put_leaf_sum(uint8_t* sum, uint64_t page_off, uint64_t highest,
-                                             uint64_t sibling, uint32_t fp) {
+                                             uint32_t fp) {
   if (!sum) return;
   uint8_t* line = sum + (page_off >> 10) * kSumBytes;
   const int lane = lane_id();
-  if (lane < kLeafCardinality)
-    reinterpret_cast<uint16_t*>(line + kSumOffFp)[lane] = (uint16_t)fp;
+  if (lane < kLeafCardinality) line[kSumOffFp + lane] = (uint8_t)fp;
   if (lane == 0) {
     *reinterpret_cast<uint64_t*>(line + kSumOffHighest) = highest;
-    *reinterpret_cast<uint32_t*>(line + kSumOffSibling) = sibling ? dir_page_index(sibling) : 0u;
-    line[0] = kSumLeaf;
+    line[kSumOffTag] = kSumLeaf;
   }
+}
+// mark a page's line as not describing a leaf
+__device__ __forceinline__ void clear_leaf_sum(uint8_t* sum, uint64_t page_off) {
+  if (sum) sum[(page_off >> 10) * kSumBytes + kSumOffTag] = 0;
 }
 // clear slot s's fingerprint (the slot became empty)
 __device__ __forceinline__ void clear_leaf_fp(uint8_t* sum, uint64_t page_off, int s) {
-  if (sum) reinterpret_cast<uint16_t*>(sum + (page_off >> 10) * kSumBytes + kSumOffFp)[s] = 0;
+  if (sum) sum[(page_off >> 10) * kSumBytes + kSumOffFp + s] = 0;
 }
 // set slot s's fingerprint (a new key took the slot)
 __device__ __forceinline__ void set_leaf_fp(uint8_t* sum, uint64_t page_off, int s, uint64_t k) {
-  if (sum)
-    reinterpret_cast<uint16_t*>(sum + (page_off >> 10) * kSumBytes + kSumOffFp)[s] =
-        (uint16_t)key_fp(k);
+  if (sum) sum[(page_off >> 10) * kSumBytes + kSumOffFp + s] = (uint8_t)key_fp(k);
 }
 
 // ---- per-lane leaf access (the summary walk, the update matcher) --------------
@@ -350,28 +350,34 @@ __device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f
 // describe a current leaf; else its highest fence, sibling and the slots
 // whose 16-bit fingerprint equals k's (bit s for slot s)
 struct SumLine {
-  uint64_t highest, sibling, cand;
+  uint64_t highest, cand;
 };
-__device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, uint16_t node,
-                                         uint64_t k, SumLine& o) {
+__device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, uint64_t k,
+                                         SumLine& o) {
   const u32x4* line = reinterpret_cast<const u32x4*>(sum + (page_off >> 10) * kSumBytes);
-  u32x4 l[8];
+  u32x4 l[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) l[j] = line[j];
-  if ((l[0].x & 0xFF) != kSumLeaf) return false;
-  o.sibling = l[0].y ? dir_page_ga(l[0].y, node) : 0;
-  o.highest = (uint64_t)l[0].z | ((uint64_t)l[0].w << 32);
+  for (int j = 0; j < 4; ++j) l[j] = line[j];
+  if ((l[0].z & 0xFF) != kSumLeaf) return false;
+  o.highest = (uint64_t)l[0].x | ((uint64_t)l[0].y << 32);
   const uint32_t fq = key_fp(k);
   uint64_t cand = 0;
 #pragma unroll
-  for (int d = 0; d < kLeafCardinality / 2; ++d) {  // dwords 4..30: two slots each
-    const u32x4 v = l[1 + d / 4];
-    const uint32_t x = (d & 3) == 0 ? v.x : (d & 3) == 1 ? v.y : (d & 3) == 2 ? v.z : v.w;
-    cand |= (uint64_t)((x & 0xFFFFu) == fq) << (2 * d);
-    cand |= (uint64_t)((x >> 16) == fq) << (2 * d + 1);
+  for (int s = 0; s < kLeafCardinality; ++s) {  // byte 9 + s of the line
+    const int b = (int)kSumOffFp + s;
+    const u32x4 v = l[b >> 4];
+    const int d = (b >> 2) & 3;
+    const uint32_t x = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+    cand |= (uint64_t)(((x >> (8 * (b & 3))) & 0xFFu) == fq) << s;
   }
   o.cand = cand;
   return true;
+}
+// a page's sibling pointer from its header (bytes 17..24, Tree.h:130-160):
+// the right turn of a summary walk
+__device__ __forceinline__ uint64_t page_sibling(const uint8_t* page) {
+  const u32x4 B = *reinterpret_cast<const u32x4*>(page + 16);
+  return (uint64_t)((B.x >> 8) | (B.y << 24)) | ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
 }
 
 }  // namespace dev

@@ -334,13 +334,14 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
       const uint64_t off = ga_offset(ptr);
       const uint8_t* page = a.arena + off;
       SumLine sl;
-      if (sum_read(a.sum, off, a.node, k, sl)) {
+      if (sum_read(a.sum, off, k, sl)) {
         if (k >= sl.highest) {  // turn right (Tree.cpp:626-629)
-          if (!sl.sibling) {
+          const uint64_t sib = page_sibling(a.arena + off);
+          if (!sib) {
             err |= kErrFence;
             break;
           }
-          ptr = sl.sibling;
+          ptr = sib;
           continue;
         }
         uint64_t cand = sl.cand;
@@ -432,11 +433,9 @@ __global__ __launch_bounds__(256) void k_sum_rebuild(const uint8_t* arena, uint6
   const u32x4 A = pw[0], B = pw[1], C = pw[2];
   const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
                             ((uint64_t)((A.w >> 8) | (B.x << 24)) << 32);
-  const uint64_t sibling = (uint64_t)((B.x >> 8) | (B.y << 24)) |
-                           ((uint64_t)((B.y >> 8) | (B.z << 24)) << 32);
   const uint64_t highest = (uint64_t)C.y | ((uint64_t)C.z << 32);
   if (leftmost != 0) {  // internal page: no summary
-    if (lane == 0) sum[pg * kSumBytes] = 0;
+    if (lane == 0) clear_leaf_sum(sum, pg * kPageSize);
     return;
   }
   uint32_t fp = 0;
@@ -446,7 +445,7 @@ __global__ __launch_bounds__(256) void k_sum_rebuild(const uint8_t* arena, uint6
     lane_entry(page, lane, ek, ev, ef, er);
     fp = ev != kValueNull ? key_fp(ek) : 0u;
   }
-  put_leaf_sum(sum, pg * kPageSize, highest, sibling, fp);
+  put_leaf_sum(sum, pg * kPageSize, highest, fp);
 }
 
 void launch_sum_rebuild(const uint8_t* arena, uint64_t pages, uint8_t* sum, hipStream_t s) {

@@ -195,8 +195,7 @@ __device__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h
   store_page(a.arena, ga_offset(s.dest), L.page);
   if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = (uint8_t)c;  // slots [0, c)
   // every slot < c is valid (value != 0: deletes never reach a split page)
-  put_leaf_sum(a.sum, ga_offset(s.dest), highest, sibling,
-               (uint32_t)lane < c ? key_fp(key) : 0u);
+  put_leaf_sum(a.sum, ga_offset(s.dest), highest, (uint32_t)lane < c ? key_fp(key) : 0u);
   return lowest;
 }
 
@@ -260,7 +259,7 @@ __device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint3
   store_page(a.arena, ga_offset(a.root), L.page);
   if (a.leaf_hw && lane_id() == 0) a.leaf_hw[ga_offset(a.root) >> 10] = kLeafHwFull;
   // the root page is internal now: its summary no longer describes a leaf
-  if (a.sum && lane_id() == 0) a.sum[(ga_offset(a.root) >> 10) * kSumBytes] = 0;
+  if (lane_id() == 0) clear_leaf_sum(a.sum, ga_offset(a.root));
 }
 
 // The page of `level` whose fences hold k: header walk from the root with
@@ -905,7 +904,7 @@ __global__ void k_empty_leaf(uint8_t* arena, uint64_t off, uint8_t* sum) {
   wave_lds_sync();
   if (lane_id() == 0) lp[kOffLeafRear / 4] = 1;
   store_page(arena, off, lp);
-  put_leaf_sum(sum, off, kKeyMax, 0, 0);
+  put_leaf_sum(sum, off, kKeyMax, 0);
 }
 
 __global__ void k_write_superblock(uint8_t* arena, Superblock sb) {

@@ -64,23 +64,25 @@ SHM_HD int hw_dma_lanes(uint32_t hw) {
   return hw >= (uint32_t)kLeafCardinality ? 64 : (kOffRecords + kLeafEntry * (int)hw + 15) / 16;
 }
 
-// Leaf summary (a side line per arena page, 128 B, not part of the page
-// bytes): what a get needs of a leaf in one HBM line instead of the page's
-// 1 KB.  Byte 0 = kSumLeaf while the line describes the current leaf (0 for
-// internal pages and pages never written as leaves); the sibling as a page
-// index (u32, 0 = none: page 0 is the superblock) at 4, the highest fence at
-// 8; fp[slot] (u16) at 16 + 2 slot = key_fp of the slot's key for a valid
-// slot (value != 0), 0 for an empty one.  A get reads the line, turns right
-// on k >= highest, and reads only the entries whose fp matches (false
-// positives ~ 53 / 65535 per leaf); every leaf writer keeps the line.
-constexpr uint32_t kSumBytes = 128;
-constexpr uint32_t kSumOffSibling = 4;
-constexpr uint32_t kSumOffHighest = 8;
-constexpr uint32_t kSumOffFp = 16;
+// Leaf summary (a side line per arena page, 64 B, not part of the page
+// bytes): what a get needs of a leaf in one HBM request instead of the
+// page's 1 KB.  The highest fence (u64) at 0; byte 8 = kSumLeaf while the
+// line describes the current leaf (0 for internal pages and pages never
+// written as leaves); fp[slot] (u8) at 9 + slot = key_fp of the slot's key for
+// a valid slot (value != 0), 0 for an empty one.  A get reads the line, turns
+// right on k >= highest (the sibling from the page header: a stale start,
+// rare), and reads only the entries whose fp matches (false positives
+// ~ 40 / 255 per leaf).  Every leaf writer keeps the line.  At 64 B per page
+// the lines of a 2^26-key shard (119 MB) and its leaf directory (64 MB) fit
+// the 256 MB Infinity Cache together.
+constexpr uint32_t kSumBytes = 64;
+constexpr uint32_t kSumOffHighest = 0;
+constexpr uint32_t kSumOffTag = 8;
+constexpr uint32_t kSumOffFp = 9;
 constexpr uint8_t kSumLeaf = 0xA5;
-static_assert(kSumOffFp + 2 * kLeafCardinality <= kSumBytes, "summary line");
+static_assert(kSumOffFp + kLeafCardinality <= kSumBytes, "summary line");
 SHM_HD uint32_t key_fp(uint64_t k) {
-  const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 48);
+  const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56);
   return f ? f : 1u;
 }
 

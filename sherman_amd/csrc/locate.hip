@@ -70,13 +70,14 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
     const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + off);
     if (match) {
       SumLine sl;
-      if (sum_read(a.sum, off, a.node, k, sl)) {
+      if (sum_read(a.sum, off, k, sl)) {
         if (k >= sl.highest) {  // turn right (Tree.cpp:626-629)
-          if (!sl.sibling) {
+          const uint64_t sib = page_sibling(a.arena + off);
+          if (!sib) {
             err |= kErrFence;
             break;
           }
-          ptr = sl.sibling;
+          ptr = sib;
           continue;
         }
         out = ptr;
