@@ -430,6 +430,40 @@ __device__ __forceinline__ void block_range(uint32_t n, uint32_t b, uint32_t nb,
   r1 = (uint32_t)(((uint64_t)(b + 1) * n + nb - 1) / nb);
 }
 
+// Segment of block range [r0, r1) holding the range's new page j (by_split
+// false: the running sum of seg_np passes j) or being its j-th split
+// (by_split: the j-th segment with seg_np > 0), one wave; before = the new
+// pages of the range's segments ahead of it.  g = r1 if the counts disagree.
+__device__ void find_seg(const uint32_t* np, uint32_t r0, uint32_t r1, uint32_t j, bool by_split,
+                         uint32_t& g, uint32_t& before) {
+  const int lane = lane_id();
+  uint32_t run_c = 0, run_np = 0;
+  for (uint32_t c0 = r0; c0 < r1; c0 += kWave) {
+    const uint32_t i = c0 + (uint32_t)lane;
+    const uint32_t v = i < r1 ? np[i] : 0u;
+    uint32_t ic = by_split ? (v ? 1u : 0u) : v, inp = v;  // inclusive scans over the wave
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t yc = (uint32_t)__shfl_up((int)ic, o), yn = (uint32_t)__shfl_up((int)inp, o);
+      if (lane >= o) {
+        ic += yc;
+        inp += yn;
+      }
+    }
+    const uint64_t m = ballot(run_c + ic > j);
+    if (m) {
+      const int l = ctz64(m);
+      g = c0 + (uint32_t)l;
+      before = run_np + rl32(inp - v, l);
+      return;
+    }
+    run_c += rl32(ic, kWave - 1);
+    run_np += rl32(inp, kWave - 1);
+  }
+  g = r1;
+  before = run_np;
+}
+
 // wait until *cnt == want (the sibling builders of a split have read page 0)
 __device__ __forceinline__ bool fan_in(uint32_t* cnt, uint32_t want) {
   uint32_t ok = 1;
@@ -595,10 +629,24 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   // leaf level: the upsert kernel left per-range new-page / split counts
   const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
   const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
-  const uint32_t total = block_sum(v_np, s_red);
-  const uint32_t nsplit = block_sum(v_ns, s_red);
-  const uint32_t pre_np = block_sum((uint32_t)t < b ? v_np : 0u, s_red);
-  const uint32_t pre_ns = block_sum((uint32_t)t < b ? v_ns : 0u, s_red);
+  // per-range prefixes of new pages and splits (every block alike): a wave
+  // finds its task's block range by them and its segment by a scan of that
+  // range's seg_np, so no block waits for another's list
+  __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
+  uint32_t total, nsplit;
+  {
+    const uint32_t xnp = block_scan(v_np, s_red, &total);
+    const uint32_t xns = block_scan(v_ns, s_red, &nsplit);
+    if ((uint32_t)t < nb) {
+      s_pnp[t] = xnp;
+      s_pns[t] = xns;
+    }
+    if (t == 0) {
+      s_pnp[nb] = total;
+      s_pns[nb] = nsplit;
+    }
+    __syncthreads();
+  }
   bool ok = true;
   uint32_t nsep = 0;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
@@ -607,39 +655,24 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     // arena exhausted: the flagged segments stay unapplied (reported)
     err |= kErrNoMem;
   } else if (total) {
-    // ---- P2: this block's segment range in order -> its split list, at the
-    // global positions the upsert kernel's per-range counts give ------------
-    uint32_t r0, r1;
-    block_range(ns, b, nb, r0, r1);
-    uint32_t run_np = pre_np, run_ns = pre_ns;
-    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
-      const uint32_t g = c0 + (uint32_t)t;
-      const uint32_t np = g < r1 ? a.seg_np[g] : 0u;
-      uint32_t tnp, tns;
-      const uint32_t xnp = block_scan(np, s_red, &tnp);
-      const uint32_t xns = block_scan(np ? 1u : 0u, s_red, &tns);
-      if (np) {
-        a.spl_seg[run_ns + xns] = g;
-        a.spl_base[run_ns + xns] = run_np + xnp;
-      }
-      run_np += tnp;
-      run_ns += tns;
-    }
-    __syncthreads();  // the block's split list is complete (workgroup scope)
-    stamp();
     // ---- P3: every wave of the grid takes new right siblings, then pages 0,
     // from the whole split list: the splits of a block range vary (a few
     // per block on average, several times that on some), and the slowest
     // block held every other at the next barrier (block-local P3: 13 us of
     // work, 19 us of barrier wait per C5 chunk, phase clock)
-    ok = grid_sync(ctl, nb, &s_flag);
     stamp();
     const uint64_t first = cursor;  // arena page of global new page 0
     const uint64_t xroot = cursor + total;  // the root's left half (grow0)
     for (uint32_t gp = (uint32_t)wid; ok && gp < total; gp += (uint32_t)W) {
-      const uint32_t k = last_le(a.spl_base, nsplit, gp);
-      const uint32_t g = a.spl_seg[k];
-      const uint32_t pb = a.spl_base[k];
+      const uint32_t r = last_le(s_pnp, nb, gp);
+      uint32_t r0, r1, g, before;
+      block_range(ns, r, nb, r0, r1);
+      find_seg(a.seg_np, r0, r1, gp - s_pnp[r], false, g, before);
+      if (g >= r1) {
+        err |= kErrPlan;
+        continue;
+      }
+      const uint32_t pb = s_pnp[r] + before;
       const int p = (int)(gp - pb) + 1;
       const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
@@ -661,8 +694,15 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       }
     }
     for (uint32_t k = (uint32_t)wid; ok && k < nsplit; k += (uint32_t)W) {
-      const uint32_t g = a.spl_seg[k];
-      const uint32_t pb = a.spl_base[k];
+      const uint32_t r = last_le(s_pns, nb, k);
+      uint32_t r0, r1, g, before;
+      block_range(ns, r, nb, r0, r1);
+      find_seg(a.seg_np, r0, r1, k - s_pns[r], true, g, before);
+      if (g >= r1) {
+        err |= kErrPlan;
+        continue;
+      }
+      const uint32_t pb = s_pnp[r] + before;
       const int P = (int)a.seg_P[g];
       const uint64_t page = a.seg_page[g];
       if (!fan_in(a.leaf_rd + g, (uint32_t)(P - 1))) err |= kErrLock;

@@ -158,8 +158,6 @@ struct UpperArgs {
   const uint32_t* seg_np;
   const uint32_t* seg_ver;
   const uint32_t* ns_dev;
-  uint32_t* spl_seg;         // split segments in key order
-  uint32_t* spl_base;        // their first new page (exclusive scan)
   uint32_t* leaf_rd;         // per segment: sibling builders that read page 0 (zero between chunks)
   // internal levels: separators (key, child) and their target page, ping-pong
   uint64_t* sep_key[2];

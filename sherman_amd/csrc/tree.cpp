@@ -87,7 +87,7 @@ struct shm_tree {
   uint32_t* pnew = nullptr;
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
-  uint32_t *spl_seg = nullptr, *spl_base = nullptr, *leaf_rd = nullptr;
+  uint32_t* leaf_rd = nullptr;
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   uint64_t* ipage[2] = {nullptr, nullptr};
   uint32_t *h_end = nullptr, *h_T = nullptr, *h_P = nullptr, *h_ver = nullptr, *h_lk = nullptr;
@@ -563,8 +563,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.seg_np = t->seg_np;
   u.seg_ver = t->seg_ver;
   u.ns_dev = d_ns;
-  u.spl_seg = t->spl_seg;
-  u.spl_base = t->spl_base;
   u.leaf_rd = t->leaf_rd;
   for (int i = 0; i < 2; ++i) {
     u.sep_key[i] = t->sep_key[i];
@@ -645,7 +643,7 @@ void free_all(shm_tree* t) {
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->seg_lb); F(t->bsum64);
   F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
-  F(t->ctl); F(t->spl_seg); F(t->spl_base); F(t->leaf_rd);
+  F(t->ctl); F(t->leaf_rd);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
@@ -913,8 +911,6 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->oslot, n);
   rc |= dalloc(&t->pnew, t->cap_pages);
   rc |= dalloc(&t->ctl, 1);
-  rc |= dalloc(&t->spl_seg, segcap);
-  rc |= dalloc(&t->spl_base, segcap);
   rc |= dalloc(&t->leaf_rd, segcap);
   for (int i = 0; i < 2; ++i) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);

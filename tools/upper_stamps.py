@@ -3,9 +3,9 @@
 Builds a tree of 2^keys_log2 keys, then applies C5-like insert batches
 (1 Mi ops, key = to_key(1 + zipf(0.99) over twice the key set)) and C3-like
 ones (zipf over the stored keys: updates only) and prints, per batch, the
-microseconds between k_upper's phase stamps (block 0's view: start, lock
-release, leaf P2, barrier, P3, barrier, then I1 / barrier / I2 / barrier /
-I3 / barrier per internal level, deletes, end)."""
+microseconds between k_upper's phase stamps (block 0's view: prefix sums,
+leaf builds, barrier, then I1 / barrier / I2 / I3 / barrier per internal
+level, deletes, end)."""
 import ctypes
 import os
 import sys
