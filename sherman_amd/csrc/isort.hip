@@ -169,11 +169,12 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
 //      batch order leaves exactly these);
 //   b. counting sort of the survivors by the next 8 key bits (the bin's
 //      keys share the top 8 bits of their offset in the shard range);
-//   c. two passes of in-register wave sorts over 64-key windows, the second
-//      offset by 32: a sub-bucket of <= 32 keys lies inside one window of
-//      one of the passes, and windows never reorder keys across sub-buckets,
-//      so the bin ends fully sorted.  A sub-bucket > 32 (skewed keys) sorts
-//      the whole bin with the LDS bitonic network instead;
+//   c. each survivor's place inside its sub-bucket by rank: the number of
+//      the sub-bucket's keys below its own (keys are unique after a.; the
+//      sub-bucket's keys are LDS broadcast reads for the lanes that share
+//      it), its value fetched from `vals` meanwhile into LDS at that place.
+//      A sub-bucket > 64 (skewed keys) sorts the whole bin with the LDS
+//      bitonic network instead (values then fetched in d.);
 //   d. each survivor's value classifies it as an upsert or a delete (value 0
 //      = kValueNull, Tree.cpp:881); local ranks by one block scan.
 // The bin's (upserts, deletes) give its place among the bins (bin_prefix),
@@ -374,15 +375,17 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
                                                    uint64_t* __restrict__ counts,
                                                    uint32_t* __restrict__ err,
                                                    uint32_t* __restrict__ S,
-                                                   const uint32_t* gate, uint32_t tag) {
+                                                   const uint32_t* gate, uint32_t tag,
+                                                   uint64_t* __restrict__ stamps) {
   constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
   __shared__ unsigned long long hkey[kUniqSlots];  // hash, then the sorted keys
   __shared__ uint32_t hidx[kUniqSlots];            // 1 + op index, then op index
+  __shared__ uint64_t hval[kUniqCap];               // the survivors' values in key order (c.)
   __shared__ uint32_t hist[kFine];
   __shared__ uint32_t wsum[kIT / kWave];
   __shared__ uint32_t s_big;
   __shared__ uint32_t s_cnt2[2];
-  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   // the coarse pass is complete: clear its group sums for the next batch
   if (b == 0)
@@ -391,6 +394,11 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     if (b == 0 && t == 0) counts[0] = counts[1] = 0;
     return;
   }
+  // diagnostic phase clock (shm__upper_stamps): stamps[p * kCoarse + b]
+  auto bstamp = [&](int p) {
+    if (stamps && t == 0) stamps[p * kCoarse + b] = wall_clock64();
+  };
+  bstamp(0);
   const uint32_t start = bins[2 * b], cnt = bins[2 * b + 1];
   if (cnt > (uint32_t)kUniqCap) {  // block-uniform
     big_bin_unique(keys1, pay1, kscr, iscr, start, cnt, vals, lrank, s_cnt2,
@@ -437,6 +445,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     }
   }
   __syncthreads();
+  bstamp(1);
   // b. survivors (this thread's SPT slots) ranked by the fine digit
   uint64_t sk[SPT];
   uint32_t si[SPT], rk[SPT];
@@ -448,7 +457,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   }
   __syncthreads();
   const uint32_t hc = t < kFine ? hist[t] : 0u;
-  if (hc > 32) s_big = 1;
+  if (hc > 64) s_big = 1;
   uint32_t u;
   const uint32_t hex = block_scan(hc, wsum, &u);  // ends with a barrier
   if (t < kFine) hist[t] = hex;
@@ -462,22 +471,46 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     }
   }
   __syncthreads();
+  bstamp(2);
   // c. finish the order
   if (!s_big) {
-    for (int pass = 0; pass < 2; ++pass) {
-      const uint32_t off = pass ? 32u : 0u;
-      for (uint32_t w0 = off + 64u * (uint32_t)wv; w0 < u; w0 += 64u * (kIT / kWave)) {
-        const uint32_t o = w0 + (uint32_t)lane;
-        uint64_t k = o < u ? hkey[o] : kKeyMax;
-        uint32_t ix = o < u ? hidx[o] : ~0u;
-        wave_sort64(k, ix);
-        if (o < u) {
-          hkey[o] = k;
-          hidx[o] = ix;
-        }
+    constexpr int RP = (kUniqCap + kIT - 1) / kIT;
+    uint64_t mk[RP], mv[RP];
+    uint32_t mi[RP], dst[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) {
+      const uint32_t p = (uint32_t)(r * kIT + t);
+      mk[r] = kKeyMax;
+      mv[r] = 0;
+      mi[r] = 0;
+      dst[r] = 0;
+      if (p < u) {
+        mk[r] = hkey[p];
+        mi[r] = hidx[p];
+        mv[r] = vals[mi[r]];  // in flight during the rank loop
       }
-      __syncthreads();
     }
+#pragma unroll
+    for (int r = 0; r < RP; ++r) {
+      const uint32_t p = (uint32_t)(r * kIT + t);
+      if (p < u) {
+        const uint32_t d = fine_of(mk[r], kr);
+        const uint32_t bs = hist[d], be = d + 1 < (uint32_t)kFine ? hist[d + 1] : u;
+        uint32_t rank = 0;
+        for (uint32_t q = bs; q < be; ++q) rank += hkey[q] < mk[r] ? 1u : 0u;
+        dst[r] = bs + rank;
+      }
+    }
+    __syncthreads();  // every rank read before the first move
+#pragma unroll
+    for (int r = 0; r < RP; ++r) {
+      if ((uint32_t)(r * kIT + t) < u) {
+        hkey[dst[r]] = mk[r];
+        hidx[dst[r]] = mi[r];
+        hval[dst[r]] = mv[r];
+      }
+    }
+    __syncthreads();
   } else {
     uint32_t m = 2;
     while (m < u) m <<= 1;
@@ -488,6 +521,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     __syncthreads();
     lds_bitonic<kUniqSlots / kIT>(reinterpret_cast<uint64_t*>(hkey), hidx, m);
   }
+  bstamp(3);
   // d. classify and rank: thread t owns survivors [E t, E t + E); then the
   // bin's place among the bins, and its survivors straight to uk / uv / dk
   constexpr int E = (kUniqCap + kIT - 1) / kIT;
@@ -501,7 +535,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     ov[r] = 0;
     if (o < u) {
       ok[r] = hkey[o];
-      ov[r] = vals[hidx[o]];
+      ov[r] = s_big ? vals[hidx[o]] : hval[o];
       if (ov[r] == kValueNull) isdel |= 1u << r;
       ++nloc;
     }
@@ -510,8 +544,10 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   // one scan of (upserts << 16 | deletes): a bin holds <= 6144 survivors
   uint32_t tot;
   const uint32_t ex = block_scan(((nloc - ndl) << 16) | ndl, wsum, &tot);
+  bstamp(4);
   uint32_t bu, bd;
   bin_prefix(lbw, b, tag, tot >> 16, tot & 0xFFFF, wsum, bu, bd, counts, err);
+  bstamp(5);
   uint32_t ru = bu + (ex >> 16), rd = bd + (ex & 0xFFFF);
 #pragma unroll
   for (int r = 0; r < E; ++r) {
@@ -525,6 +561,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
       }
     }
   }
+  bstamp(6);
 }
 
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
@@ -542,10 +579,10 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, hipStream_t s) {
+                       uint32_t tag, uint64_t* stamps, hipStream_t s) {
   const KeyRange kr{key_lo, key_bits};
   hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
-                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag);
+                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag, stamps);
 }
 
 }  // namespace dev

@@ -189,6 +189,8 @@ struct UpperArgs {
   uint64_t* stamps;
 };
 constexpr int kUpperStamps = 32;
+// diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins
+constexpr int kStampWords = kUpperStamps + 8 * 256;
 uint32_t upper_blocks();
 void launch_upper(const UpperArgs& a, hipStream_t s);
 
@@ -241,7 +243,7 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, hipStream_t s);
+                       uint32_t tag, uint64_t* stamps, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);

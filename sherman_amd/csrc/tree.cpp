@@ -480,7 +480,7 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
                          reinterpret_cast<uint64_t*>(t->bins + 2 * dev::kCoarse), t->kb, t->ic,
                          t->uk, t->uv, t->dk, t->d_counts, t->d_err, t->part_S, &t->ctl->gate,
-                         tag, s);
+                         tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, s);
   DBG(s, "ordering");
   return SHM_OK;
 }
@@ -1251,13 +1251,13 @@ int shm__upper_stamps(shm_tree* t, int enable, uint64_t* out) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   if (enable == 1 && !t->stamps) {
-    if (hipMalloc(&t->stamps, sizeof(uint64_t) * dev::kUpperStamps) != hipSuccess)
+    if (hipMalloc(&t->stamps, sizeof(uint64_t) * dev::kStampWords) != hipSuccess)
       return SHM_ENOMEM;
-    HIP_OK(hipMemset(t->stamps, 0, sizeof(uint64_t) * dev::kUpperStamps));
+    HIP_OK(hipMemset(t->stamps, 0, sizeof(uint64_t) * dev::kStampWords));
   }
   if (out && t->stamps) {
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out, t->stamps, sizeof(uint64_t) * dev::kUpperStamps,
+    HIP_OK(hipMemcpy(out, t->stamps, sizeof(uint64_t) * dev::kStampWords,
                      hipMemcpyDeviceToHost));
   }
   if (enable == 0 && t->stamps) {

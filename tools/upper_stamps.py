@@ -32,7 +32,7 @@ def main():
     fn = lib.shm__upper_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     fn(t.h, 1, None)
-    out = (ctypes.c_uint64 * 32)()
+    out = (ctypes.c_uint64 * (32 + 8 * 256))()
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     for name, zn in (("c5", 2 * n), ("c3", n)):
@@ -48,6 +48,15 @@ def main():
             ts = [int(out[i]) for i in range(1, cnt)]
             d = [round((ts[i] - ts[i - 1]) / 100.0, 1) for i in range(1, len(ts))]  # 100 MHz
             print(name, b, "total %.1f us" % ((ts[-1] - ts[0]) / 100.0), d, flush=True)
+            # k_bin_unique: per phase, mean / max over bins of the clock
+            # since the earliest bin's start (phases a, b, c, d, prefix, end)
+            bs = [[int(out[32 + p * 256 + x]) for x in range(256)] for p in range(7)]
+            t0 = min(bs[0])
+            row = []
+            for p in range(7):
+                v = [(x - t0) / 100.0 for x in bs[p] if x]
+                row.append("%.1f/%.1f" % (sum(v) / max(len(v), 1), max(v) if v else 0))
+            print("   bin_unique phases (mean/max us):", " ".join(row), flush=True)
     fn(t.h, 0, None)
     t.close()
 
