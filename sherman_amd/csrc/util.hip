@@ -84,6 +84,10 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
     return;
   }
   const uint64_t nv = dev_n(n_dev, n);
+  if ((uint64_t)b * kSegTile >= nv) {  // past the device count (the grid covers n)
+    if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
+    return;
+  }
   const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint32_t h[kScanPer], c = 0;
 #pragma unroll
@@ -134,7 +138,6 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
     if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
     if (i + 1 == nv) *num_seg = pos;
   }
-  if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
 }
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
