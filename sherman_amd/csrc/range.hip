@@ -101,11 +101,19 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
   RPage w;
   uint64_t p = 0;
   int hops = 0;
+  uint32_t hw = kLeafCardinality;  // slots of the current leaf that may be valid
   if (act) {
     p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
     if (!ptr_ok(p, a.node, a.arena_bytes)) {
       err |= kErrBadPtr;
       act = false;
+    } else if (a.leaf_hw) {
+      // the start page's last 256 B only if its occupancy bound reaches
+      // slot 40 (internal pages: kLeafHwFull, read whole)
+      const uint32_t h = a.leaf_hw[ga_offset(p) >> 10];
+      rload3(a.arena, p, li, w);
+      if (h >= kChunk3Hw) rload_last(a.arena, p, li, w);
+      hw = h < (uint32_t)kLeafCardinality ? h : (uint32_t)kLeafCardinality;
     } else {
       rload(a.arena, p, li, w);
     }
@@ -141,6 +149,7 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
           desc = false;
         } else {
           p = np;
+          hw = kLeafCardinality;  // read whole below
         }
       } else {
         desc = false;  // a leaf: w holds it
@@ -151,9 +160,8 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
   }
 
   // ---- scan the leaf chain; w holds leaf p ------------------------------------
-  // (the start leaf whole; a sibling's bytes past slot hw - 1 are not read)
+  // (a leaf's bytes past slot hw - 1 are not read)
   const int ebase = chunk_base<kRE>(li);
-  uint32_t hw = kLeafCardinality;  // slots of the current leaf that may be valid
   while (ballot(act)) {
     if (act) rstage(lp, li, w);
     wave_lds_sync();
