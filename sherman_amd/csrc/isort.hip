@@ -427,8 +427,15 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   if (t < kFine) hist[t] = 0;
   if (t == 0) s_big = 0;
   __syncthreads();
+  // the op that claims a key's slot also takes the key's rank in its fine
+  // sub-bucket, so b. touches only the claimed slots
+  uint64_t ck[kUniqPer];
+  uint32_t ch[kUniqPer], cr[kUniqPer];
 #pragma unroll
   for (int r = 0; r < kUniqPer; ++r) {
+    ch[r] = ~0u;
+    ck[r] = 0;
+    cr[r] = 0;
     const uint32_t o = (uint32_t)(r * kIT + t);
     if (o >= cnt) continue;
     const uint64_t k = keys1[start + o];
@@ -437,6 +444,11 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     for (int probe = 0; probe < kUniqSlots; ++probe) {
       const unsigned long long old = atomicCAS(&hkey[h], (unsigned long long)kKeyMax,
                                                (unsigned long long)k);
+      if (old == kKeyMax) {
+        ch[r] = h;
+        ck[r] = k;
+        cr[r] = atomicAdd(&hist[fine_of(k, kr)], 1u);
+      }
       if (old == kKeyMax || old == k) {
         atomicMax(&hidx[h], ix + 1u);
         break;
@@ -446,28 +458,22 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   }
   __syncthreads();
   bstamp(1);
-  // b. survivors (this thread's SPT slots) ranked by the fine digit
-  uint64_t sk[SPT];
-  uint32_t si[SPT], rk[SPT];
-#pragma unroll
-  for (int r = 0; r < SPT; ++r) {
-    sk[r] = hkey[SPT * t + r];
-    si[r] = hidx[SPT * t + r] - 1u;
-    rk[r] = sk[r] != kKeyMax ? atomicAdd(&hist[fine_of(sk[r], kr)], 1u) : 0u;
-  }
-  __syncthreads();
+  // b. survivors placed by fine digit: sub-bucket base + the claim's rank
   const uint32_t hc = t < kFine ? hist[t] : 0u;
   if (hc > 64) s_big = 1;
   uint32_t u;
   const uint32_t hex = block_scan(hc, wsum, &u);  // ends with a barrier
   if (t < kFine) hist[t] = hex;
-  __syncthreads();
+  uint32_t ci[kUniqPer];
 #pragma unroll
-  for (int r = 0; r < SPT; ++r) {
-    if (sk[r] != kKeyMax) {
-      const uint32_t p = hist[fine_of(sk[r], kr)] + rk[r];
-      hkey[p] = sk[r];
-      hidx[p] = si[r];
+  for (int r = 0; r < kUniqPer; ++r) ci[r] = ch[r] != ~0u ? hidx[ch[r]] - 1u : 0u;
+  __syncthreads();  // every claimed slot read (and hist scanned) before the moves
+#pragma unroll
+  for (int r = 0; r < kUniqPer; ++r) {
+    if (ch[r] != ~0u) {
+      const uint32_t p = hist[fine_of(ck[r], kr)] + cr[r];
+      hkey[p] = ck[r];
+      hidx[p] = ci[r];
     }
   }
   __syncthreads();
