@@ -168,7 +168,9 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
 //      survivors are the batch's last writers (Tree.cpp:878-889 applied in
 //      batch order leaves exactly these);
 //   b. counting sort of the survivors by the next 8 key bits (the bin's
-//      keys share the top 8 bits of their offset in the shard range);
+//      keys share the top 8 bits of their offset in the shard range): the
+//      op that claims a key's slot in a. takes the key's rank in its
+//      sub-bucket, b. places the claimed keys at sub-bucket base + rank;
 //   c. each survivor's place inside its sub-bucket by rank: the number of
 //      the sub-bucket's keys below its own (keys are unique after a.; the
 //      sub-bucket's keys are LDS broadcast reads for the lanes that share
