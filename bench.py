@@ -96,9 +96,13 @@ def parse():
                    help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
                         "range partition (the per-GPU work of an N-GPU run, no exchange)")
     p.add_argument("--sim-rank", type=int, default=0)
-    p.add_argument("--start", choices=("dir", "root"), default="dir",
-                   help="where gets and locates start: the leaf directory (default) or the "
-                        "root (a descent through the cached upper levels; A/B for DESIGN §8)")
+    p.add_argument("--start", choices=("dir", "root", "lds"), default="dir",
+                   help="where gets and locates start: the leaf directory (default), the "
+                        "root (a descent through the cached upper levels) or an LDS replica "
+                        "of the top levels (gets only; A/B for DESIGN §8)")
+    p.add_argument("--index-stats", action="store_true",
+                   help="c2: an untimed pass over the profile steps counting the walk's "
+                        "directory misses, right moves and entry reads (shm_index_stats)")
     p.add_argument("--no-range-hint", action="store_true",
                    help="do not pass the shard key range to the tree (A/B)")
     p.add_argument("--router", choices=("auto", "cabi", "python"), default="auto",
@@ -197,8 +201,13 @@ def main():
     # N > 1: a rank receives ~batch routed keys (+ a few %), keep one chunk
     tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch + (batch >> 2 if world > 1 else 0)), device=local,
                     node_id=rank, sort_gets={"on": True, "off": False}.get(args.sort, "auto"), key_lo=key_lo, key_bits=key_bits,
-                    leaf_dir=args.start == "dir")
+                    leaf_dir=args.start == "dir", top_lds=args.start == "lds")
 
+    c1 = None
+    if world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
+        # the reference benchmark's tree, one insert at a time on a host
+        # thread while the GPU work runs (cpu_baseline_c1)
+        c1 = C1Build()
     t0 = time.time()
     keys_local, inserted = build_shard(tree, n_keys, s_world, s_rank, dev)
     n_keys = inserted if sim else n_keys
@@ -218,8 +227,10 @@ def main():
     found = torch.empty(batch, dtype=torch.uint8, device=dev)
     if args.workload == "c2":
         if world == 1:
-            qs = [keys_local[torch.randint(0, n_keys, (batch,), device=dev, generator=g)]
+            # qi: the ids' positions (keys_local[j] = key(j + 1), value 2 (j + 1))
+            qi = [torch.randint(0, n_keys, (batch,), device=dev, generator=g)
                   for _ in range(N_BATCHES)]
+            qs = [keys_local[i] for i in qi]
         else:
             qs = []
             for _ in range(N_BATCHES):
@@ -302,6 +313,13 @@ def main():
                           (op_idx[~is_scan] + 1).contiguous()))
         del keys_local
         route = ShardRouter(tree, world, dist, cshard=cshard) if world > 1 else None
+        # routed scans: every rank passes the same piece-matrix width, the
+        # largest scan count of any rank's batches (shm_shard_range_query)
+        n_cap = max(m[0].numel() for m in mixed)
+        if dist is not None:
+            nc = torch.tensor([n_cap], dtype=torch.int64, device=dev)
+            dist.all_reduce(nc, op=dist.ReduceOp.MAX)
+            n_cap = int(nc.item())
         scan_out = {}
         applied = [0]  # batches applied so far (all step loops)
 
@@ -319,11 +337,11 @@ def main():
                 scan_out["r"] = PendingRange(None, *tree.range_query_batch(lo, hi))
                 tree.insert_batch_async(pk, pv)
             else:
-                scan_out["r"] = PendingRange(None, *route.range_query(lo, hi))
+                scan_out["r"] = PendingRange(None, *route.range_query(lo, hi, n_cap))
                 route.insert(pk, pv)
     else:
         zipf = Zipf(n_keys, args.theta, dev)
-        mixed = []
+        mixed, c3_ids = [], []
         for b in range(N_BATCHES):
             ids = zipf.sample(batch, g) + 1  # key(1 + zipf_next())
             k = torch.empty_like(ids)
@@ -332,6 +350,8 @@ def main():
             op_idx = torch.arange(b * batch, (b + 1) * batch, dtype=torch.int64, device=dev)
             mixed.append((k[is_get].contiguous(), k[~is_get].contiguous(),
                           (op_idx[~is_get] + 1).contiguous()))
+            if b < 2:  # the gets' ids: their preload value is 2 id (parity)
+                c3_ids.append(ids[is_get].contiguous())
         del keys_local
 
         def step(i):
@@ -345,14 +365,14 @@ def main():
     cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
-            cpu, parity = cpu_baseline_get(tree, qs, vals, found, args, step, dev)
+            parity = parity_get(qs[0], qi[0], vals, found, step)
         elif args.workload == "c5":
-            cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step)
+            cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step, n_keys)
         else:
-            cpu, parity = cpu_baseline_mixed(tree, mixed, vals, found, args, step)
+            cpu, parity = cpu_baseline_mixed(tree, mixed, c3_ids, vals, found, args, step)
 
     # ---- timed steps --------------------------------------------------------
-    if cpu is not None:
+    if cpu is not None or parity is not None:
         # the CPU baseline left the GPU idle for ~10 s; the first tens of
         # steps after such a pause ran up to 5x slower (measured: C5 563
         # against 3059 Mops/s with a 1 s baseline), so re-warm the device
@@ -366,6 +386,10 @@ def main():
     for i in range(args.steps):
         step(i)
     host_issue = time.perf_counter() - t_start  # host time to issue the steps
+    if cshard is not None:
+        # inside the timed region: a routed insert's overflow tails (applied
+        # by the next call on the shard) are part of the step's work
+        cshard.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
     tree.synchronize()  # raises any error of the queued batches
@@ -429,6 +453,21 @@ def main():
     torch.cuda.synchronize()
     prof = tree.profile_read(reset=True)
     tree.profile(False)
+    idx = None
+    if args.index_stats and args.workload == "c2":
+        tree.profile(False, index_stats=True)
+        for i in range(max(args.profile_steps, 1)):
+            one(i)
+        torch.cuda.synchronize()
+        idx = tree.index_stats()
+        tree.profile(False)
+        g_ = max(idx["gets"], 1)
+        idx.update({k + "_per_get": round(idx[k] / g_, 4)
+                    for k in ("start_internal", "right_moves", "page_hops", "entry_reads")})
+    if c1 is not None:
+        # C1 on the host cores, after every GPU measurement (the oracle's
+        # build has run beside them)
+        cpu = c1.bench(args.cpu_seconds)
     walk_ms = prof["walk_ms"] / max(prof["calls"], 1)
     ins_ms = prof["insert_ms"] / max(prof["insert_calls"], 1)
     ups_ms = prof["upsert_ms"] / max(prof["insert_calls"], 1)
@@ -536,6 +575,28 @@ def main():
                                          [round(x, 1) for x in lat])),
             "cluster_sum_mops": round(cluster_sum, 2),
         }
+        if idx is not None:
+            out["index_stats"] = idx
+        if args.workload == "c2":
+            step_s = elapsed / args.steps
+            rf = out["roofline"]
+            rf["alg_bytes_note"] = (
+                "%d B/get: %s" % (bpg, "the summary walk's three random 128 B lines (directory "
+                                  "entry, leaf summary, entry) + 8 B key + 8 B value, DESIGN §3's "
+                                  "redefinition of SURVEY §8d's 1040 B whole-leaf read"
+                                  if not page_walk else "SURVEY §8d (1 KB leaf + key + value)"))
+            rf["reference_bytes_frac"] = (round(rf["reference_bytes_GBps"] / HBM_PEAK_GBS, 4)
+                                          if rf["reference_bytes_GBps"] else None)
+            # the timed steps themselves (two walks in flight on two streams):
+            # algorithmic bytes of one batch over one step
+            rf["step_frac"] = round(q_per_launch * bpg / step_s / 1e9 / HBM_PEAK_GBS, 4) \
+                if q_per_launch else None
+            # request roofline: the walk is bound by random 128 B requests,
+            # not bytes: measured TCC read requests per get (PMC)
+            # x gets/s of the timed steps / the measured random-request ceiling
+            req = _request_roofline(batch, args.keys_log2, mops * 1e6 / world, page_walk)
+            if req:
+                rf.update(req)
         if args.workload == "c5":
             # the insert pipeline dominates: ops x 1074 B over its measured
             # chunk time (HIP events on the insert stream)
@@ -596,6 +657,29 @@ def _profile_traffic(name, field, batch, keys_log2, kernel=None):
     if pmc.get("batch") == batch and pmc.get("keys_log2") == keys_log2:
         return pmc.get(field)
     return None
+
+
+def _request_roofline(batch, keys_log2, gets_per_s, page_walk):
+    """requests/get from the committed PMC pass (profiles/pmc_walk.json,
+    TCC_EA0_RDREQ per launch, tools/fold_c2.py) when it was taken at this
+    batch and key count, the random-request ceiling from
+    profiles/cal_fetch.json: {request_frac, ...} or {}."""
+    if page_walk:
+        return {}
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_walk.json")))
+        cal = json.load(open(os.path.join(ROOT, "profiles", "cal_fetch.json")))
+    except (OSError, ValueError):
+        return {}
+    if not (pmc.get("batch") == batch and pmc.get("keys_log2") == keys_log2 and
+            pmc.get("tcc_ea_rdreq_per_launch") and "k_get_sum" in pmc.get("kernel", "")):
+        return {}
+    rpg = pmc["tcc_ea_rdreq_per_launch"] / batch
+    ceil = cal.get("walk_mix_ceiling_G_per_s") or cal["random_request_ceiling_G_per_s"]
+    rate = rpg * gets_per_s / 1e9
+    return {"requests_per_get": round(rpg, 3), "requests_G_per_s": round(rate, 2),
+            "request_ceiling_G_per_s": ceil, "request_frac": round(rate / ceil, 4),
+            "request_source": "profiles/pmc_walk.json (TCC_EA0_RDREQ), profiles/cal_fetch.json"}
 
 
 def make_cshard(tree, world, rank, dist, dev, args, keys_local):
@@ -691,92 +775,137 @@ C1_WARM = 0.8              # kWarmRatio (test/benchmark.cpp:22)
 C1_PRELOAD = 1024000       # test/benchmark.cpp:269-274
 
 
-def c1_tree_image(dev):
+class C1Build:
     """The reference benchmark's tree at C1 (kKeySpace = 2^26 WITH the
-    modulus): preload to_key(i) -> 2i for i = 1..1,024,000, then the warm-up
-    inserts to_key(i) -> 2i for i in [1, 0.8 * kKeySpace) (the preload is a
-    subset with the same values), built through the GPU batch insert (the
-    same key -> value contents; keys that collide under the modulus keep the
-    largest i, one of the orders the reference's racing warm-up threads can
-    produce).  Returns (image, root) for the oracle."""
+    modulus), built the way test/benchmark.cpp builds it: one Tree::insert at
+    a time (the oracle's restatement, 27/27 leaf splits), node 0's preload
+    to_key(i) -> 2i for i = 1..1,024,000 (benchmark.cpp:269-274), then the
+    warm-up to_key(i) -> 2i for i in [1, 0.8 kKeySpace) in order
+    (benchmark.cpp:114-120).  ~55 M single inserts take about a minute on one
+    core, so the build runs on a host thread (ctypes releases the GIL) while
+    the GPU tree is built and measured; bench() joins it and times the read
+    phase."""
+
+    def __init__(self):
+        import threading
+        from oracle.pyoracle import OracleTree
+        self.orc = OracleTree(2 << 30)
+        self.t0 = time.time()
+        self.build_s = None
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _run(self):
+        self.orc.c1_build(C1_KEYSPACE, C1_WARM, C1_PRELOAD)
+        self.build_s = time.time() - self.t0
+
+    def bench(self, seconds):
+        """C1 (BASELINE.json configs[0]): the reference benchmark's measured
+        phase, kNodeCount = 1, kReadRatio = 100, zipf theta = 0 over
+        kKeySpace, restated in C (oracle/ orc_c1_bench: pinned threads, key =
+        to_key(zipf_next()), Tree::search, per-thread op counters sampled
+        every 2 s), on every CPU the process may use; the steady-state mean
+        over >= 5 two-second windows (test/benchmark.cpp:165-188, 302-341)."""
+        import numpy as np
+        self.th.join()
+        threads = _threads()
+        windows = max(5, int(round(seconds / 2.0)))
+        w = self.orc.c1_bench(threads, C1_KEYSPACE, theta=0.0, windows=windows, window_s=2.0)
+        rc, shape = self.orc.check()
+        self.orc.close()
+        return {
+            "value": round(float(np.mean(w[1:])), 3),
+            "unit": "Mops/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"C1: reference test/benchmark read phase restated in C (oracle/), "
+                      f"kKeySpace 2^26 with the modulus; tree built one Tree::insert at a time "
+                      f"in the reference's order (preload 1,024,000 + warm 0.8, {self.build_s:.0f} s): "
+                      f"{shape['keys']} keys, {shape['leaves']} leaves "
+                      f"({shape['keys'] / max(shape['leaves'], 1):.1f} keys/leaf = "
+                      f"{100 * shape['keys'] / max(shape['leaves'], 1) / 54:.1f} % of 54), "
+                      f"height {shape['height']}, check {rc}; uniform to_key(zipf(theta=0)) "
+                      f"searches, {threads} pinned threads on {cpu_name()}, {windows} x 2 s "
+                      f"windows (first dropped): " + ", ".join("%.2f" % x for x in w),
+        }
+
+
+def parity_get(q, qi, vals, found, step):
+    """One full C2 batch through the GPU path (step 0) against the values the
+    build wrote: query j is key(qi[j] + 1), stored with value 2 (qi[j] + 1),
+    so every get must be found with exactly that value (what Tree::search
+    returns over the same key stream; the expectation is the key stream's,
+    not the tree's own image)."""
     import torch
-    import sherman_amd as shm
-    t = shm.Tree(arena_bytes=3 << 30, max_batch=1 << 20, device=dev.index or 0)
-    end = int(C1_WARM * C1_KEYSPACE)
-    k = torch.empty(1 << 20, dtype=torch.int64, device=dev)
-    for first in range(1, end, 1 << 20):
-        m = min(1 << 20, end - first)
-        t.gen_keys(first, m, k[:m], keyspace=C1_KEYSPACE)
-        ids = torch.arange(first, first + m, dtype=torch.int64, device=dev)
-        t.insert_batch_async(k[:m], ids * 2)
-    t.synchronize()
-    img, root = t.dump_image()
-    t.close()
-    return img, root
-
-
-def cpu_baseline_c1(dev, seconds):
-    """C1 (BASELINE.json configs[0]): the reference benchmark's measured
-    phase, kNodeCount = 1, kReadRatio = 100, zipf theta = 0 over kKeySpace,
-    restated in C (oracle/ orc_c1_bench: pinned threads, key =
-    to_key(zipf_next()), Tree::search, per-thread op counters sampled every
-    2 s), on every CPU of the affinity mask; the steady-state mean over
-    >= 5 two-second windows (test/benchmark.cpp:165-188, 302-341)."""
-    import numpy as np
-    from oracle.pyoracle import OracleTree
-    img, root = c1_tree_image(dev)
-    orc = OracleTree(image=img, root_ptr=root)
-    threads = _threads()
-    windows = max(5, int(round(seconds / 2.0)))
-    w = orc.c1_bench(threads, C1_KEYSPACE, theta=0.0, windows=windows, window_s=2.0)
-    rc, shape = orc.check()
-    orc.close()
-    del img
-    return {
-        "value": round(float(np.mean(w[1:])), 3),
-        "unit": "Mops/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"C1: reference test/benchmark read phase restated in C (oracle/), "
-                  f"kKeySpace 2^26 with the modulus, {shape['keys']} keys (preload 1,024,000 + "
-                  f"warm 0.8), uniform to_key(zipf(theta=0)) searches, {threads} pinned "
-                  f"threads on {cpu_name()}, {windows} x 2 s windows (first dropped): "
-                  + ", ".join("%.2f" % x for x in w),
-    }
-
-
-def cpu_baseline_get(tree, qs, vals, found, args, step, dev):
-    """Parity of one full C2 batch against the oracle's Tree::search over the
-    GPU's own page image, then the C1 CPU baseline (cpu_baseline_c1)."""
-    import numpy as np
-    import torch
-
-    orc = _oracle_on_gpu_image(tree)
-    q0 = qs[0].cpu().numpy().view(np.uint64)
-    step(0)  # the same queries through the GPU path
+    step(0)
     torch.cuda.synchronize()
-    gv = vals.cpu().numpy().view(np.uint64)
-    gf = found.cpu().numpy()
-    ov, of, _ = orc.search_batch_mt(q0, _threads())
-    parity = bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
-    orc.close()
-    return cpu_baseline_c1(dev, args.cpu_seconds), parity
+    want = (qi + 1) * 2
+    return bool(torch.equal(vals, want) and bool(found.all()))
 
 
-def cpu_baseline_c5(tree, mixed, scan_out, args, step):
-    """C5 batches on the oracle over the GPU's image: the batch's range scans
-    (restated Tree::range_query) then its inserts (restated Tree::insert), on
-    every CPU of the affinity mask (inserts partitioned by page lock word,
-    orc_apply_batch_mt), for ~args.cpu_seconds.  Parity: the first
-    two batches' scans return the GPU's values per scan (as multisets: leaf
-    boundaries after the batched splits may differ from the one-op-at-a-time
-    oracle's, and slots inside a leaf are unsorted)."""
+def c5_model(tree, n_keys, dev):
+    """The C5 key -> value contents as sorted host arrays, built from the key
+    stream (key(i) -> 2i, i = 1..n_keys), not from the tree: the parity
+    model for the C5 scans."""
+    import numpy as np
+    import torch
+    k = torch.empty(n_keys, dtype=torch.int64, device=dev)
+    tree.gen_keys(1, n_keys, k)
+    sk, order = torch.sort(k ^ (-(1 << 63)))  # u64 order as int64
+    keys = (sk ^ (-(1 << 63))).cpu().numpy().view(np.uint64)
+    vals = ((order + 1) * 2).cpu().numpy().view(np.uint64)
+    del k, sk, order
+    return keys, vals
+
+
+def c5_model_scans(keys, vals, lo, hi):
+    """Per scan [lo, hi] the model's values (counts, concatenated values)."""
+    import numpy as np
+    left = np.searchsorted(keys, lo, "left")
+    right = np.maximum(np.searchsorted(keys, hi, "right"), left)
+    counts = (right - left).astype(np.int64)
+    total = int(counts.sum())
+    start = np.repeat(left - (np.cumsum(counts) - counts), counts)
+    return counts, vals[np.arange(total) + start]
+
+
+def c5_model_apply(keys, vals, pk, pv):
+    """The model after one insert batch (last writer in batch order)."""
+    import numpy as np
+    assert not (pv == 0).any()  # C5 values are op index + 1: no deletes
+    u, ix = np.unique(pk[::-1], return_index=True)
+    uv = pv[::-1][ix]
+    pos = np.searchsorted(keys, u)
+    hit = (pos < keys.size) & (keys[np.minimum(pos, keys.size - 1)] == u)
+    vals[pos[hit]] = uv[hit]
+    new = ~hit
+    return np.insert(keys, pos[new], u[new]), np.insert(vals, pos[new], uv[new])
+
+
+def same_multisets(counts, a, b):
+    """a and b hold the same values per segment (segments of `counts`)."""
+    import numpy as np
+    if a.size != b.size:
+        return False
+    sid = np.repeat(np.arange(counts.size), counts)
+    return bool(np.array_equal(a[np.lexsort((a, sid))], b[np.lexsort((b, sid))]))
+
+
+def cpu_baseline_c5(tree, mixed, scan_out, args, step, n_keys):
+    """C5 batches on the oracle over the GPU's image (the CPU timing leg):
+    the batch's range scans (restated Tree::range_query) then its inserts
+    (restated Tree::insert), on every CPU of the affinity mask (inserts
+    partitioned by page lock word, orc_apply_batch_mt), for
+    ~args.cpu_seconds.  Parity: the first two batches' scans return, per
+    scan, the values of a model of the contents built from the key stream
+    and the batches themselves (c5_model: preload, then batch 0's inserts),
+    as multisets (slots inside a leaf are unsorted)."""
     import numpy as np
     import torch
 
     orc = _oracle_on_gpu_image(tree, spare_bytes=2 << 30)  # C5 inserts new keys
     threads = _threads()
-    parity = True
+    gpu = []
     done, secs, b = 0, 0.0, 0
     while secs < args.cpu_seconds or b < 2:
         lo, hi, pk, pv = mixed[b % len(mixed)]
@@ -784,25 +913,27 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
             step(b)  # applies mixed[b]: the first two batches of the run
             torch.cuda.synchronize()
             gc, gv = scan_out["r"].result()
-            gc = gc.cpu().numpy()
-            gv = gv.cpu().numpy().view(np.uint64)
-            goff = np.concatenate([[0], np.cumsum(gc)])
+            gpu.append((gc.cpu().numpy(), gv.cpu().numpy().view(np.uint64)))
         loh = lo.cpu().numpy().view(np.uint64)
         hih = hi.cpu().numpy().view(np.uint64)
         pkh = pk.cpu().numpy().view(np.uint64)
         pvh = pv.cpu().numpy().view(np.uint64)
-        oc, ov, s1 = orc.range_query_batch_mt(loh, hih, threads)
+        _, _, s1 = orc.range_query_batch_mt(loh, hih, threads)
         s2 = orc.apply_batch_mt(pkh, pvh, threads)
         secs += s1 + s2
-        if b < 2:
-            ooff = np.concatenate([[0], np.cumsum(oc)]).astype(np.int64)
-            parity = parity and bool(np.array_equal(oc.astype(np.int64), gc))
-            for i in range(loh.size if parity else 0):
-                parity = parity and bool(np.array_equal(
-                    np.sort(ov[ooff[i]:ooff[i + 1]]), np.sort(gv[goff[i]:goff[i + 1]])))
         done += loh.size + pkh.size
         b += 1
     orc.close()
+    keys, vals = c5_model(tree, n_keys, torch.device(f"cuda:{tree.device}"))
+    parity = True
+    for bb in range(2):
+        lo, hi, pk, pv = (x.cpu().numpy().view(np.uint64) for x in mixed[bb])
+        mc, mv = c5_model_scans(keys, vals, lo, hi)
+        gc, gv = gpu[bb]
+        parity = parity and bool(np.array_equal(mc, gc.astype(np.int64))) and \
+            same_multisets(mc, mv, gv)
+        keys, vals = c5_model_apply(keys, vals, pk, pv)
+    del keys, vals
     cpu = {
         "value": round(done / secs / 1e6, 3),
         "unit": "Mops/s",
@@ -816,32 +947,43 @@ def cpu_baseline_c5(tree, mixed, scan_out, args, step):
     return cpu, parity
 
 
-def cpu_baseline_mixed(tree, mixed, vals, found, args, step):
-    """Mixed batches on the oracle over the GPU's image: gets on `threads`
-    pinned threads, then the batch's inserts on the same threads partitioned
-    by page lock word (orc_apply_batch_mt), for ~args.cpu_seconds.  Parity: the first two batches'
-    get results (the second sees the first's inserts) equal the GPU's."""
+def cpu_baseline_mixed(tree, mixed, c3_ids, vals, found, args, step):
+    """Mixed batches on the oracle over the GPU's image (the CPU timing leg):
+    gets on `threads` pinned threads, then the batch's inserts on the same
+    threads partitioned by page lock word (orc_apply_batch_mt), for
+    ~args.cpu_seconds.  Parity: the first two batches' gets return what the
+    stream wrote — batch 0 the preload value 2 id, batch 1 batch 0's last
+    write to the key or else 2 id (every get finds its key: the zipf draws
+    stored ids)."""
     import numpy as np
     import torch
 
     orc = _oracle_on_gpu_image(tree)
     threads = _threads()
     parity = True
+    last = None  # batch 0's last writer per key (sorted keys, values)
     done, secs, b = 0, 0.0, 0
     while secs < args.cpu_seconds or b < 2:
         gk, pk, pv = mixed[b % N_BATCHES]
+        gkh = gk.cpu().numpy().view(np.uint64)
+        pkh = pk.cpu().numpy().view(np.uint64)
+        pvh = pv.cpu().numpy().view(np.uint64)
         if b < 2:
             step(b)
             torch.cuda.synchronize()
             gv = vals[:gk.numel()].cpu().numpy().view(np.uint64)
             gf = found[:gk.numel()].cpu().numpy()
-        gkh = gk.cpu().numpy().view(np.uint64)
-        pkh = pk.cpu().numpy().view(np.uint64)
-        pvh = pv.cpu().numpy().view(np.uint64)
+            want = (c3_ids[b].cpu().numpy() * 2).astype(np.uint64)
+            if last is not None:
+                u, uv = last
+                pos = np.minimum(np.searchsorted(u, gkh), u.size - 1)
+                hit = u[pos] == gkh
+                want[hit] = uv[pos[hit]]
+            parity = parity and bool(np.array_equal(gv, want) and gf.all())
+            u, ix = np.unique(pkh[::-1], return_index=True)
+            last = (u, pvh[::-1][ix])
         ov, of, s = orc.search_batch_mt(gkh, threads)
         s += orc.apply_batch_mt(pkh, pvh, threads)
-        if b < 2:
-            parity = parity and bool(np.array_equal(ov, gv) and np.array_equal(of, gf))
         secs += s
         done += gkh.size + pkh.size
         b += 1

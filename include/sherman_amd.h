@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 5
+#define SHM_ABI_VERSION 6
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -63,6 +63,10 @@ extern "C" {
                                     reordered unless SHM_FLAG_SORT_GETS: the
                                     leaf-summary walk reads ~3 lines per get
                                     and ordering never pays */
+#define SHM_FLAG_TOP_LDS 0x8u    /* without SHM_FLAG_LEAF_DIR: gets start from
+                                    an LDS replica of the top of the tree (the
+                                    pages of the deepest upper level that fits
+                                    4096 entries) instead of the root */
 
 typedef struct shm_tree shm_tree;
 
@@ -73,7 +77,7 @@ typedef struct shm_config {
   uint16_t reserved0;
   uint32_t flags;        /* SHM_FLAG_* */
   uint64_t arena_bytes;  /* HBM page arena (1 KB pages), at most 4 TB (else SHM_EINVAL) */
-  uint64_t max_batch;    /* largest n accepted by a batch call */
+  uint64_t max_batch;    /* ops per device chunk of a batch call (< 2^24) */
   uint32_t num_locks;    /* HBM lock table words (reference: 16384) */
   uint32_t sort_bits;    /* top key bits that order gets: 0 or 16 */
   /* key range hint: this shard's keys lie in [key_lo, key_lo + 2^key_bits)
@@ -123,9 +127,12 @@ int shm_search_batch(shm_tree *t, const uint64_t *keys, uint64_t n,
  * vals[i] == 0 (kValueNull) deletes keys[i]. Mutating calls on one handle are
  * serialised internally. Returns once the batch has been applied on `stream`
  * (one host synchronisation, for the status): SHM_EINVAL if the batch held
- * kKeyMax (the max_batch chunk holding it is rejected whole, earlier chunks
- * stay applied), SHM_ENOMEM if the arena ran out (the splits that did not fit
- * are left unapplied), SHM_EIO on a device fault. */
+ * kKeyMax (the max_batch chunk holding it is rejected whole; the call's other
+ * chunks, before and after it, are applied), SHM_ENOMEM if the arena ran out
+ * (the splits that did not fit are left unapplied), SHM_EIO on a device fault
+ * (a chunk whose split propagation stopped keeps its leaf splits linked by
+ * sibling pointers, B-link reachable, and drops its parent updates and
+ * deletes; later chunks run normally). */
 int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
                      uint64_t n, void *stream);
 /* The same batch queued on `stream` without any host wait (the reference's
@@ -187,7 +194,7 @@ int shm_load_image(shm_tree *t, const void *host_buf, uint64_t bytes,
 int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
               uint64_t *n_keys);
 int shm_synchronize(shm_tree *t);
-/* Copy `bytes` (a multiple of 4, <= 256) of device memory at `src` to
+/* Copy `bytes` (a multiple of 4, <= 1024) of device memory at `src` to
  * host_out once the work queued on `stream` before it has produced them,
  * through the library's zero-copy read-back (one-wave kernel into mapped
  * host memory + a spin on a sequence word) instead of a D2H copy and a stream
@@ -213,8 +220,25 @@ typedef struct shm_profile_t {
   uint64_t range_queries;/* scans in those launches */
   double range_ms;       /* sum of k_range kernel time */
 } shm_profile_t;
+/* on: bit 0 = the event timing above, bit 1 = the index statistics below */
 int shm_profile_enable(shm_tree *t, int on);
 int shm_profile_read(shm_tree *t, shm_profile_t *out, int reset);
+
+/* Index statistics of the batched get walk (the role of the reference's
+ * Tree::index_cache_statistics / clear_statistics, include/Tree.h:62-63:
+ * how often the index cache — here the leaf directory or the LDS replica —
+ * took a get straight to its leaf), collected while shm_profile_enable bit
+ * 1 is on. */
+typedef struct shm_index_stats_t {
+  uint64_t gets;            /* queries walked */
+  uint64_t start_internal;  /* start page without a leaf summary: a directory
+                               miss, or a descent (no directory) */
+  uint64_t right_moves;     /* B-link right turns (a stale directory entry) */
+  uint64_t page_hops;       /* pages walked from their own bytes */
+  uint64_t entry_reads;     /* leaf entries read (fingerprint matches) */
+  uint64_t hits;            /* queries found */
+} shm_index_stats_t;
+int shm_index_stats(shm_tree *t, shm_index_stats_t *out, int reset);
 
 /* multi-GPU routing helpers (range shards: shard s owns
  * [s * 2^64 / P, (s+1) * 2^64 / P)) ------------------------------------------ */
@@ -241,14 +265,19 @@ int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *p
  * Rank r of P (P <= 16) owns keys [r * 2^64 / P, (r+1) * 2^64 / P) in its own
  * shm_tree (create it with key_lo / key_bits of that slice).  One process per
  * GPU; every rank makes the same calls in the same order (collectives).
- * A routed get: bucket by owner, pack each peer's run into a fixed-size
- * slot (1.25 n / P + 256 keys, kKeyMax padding), ncclAllToAll of the slots,
- * local shm_search_batch, results back the same way, unpack; no host wait
- * (every rank passes the same n; a run longer than its slot is reported as
- * a device error at the tree's next synchronising call).  A routed insert:
- * the same exchange with the values, then shm_insert_batch_async on the
- * owner (rank-major batch order across ranks).  Device pointers; n <=
- * the local tree's max_batch. */
+ * Every rank's tree has the same max_batch (checked at create).
+ * A routed get: each key into its owner's run of fixed-size slots
+ * (1.25 n / P + 256 keys, kKeyMax padding), ncclAllToAll of the slots and
+ * of the per-peer counts, local shm_search_batch, results back the same
+ * way, gathered to input order; no host wait before the key exchange (every
+ * rank passes the same n).  Keys past their run's slot are answered by an
+ * exact second round that end() runs after one read-back of the counts: no
+ * lookup is dropped.  A routed insert: stable bucketing, each owner's run
+ * in a slot of max_batch / P (kKeyMax padding the receiver skips), keys /
+ * values / counts exchanged, queued as one insert on the owner with no host
+ * wait (rank-major batch order across ranks); a run's tail past its slot is
+ * sent and applied by the next call on the shard (or shm_shard_synchronize)
+ * before anything else.  Device pointers; n <= the local tree's max_batch. */
 typedef struct shm_shard shm_shard;
 /* rank 0 makes the id (NCCL_UNIQUE_ID_BYTES = 128), the caller broadcasts it */
 int shm_nccl_unique_id(void *id_out, uint64_t bytes);
@@ -270,6 +299,26 @@ int shm_shard_search_begin(shm_shard *s, const uint64_t *keys, uint64_t n, void 
 int shm_shard_search_end(shm_shard *s, uint32_t ticket, uint64_t *vals_out, uint8_t *found_out);
 int shm_shard_insert(shm_shard *s, const uint64_t *keys, const uint64_t *vals, uint64_t n,
                      void *stream);
+/* Tree::range_query over the shards (src/Tree.cpp:461-540, intended
+ * semantics): scan i = [from[i], to[i]] inclusive; its pieces go only to the
+ * shards it overlaps (row p of a P x n_cap piece matrix to rank p), the
+ * owners scan them, counts come back, and ONE host read-back of the
+ * per-peer value totals sizes the value exchange.  counts_out[i], offsets_out
+ * (exclusive scan) and *total_out are always produced; values in key order
+ * across shards go to vals_out when total <= vals_cap, else SHM_ENOSPC
+ * (counts and offsets stay valid, and shm_shard_range_values copies the
+ * batch's values into a larger buffer without another exchange).  n_cap:
+ * the same on every rank, >= n, P * n_cap <= max_batch. */
+int shm_shard_range_query(shm_shard *s, const uint64_t *from, const uint64_t *to, uint64_t n,
+                          uint64_t n_cap, uint64_t *counts_out, uint64_t *offsets_out,
+                          uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_out,
+                          void *stream);
+/* the last shm_shard_range_query batch's values (its offsets_out must still
+ * be live), local only: valid until the next call on the shard */
+int shm_shard_range_values(shm_shard *s, uint64_t *vals_out, uint64_t vals_cap, void *stream);
+/* Apply what a routed insert left for the next call (its overflow tails),
+ * then shm_synchronize the local tree: the status of every routed batch. */
+int shm_shard_synchronize(shm_shard *s);
 
 /* workload generators on device (test/benchmark.cpp:43-46, zipf.h) ----------- */
 /* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */

@@ -52,6 +52,7 @@ def lib():
         L.orc_range_query_batch_mt.restype = u64
         L.orc_range_query_batch_mt.argtypes = [vp, vp, vp, u64, vp, vp, u64, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_double)]
+        L.orc_c1_build.argtypes = [vp, u64, ctypes.c_double, u64]
         L.orc_c1_bench.argtypes = [vp, ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_int,
                                    ctypes.c_double, vp]
         L.orc_root_ptr.restype = u64
@@ -190,6 +191,12 @@ class OracleTree:
             if total <= cap:
                 return counts, out[:total].copy(), secs.value
             cap = int(total)
+
+    def c1_build(self, keyspace, warm_ratio=0.8, preload=1024000):
+        """The reference benchmark's tree, one insert at a time in the
+        reference's order (orc_c1_build; ctypes releases the GIL, so this
+        can run beside other work)."""
+        lib().orc_c1_build(self.h, keyspace, warm_ratio, preload)
 
     def c1_bench(self, nthreads, keyspace, theta=0.0, seed_base=0x5EED0000, windows=5,
                  window_s=2.0):

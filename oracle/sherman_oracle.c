@@ -1239,6 +1239,19 @@ static void *c1_worker(void *a_) {
  * seed_base + thread id) and searches it; the main thread samples the
  * threads' op counters every window_s seconds (test/benchmark.cpp:302-341)
  * and writes each window's Mops/s to win_mops[0 .. windows). */
+/* The tree test/benchmark.cpp builds before its measured phase, one
+ * Tree::insert at a time as the reference does (27/27 leaf splits,
+ * Tree.cpp:914-968): node 0's preload to_key(i) -> 2i for i = 1..preload
+ * (benchmark.cpp:269-274), then the warm-up to_key(i) -> 2i for
+ * i in [1, warm_ratio * keyspace) (benchmark.cpp:114-120; the reference's
+ * threads take i % T == id concurrently: one thread here takes every i in
+ * order, the order a round-robin interleaving of those threads gives). */
+void orc_c1_build(orc_tree *t, uint64_t keyspace, double warm_ratio, uint64_t preload) {
+  for (uint64_t i = 1; i <= preload; ++i) orc_insert(t, orc_to_key(i, keyspace), i * 2);
+  const uint64_t end = (uint64_t)(warm_ratio * (double)keyspace);
+  for (uint64_t i = 1; i < end; ++i) orc_insert(t, orc_to_key(i, keyspace), i * 2);
+}
+
 void orc_c1_bench(orc_tree *t, int nthreads, uint64_t keyspace, double theta,
                   uint64_t seed_base, int windows, double window_s, double *win_mops) {
   if (nthreads < 1) nthreads = 1;

@@ -79,6 +79,7 @@ uint64_t orc_range_query_batch_mt(orc_tree *t, const uint64_t *from, const uint6
                                   uint64_t n, uint64_t *counts, uint64_t *out, uint64_t cap,
                                   int nthreads, double *secs);
 /* the reference benchmark's read phase (test/benchmark.cpp:165-188, 302-341) */
+void orc_c1_build(orc_tree *t, uint64_t keyspace, double warm_ratio, uint64_t preload);
 void orc_c1_bench(orc_tree *t, int nthreads, uint64_t keyspace, double theta,
                   uint64_t seed_base, int windows, double window_s, double *win_mops);
 void orc_apply_batch(orc_tree *t, const uint64_t *keys, const uint64_t *vals,

@@ -27,6 +27,7 @@ SHM_ENOSPC = -28
 SHM_FLAG_SORT_GETS = 0x1
 SHM_FLAG_LEAF_DIR = 0x2
 SHM_FLAG_AUTO_SORT_GETS = 0x4
+SHM_FLAG_TOP_LDS = 0x8
 
 KEY_MAX = (1 << 64) - 1
 PAGE_SIZE = 1024
@@ -77,6 +78,11 @@ class ShermanError(RuntimeError):
         super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
 
 
+class ShmIndexStats(ctypes.Structure):
+    _fields_ = [(f, u64) for f in ("gets", "start_internal", "right_moves", "page_hops",
+                                   "entry_reads", "hits")]
+
+
 class ShmProfile(ctypes.Structure):
     _fields_ = [
         ("calls", u64),
@@ -94,7 +100,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 5  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 6  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -121,6 +127,7 @@ _SIGNATURES = [
     ("shm_read_words", ctypes.c_int, [vp, vp, u64, vp, vp]),
     ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
+    ("shm_index_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmIndexStats), ctypes.c_int]),
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
     ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
@@ -134,6 +141,10 @@ _SIGNATURES = [
     ("shm_shard_search_begin", ctypes.c_int, [vp, vp, u64, vp, ctypes.POINTER(u32)]),
     ("shm_shard_search_end", ctypes.c_int, [vp, u32, vp, vp]),
     ("shm_shard_insert", ctypes.c_int, [vp, vp, vp, u64, vp]),
+    ("shm_shard_range_query", ctypes.c_int,
+     [vp, vp, vp, u64, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
+    ("shm_shard_synchronize", ctypes.c_int, [vp]),
+    ("shm_shard_range_values", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     ("shm_hash_keys", ctypes.c_int, [vp, vp, u64, u64, vp, vp]),
 ]
@@ -237,7 +248,7 @@ class Tree:
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
                  node_id=0, sort_gets="auto", num_locks=None, sort_bits=16,
-                 key_lo=0, key_bits=64, leaf_dir=True):
+                 key_lo=0, key_bits=64, leaf_dir=True, top_lds=False):
         L = lib()
         cfg = ShmConfig()
         _check(L.shm_config_init(ctypes.byref(cfg)), "config")
@@ -254,7 +265,8 @@ class Tree:
         # "auto" (order dense batches, SHM_FLAG_AUTO_SORT_GETS)
         cfg.flags = ((SHM_FLAG_SORT_GETS if sort_gets is True else 0) |
                      (SHM_FLAG_AUTO_SORT_GETS if sort_gets == "auto" else 0) |
-                     (SHM_FLAG_LEAF_DIR if leaf_dir else 0))
+                     (SHM_FLAG_LEAF_DIR if leaf_dir else 0) |
+                     (SHM_FLAG_TOP_LDS if top_lds else 0))
         h = vp()
         _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")
         self.h = h
@@ -411,8 +423,16 @@ class Tree:
         _check(lib().shm_load_image(self.h, image.ctypes.data_as(vp), image.nbytes,
                                     root_ptr), "load_image")
 
-    def profile(self, on=True):
-        _check(lib().shm_profile_enable(self.h, 1 if on else 0), "profile_enable")
+    def profile(self, on=True, index_stats=False):
+        _check(lib().shm_profile_enable(self.h, (1 if on else 0) | (2 if index_stats else 0)),
+               "profile_enable")
+
+    def index_stats(self, reset=True):
+        """The get walk's index statistics (shm_index_stats; collected while
+        profile(index_stats=True))."""
+        st = ShmIndexStats()
+        _check(lib().shm_index_stats(self.h, ctypes.byref(st), 1 if reset else 0), "index_stats")
+        return {f: getattr(st, f) for f, _ in ShmIndexStats._fields_}
 
     def profile_read(self, reset=True):
         p = ShmProfile()
@@ -469,12 +489,55 @@ def from_i64(x):
     return x & ((1 << 64) - 1)
 
 
+# library-internal test hooks (csrc/shard.cpp): an in-process group of P
+# shard handles on one GPU whose collectives are device copies
+_HOOKS = [
+    ("shm__local_group_create", ctypes.c_int, [u32, ctypes.POINTER(vp)]),
+    ("shm__local_group_destroy", ctypes.c_int, [vp]),
+    ("shm__shard_create_local", ctypes.c_int, [vp, vp, u32, ctypes.POINTER(vp)]),
+]
+
+
+def _hooks():
+    L = lib()
+    for name, res, args in _HOOKS:
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+class LocalGroup:
+    """P in-process ranks on one GPU for CShard.local (test hook): every
+    rank is driven by its own host thread, all on one shared stream."""
+
+    def __init__(self, world):
+        g = vp()
+        _check(_hooks().shm__local_group_create(world, ctypes.byref(g)), "local_group")
+        self.h, self.world = g, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            _hooks().shm__local_group_destroy(self.h)
+            self.h = None
+
+
 class CShard:
     """A range shard of a multi-GPU tree behind the C-ABI (shm_shard_*): the
-    routed get / insert (bucketing, RCCL count exchange, grouped
-    ncclSend / ncclRecv of keys and values, local batch, un-permute) runs in
-    C++ over its own RCCL communicators.  All ranks construct it together
-    (ncclCommInitRank); rank 0's unique id travels over `dist`."""
+    routed get / insert / range scan (slots, RCCL all-to-all, the overflow
+    rounds, local batch, gather) runs in C++ over its own RCCL
+    communicators.  All ranks construct it together (ncclCommInitRank); rank
+    0's unique id travels over `dist`."""
+
+    @classmethod
+    def local(cls, tree, group, rank):
+        """Rank `rank` of a LocalGroup (test hook; call from that rank's
+        thread: creation is a collective)."""
+        self = cls.__new__(cls)
+        h = vp()
+        _check(_hooks().shm__shard_create_local(tree.h, group.h, rank, ctypes.byref(h)),
+               "shard_create_local")
+        self.h, self.tree, self.world, self.rank = h, tree, group.world, rank
+        return self
 
     def __init__(self, tree, world, rank, dist, group=None):
         import torch
@@ -520,6 +583,36 @@ class CShard:
     def insert(self, keys, vals, stream=None):
         _check(lib().shm_shard_insert(self.h, _ptr(keys), _ptr(vals), keys.numel(),
                                       _stream_ptr(stream)), "shard_insert")
+
+    def range_query(self, lo, hi, n_cap=None, stream=None):
+        """Routed scans [lo_i, hi_i]: (counts, values in key order across
+        shards).  n_cap: the same on every rank, >= lo.numel() (default: the
+        tree's max_batch // P, so every rank may pass any n up to it)."""
+        import torch
+        n, dev = lo.numel(), lo.device
+        if n_cap is None:
+            n_cap = self.tree.max_batch // self.world
+        counts = torch.empty(n, dtype=torch.int64, device=dev)
+        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        cap = getattr(self, "_rq_cap", 1 << 16)
+        vals = torch.empty(cap, dtype=torch.int64, device=dev)
+        total = u64(0)
+        rc = lib().shm_shard_range_query(self.h, _ptr(lo), _ptr(hi), n, n_cap, _ptr(counts),
+                                         _ptr(offs), _ptr(vals), cap, ctypes.byref(total),
+                                         _stream_ptr(stream))
+        total = int(total.value)
+        self._rq_cap = max(cap, total + total // 4)
+        if rc == SHM_ENOSPC:
+            # the exchange completed: copy its values into a buffer that fits
+            # (local, no second collective)
+            vals = torch.empty(self._rq_cap, dtype=torch.int64, device=dev)
+            rc = lib().shm_shard_range_values(self.h, _ptr(vals), self._rq_cap,
+                                              _stream_ptr(stream))
+        _check(rc, "shard_range_query")
+        return counts, vals[:total]
+
+    def synchronize(self):
+        _check(lib().shm_shard_synchronize(self.h), "shard_synchronize")
 
 
 def header_symbols(path=HEADER_PATH):

@@ -300,8 +300,9 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 // ---- the summary walk: lane = query ------------------------------------------
 //
 // Per get, three HBM lines instead of a 1 KB page: the leaf-directory entry,
-// the leaf's summary line (layout.h: fences, a 16-bit fingerprint per slot)
-// and the entries whose fingerprint matches (false positives ~ 53 / 65535).
+// the leaf's 64 B summary line (layout.h: the highest fence, an 8-bit
+// fingerprint per slot) and the entries whose fingerprint matches (false
+// positives ~ 36 / 255 per get at C2's 36 keys per leaf).
 // A stale directory is fixed by turning right on k >= highest from the
 // summary (B-link).  Pages without a summary (internal pages: a directory
 // miss, or no directory) are walked from their own bytes, lane by lane:
@@ -310,17 +311,55 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
 // key == k, value != 0 and f == r.  Batches are serialised against inserts
 // by the call order, so a page is never torn under a get; the entry-level
 // f == r check stays.
+//
+// Without a directory the walk starts at the root, or — with the LDS
+// replica of the top of the tree (a.top_n: every page of one upper level
+// with its lowest fence, launch_top) — at the page of that level holding k,
+// found by a binary search of the block's LDS copy (the north star's "upper
+// tree levels replicated in LDS"; DESIGN §8 measures it against the
+// directory).
+
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
 
 template <int TPB>
 __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_top[];  // top_n x (8 + 4) B
   const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
-  if (i >= a.n) return;
-  const uint64_t k = a.keys[i];
+  const uint32_t tn = a.top_n;
+  uint64_t* tk = reinterpret_cast<uint64_t*>(s_top);
+  uint32_t* tpg = reinterpret_cast<uint32_t*>(s_top + 8 * (uint64_t)tn);
+  if (tn) {  // block-uniform: the replica into LDS
+    for (uint32_t j = threadIdx.x; j < tn; j += TPB) {
+      tk[j] = a.top_keys[j];
+      tpg[j] = a.top_pages[j];
+    }
+    __syncthreads();
+  }
+  const bool act = i < a.n;
+  const uint64_t k = act ? a.keys[i] : kKeyMax;
   uint64_t val = 0;
   uint32_t err = 0;
+  uint32_t c_int = 0, c_right = 0, c_hops = 0, c_ent = 0;
   if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
     uint64_t ptr = a.root;
-    if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+    if (a.dir) {
+      ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+    } else if (tn) {
+      // the last page of the level whose lowest fence is <= k (tk[0] = kKeyMin)
+      uint32_t lo = 0, hi = tn;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tk[mid] <= k)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      ptr = dir_page_ga(tpg[lo], a.node);
+    }
     int retries = 0;
     for (int hop = 0;; ++hop) {
       if (hop > kMaxRounds) {
@@ -342,12 +381,14 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
             break;
           }
           ptr = sib;
+          ++c_right;
           continue;
         }
         uint64_t cand = sl.cand;
         while (cand) {
           uint64_t ek, ev;
           uint32_t ef, er;
+          ++c_ent;
           lane_entry(page, ctz64(cand), ek, ev, ef, er);
           if (entry_hit(ek, ev, ef, er, k)) {
             val = ev;
@@ -358,6 +399,8 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
         break;
       }
       // no summary: the page's own bytes
+      if (hop == 0) c_int = 1;
+      ++c_hops;
       const u32x4* pw = reinterpret_cast<const u32x4*>(page);
       const u32x4 A = pw[0], B = pw[1], C = pw[2];
       const uint64_t leftmost = (uint64_t)((A.z >> 8) | (A.w << 24)) |
@@ -379,6 +422,7 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
       }
       if (k >= highest && sibling) {
         ptr = sibling;
+        ++c_right;
         continue;
       }
       if (k < lowest || k >= highest) {
@@ -411,7 +455,16 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
                     : ((uint64_t)pd[13 + 4 * (lo - 1)] | ((uint64_t)pd[14 + 4 * (lo - 1)] << 32));
     }
   }
+  if (a.stats) {  // wave-uniform; every lane of the wave is here
+    const uint32_t v[kIdxStats] = {wave_sum32(act && k != kKeyMax ? 1u : 0u), wave_sum32(c_int),
+                                   wave_sum32(c_right), wave_sum32(c_hops), wave_sum32(c_ent),
+                                   wave_sum32(act && val != kValueNull ? 1u : 0u)};
+    if (lane_id() == 0)
+      for (int j = 0; j < kIdxStats; ++j)
+        if (v[j]) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + j), v[j]);
+  }
   if (err) atomicOr(a.err, err);
+  if (!act) return;
   a.out_val[i] = val;
   if (a.out_found) a.out_found[i] = val != kValueNull ? 1 : 0;
 }
@@ -419,7 +472,135 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
 void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s) {
   if (n == 0) return;
   constexpr int TPB = 256;
-  hipLaunchKernelGGL(k_get_sum<TPB>, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, s, a);
+  const size_t lds = (size_t)a.top_n * 12;
+  hipLaunchKernelGGL(k_get_sum<TPB>, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds, s, a);
+}
+
+// ---- the top of the tree for the LDS replica ---------------------------------
+// One block, breadth first from the root: level by level, every page's
+// children (leftmost, then the records' pointers) and their lowest fences
+// (the parent's lowest for leftmost, the record key otherwise,
+// Tree.cpp:665-685), in key order, until the next level would not fit max_n
+// pages or the leaves are next.  scratch: 4 x max_n u64.
+__global__ __launch_bounds__(1024) void k_top(const uint8_t* arena, uint64_t arena_bytes,
+                                              uint16_t node, uint64_t root, uint32_t max_n,
+                                              uint64_t* keys, uint32_t* pages,
+                                              uint64_t* scratch, uint32_t* n_out,
+                                              uint32_t* err) {
+  __shared__ uint32_t s_n, s_ws[16], s_stop;
+  const int t = threadIdx.x;
+  uint64_t* cur_p = scratch;
+  uint64_t* cur_k = scratch + max_n;
+  uint64_t* nxt_p = scratch + 2 * (uint64_t)max_n;
+  uint64_t* nxt_k = scratch + 3 * (uint64_t)max_n;
+  if (t == 0) {
+    cur_p[0] = root;
+    cur_k[0] = kKeyMin;
+    s_n = 1;
+    s_stop = 0;
+  }
+  __syncthreads();
+  for (int level = 0; level < kMaxLevelOfTree; ++level) {
+    const uint32_t n = s_n;
+    // children per page of the current level (0: a leaf level; stop)
+    uint32_t total = 0;
+    for (uint32_t base = 0; base < n; base += 1024) {
+      const uint32_t j = base + t;
+      uint32_t c = 0;
+      if (j < n) {
+        const uint64_t p = cur_p[j];
+        if (!ptr_ok(p, node, arena_bytes)) {
+          atomicOr(err, kErrBadPtr);
+          atomicOr(&s_stop, 1u);
+        } else {
+          const uint8_t* pg = arena + ga_offset(p);
+          const uint32_t* d = reinterpret_cast<const uint32_t*>(pg);
+          const uint64_t leftmost = (uint64_t)((d[2] >> 8) | (d[3] << 24)) |
+                                    ((uint64_t)((d[3] >> 8) | (d[4] << 24)) << 32);
+          const int cnt = (int)(int16_t)(d[4] >> 16) + 1;
+          c = leftmost ? 1u + (uint32_t)(cnt < 0 ? 0 : cnt) : 0u;
+          if (!leftmost || pg[kOffLevel] <= 1) atomicOr(&s_stop, 1u);  // children are leaves
+        }
+      }
+      total += c;
+    }
+    // block total of children
+    uint32_t v = total;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    if ((t & 63) == 0) s_ws[t >> 6] = v;
+    __syncthreads();
+    uint32_t all = 0;
+    for (int w = 0; w < 16; ++w) all += s_ws[w];
+    const bool stop = s_stop != 0 || all > max_n || all == 0;
+    __syncthreads();
+    if (stop) break;
+    // children in order: one pass per 1024 pages, an exclusive scan of counts
+    uint32_t run = 0;
+    for (uint32_t base = 0; base < n; base += 1024) {
+      const uint32_t j = base + t;
+      uint32_t c = 0;
+      uint64_t leftmost = 0, lowest = 0;
+      const uint8_t* pg = nullptr;
+      if (j < n) {
+        pg = arena + ga_offset(cur_p[j]);
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(pg);
+        leftmost = (uint64_t)((d[2] >> 8) | (d[3] << 24)) |
+                   ((uint64_t)((d[3] >> 8) | (d[4] << 24)) << 32);
+        const int cnt = (int)(int16_t)(d[4] >> 16) + 1;
+        c = 1u + (uint32_t)(cnt < 0 ? 0 : cnt);
+        lowest = cur_k[j];
+      }
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if ((t & 63) >= o) incl += y;
+      }
+      if ((t & 63) == 63) s_ws[t >> 6] = incl;
+      __syncthreads();
+      uint32_t wb = 0, bt = 0;
+      for (int w = 0; w < 16; ++w) {
+        wb += w < (t >> 6) ? s_ws[w] : 0u;
+        bt += s_ws[w];
+      }
+      const uint32_t pos = run + wb + incl - c;
+      if (c) {
+        nxt_p[pos] = leftmost;
+        nxt_k[pos] = lowest;
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(pg);
+        for (uint32_t r = 0; r + 1 < c; ++r) {
+          const uint32_t w0 = (kOffRecords + kInternalEntry * r) / 4;
+          nxt_k[pos + 1 + r] = (uint64_t)d[w0] | ((uint64_t)d[w0 + 1] << 32);
+          nxt_p[pos + 1 + r] = (uint64_t)d[w0 + 2] | ((uint64_t)d[w0 + 3] << 32);
+        }
+      }
+      run += bt;
+      __syncthreads();
+    }
+    // swap
+    uint64_t* x = cur_p;
+    cur_p = nxt_p;
+    nxt_p = x;
+    x = cur_k;
+    cur_k = nxt_k;
+    nxt_k = x;
+    if (t == 0) s_n = all;
+    __syncthreads();
+  }
+  const uint32_t n = s_n;
+  for (uint32_t j = t; j < n; j += 1024) {
+    keys[j] = cur_k[j];
+    pages[j] = dir_page_index(cur_p[j]);
+  }
+  if (t == 0) *n_out = n;
+}
+
+void launch_top(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                uint32_t max_n, uint64_t* keys, uint32_t* pages, uint64_t* scratch,
+                uint32_t* n_out, uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_top, dim3(1), dim3(1024), 0, s, arena, arena_bytes, node, root, max_n,
+                     keys, pages, scratch, n_out, err);
 }
 
 // summaries of a loaded image: one wave per page

@@ -62,6 +62,8 @@ struct WaveLds {
   uint64_t a_key[kWave];
   uint64_t a_val[kWave];
   uint32_t a_ver[kWave];
+  uint64_t o_key[kWave];  // a segment's ops staged (stage_ops)
+  uint64_t o_val[kWave];
 };
 
 __device__ __forceinline__ uint32_t lock_index(uint64_t page, uint32_t n) {
@@ -265,7 +267,12 @@ __device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint3
 // The page of `level` whose fences hold k: header walk from the root with
 // page_search's sibling rule (Tree.cpp:593-663) and internal_page_search
 // (665-685), one wave.  0 on an inconsistency (error bits in *err).
-__device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err) {
+// soft: a starting point only (the caller re-checks under the page's lock):
+// a failure returns 0 without error bits
+__device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err,
+                              bool soft = false) {
+  uint32_t scratch = 0;
+  if (soft) err = &scratch;
   uint64_t ptr = a.root;
   // start at the level's page on the path of k's directory prefix (a page
   // keeps its lowest fence when it splits, so a stale hint is still a valid
@@ -293,6 +300,9 @@ __device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, ui
         *err |= kErrInconsistent;
         return 0;
       }
+      // a page rewritten by another wave of this launch: drop cached lines
+      // of it before reading again (L2 is per XCD and not coherent)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       continue;
     }
     if (hinted && (h.level != level || k < h.lowest)) {  // not this level's page any more
@@ -366,7 +376,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* red, uint32
 // generation a barrier completes is derived from the value an arrival
 // returns.  Bounded: a spin past kBarrierSpins sets the abort word, which
 // releases every other block too; returns false then.
-__device__ bool grid_sync(UpperCtl* ctl, uint32_t nb, uint32_t* flag) {
+__device__ bool grid_sync(UpperCtl* ctl, uint32_t par, uint32_t nb, uint32_t* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -374,16 +384,17 @@ __device__ bool grid_sync(UpperCtl* ctl, uint32_t nb, uint32_t* flag) {
     const uint32_t x = blockIdx.x % nx;
     const uint64_t m = nb / nx + (x < nb % nx ? 1u : 0u);  // blocks of group x
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint64_t old =
-        __hip_atomic_fetch_add(&ctl->xbar[x][0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* abort = &ctl->abort[par][0];
+    const uint64_t old = __hip_atomic_fetch_add(&ctl->xbar[par][x][0], 1ull, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t e = old / m + 1;  // the generation this barrier completes
     uint32_t ok = 1;
     auto spin_until = [&](uint64_t* w, uint64_t want) {
       for (uint32_t spin = 0;; ++spin) {
         if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return;
-        if (__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+        if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
             spin > kBarrierSpins) {
-          __hip_atomic_store(&ctl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ok = 0;
           return;
         }
@@ -393,13 +404,13 @@ __device__ bool grid_sync(UpperCtl* ctl, uint32_t nb, uint32_t* flag) {
     if (old % m == m - 1) {
       // leader: the group's releases happened before its arrivals
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      const uint64_t ot =
-          __hip_atomic_fetch_add(&ctl->top[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      spin_until(&ctl->top[0], (ot / nx + 1) * nx);
+      const uint64_t ot = __hip_atomic_fetch_add(&ctl->top[par][0], 1ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      spin_until(&ctl->top[par][0], (ot / nx + 1) * nx);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      __hip_atomic_store(&ctl->gen[x][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl->gen[par][x][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      spin_until(&ctl->gen[x][0], e);
+      spin_until(&ctl->gen[par][x][0], e);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -464,13 +475,30 @@ __device__ void find_seg(const uint32_t* np, uint32_t r0, uint32_t r1, uint32_t 
   before = run_np;
 }
 
-// wait until *cnt == want (the sibling builders of a split have read page 0)
-__device__ __forceinline__ bool fan_in(uint32_t* cnt, uint32_t want) {
+// Fan-in counters (a split's sibling builders have read its page 0): one
+// word per segment, tag << 32 | count, the tag naming the chunk and level.
+// An arrival of a new tag restarts the count, so no word is ever reset and
+// a launch that stopped early leaves nothing a later one could miscount.
+__device__ __forceinline__ void fan_arrive(uint64_t* w, uint32_t tag) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(w);
+  unsigned long long old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const unsigned long long nv = (uint32_t)(old >> 32) == tag
+                                      ? old + 1ull
+                                      : (((unsigned long long)tag << 32) | 1ull);
+    const unsigned long long prev = atomicCAS(p, old, nv);
+    if (prev == old) return;
+    old = prev;
+  }
+}
+// wait until the word reads (tag, want)
+__device__ __forceinline__ bool fan_in(uint64_t* cnt, uint32_t want, uint32_t tag) {
+  const uint64_t target = ((uint64_t)tag << 32) | want;
   uint32_t ok = 1;
   if (lane_id() == 0) {
     ok = 0;
     for (uint32_t spin = 0; spin < kFanSpins; ++spin) {
-      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) {
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target) {
         ok = 1;
         break;
       }
@@ -478,6 +506,9 @@ __device__ __forceinline__ bool fan_in(uint32_t* cnt, uint32_t want) {
     }
   }
   return rl32(ok, 0) != 0;
+}
+__device__ __forceinline__ uint32_t fan_tag(uint64_t batch, uint32_t level) {
+  return (uint32_t)(batch << 3) | level;
 }
 
 // Tree::del of one key (leaf_page_del, Tree.cpp:993-1057), one wave: walk
@@ -591,12 +622,274 @@ __device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_
 
 }  // namespace
 
+// ---- the restructured levels ----------------------------------------------------
+// The segment's ops staged in the wave's LDS (<= 64 of them): the merge and
+// the survivor test then read LDS instead of making dependent global loads.
+__device__ __forceinline__ Ops stage_ops(WaveLds& L, const Ops& o) {
+  if (o.nb > (uint32_t)kWave) return o;
+  const int lane = lane_id();
+  if ((uint32_t)lane < o.nb) {
+    L.o_key[lane] = o.key[o.st + lane];
+    L.o_val[lane] = o.val[o.st + lane];
+  }
+  wave_lds_sync();
+  return Ops{L.o_key, L.o_val, 0, o.nb};
+}
+
+// n pages past the leaf level's (device bump allocation, one atomic per
+// call; lane 0 result broadcast): the arena page of the first, or ~0 when
+// the arena cannot hold them (kErrNoMem; the pages are not used)
+__device__ __forceinline__ uint64_t alloc_pages(const UpperArgs& a, uint64_t base, uint64_t cap,
+                                                uint32_t n, uint32_t& err) {
+  uint64_t first = 0;
+  if (lane_id() == 0) {
+    first = base + atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->alloc[a.par][0]),
+                             (unsigned long long)n);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->made[a.par][0]),
+              (unsigned long long)n);
+  }
+  first = rl64(first, 0);
+  if (first + n > cap) {
+    err |= kErrNoMem;
+    return ~0ull;
+  }
+  return first;
+}
+
+// append separator (key, child) with its parent page to level `lvl`'s list
+__device__ __forceinline__ void emit_sep(const UpperArgs& a, uint32_t lvl, uint64_t key,
+                                         uint64_t child, uint64_t parent, uint32_t& err) {
+  if (lane_id() != 0) return;
+  const uint32_t j = atomicAdd(&a.ctl->lvl_sep[a.par][lvl], 1u);
+  if ((uint64_t)j >= a.sep_cap) {
+    err |= kErrPlan;
+    return;
+  }
+  a.sep_key[lvl & 1][j] = key;
+  a.sep_ptr[lvl & 1][j] = child;
+  a.ipage[lvl & 1][j] = parent;
+}
+
+// the page's lock word held exclusively (tag | 1, as the deletes take it;
+// free = any value <= the chunk's tag), released at the chunk's tag
+__device__ __forceinline__ bool lock_excl(const UpperArgs& a, uint64_t page) {
+  uint32_t got = 0;
+  if (lane_id() == 0) {
+    unsigned long long* wd =
+        reinterpret_cast<unsigned long long*>(a.locks) + lock_index(page, a.num_locks);
+    const unsigned long long mine = (unsigned long long)(a.tag | 1ull);
+    for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+      const unsigned long long cur = __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur <= (unsigned long long)a.tag && atomicCAS(wd, cur, mine) == cur) {
+        got = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  got = rl32(got, 0);
+  if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return got != 0;
+}
+__device__ __forceinline__ void unlock_excl(const UpperArgs& a, uint64_t page) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the page's stores performed
+  if (lane_id() == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(a.locks + lock_index(page, a.num_locks), a.tag, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// One internal page of `level` receives the ops o (sorted separators, their
+// children), the survivors already in L.a_*: rewritten in place when they
+// fit (T <= 60), else split into P pages, new right siblings first, page 0
+// last (Tree.cpp:699-826 for a batch of separators), new separators emitted
+// to the next level; the root splits into a fresh page X and becomes the new
+// root one level up (update_new_root, Tree.cpp:126-149).
+__device__ void apply_internal(const UpperArgs& a, WaveLds& L, const Hdr& h, int na, const Ops& o,
+                               uint64_t page, uint32_t level, uint64_t base, uint64_t cap,
+                               uint32_t& err) {
+  const uint32_t T2 = (uint32_t)na + o.nb;
+  const uint32_t P = T2 <= (uint32_t)(kInternalCardinality - 1)
+                         ? 1u
+                         : (T2 + 1 + kInternalSplitFill) / (kInternalSplitFill + 1);
+  if (P == 1) {
+    (void)build_internal_page(a, L, h, na, o, SplitPage{0, 1, T2, 0, page}, level);
+    return;
+  }
+  const bool grow = page == a.root;
+  const uint64_t first = alloc_pages(a, base, cap, P - 1 + (grow ? 1u : 0u), err);
+  if (first == ~0ull) return;  // no room: the page stays as it was (reported)
+  for (uint32_t p = 1; p < P; ++p) {
+    const SplitPage sp{(int)p, (int)P, T2, first, new_ga(a.node, first, (int)p)};
+    const uint64_t low = build_internal_page(a, L, h, na, o, sp, level);
+    const uint64_t par = grow ? a.root : parent_of(a, low, level + 1, &err);
+    emit_sep(a, level + 1, low, sp.dest, par, err);
+  }
+  const uint64_t dest0 = grow ? ga_make(a.node, (first + P - 1) * kPageSize) : page;
+  (void)build_internal_page(a, L, h, na, o, SplitPage{0, (int)P, T2, first, dest0}, level);
+  if (grow) {
+    write_new_root(a, L, dest0, level + 1, h.fver);
+    if (lane_id() == 0) atomicMax(&a.ctl->root_new[a.par][0], level + 1);
+  }
+}
+
+// Level >= 2: a run of separators (sorted keys [hs, he) of the block's LDS
+// list, one parent hint) applied under the parent's exclusive word, as
+// internal_page_store does (Tree.cpp:699-826: lock, read, turn right past
+// the highest fence, insert, split at 61) for a batch.  Separators of one
+// parent may sit in several blocks' lists: their runs serialise on the
+// word.  The ops below the page's highest fence go in; the rest move right
+// (B-link); a page no longer at `level` (the root grew, or a page another
+// wave has just created is not visible yet) is found again from the root.
+__device__ void apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
+                          const uint64_t* ptrs, uint32_t hs, uint32_t he, uint64_t page,
+                          uint32_t level, uint64_t base, uint64_t cap, uint32_t& err) {
+  for (int hop = 0; hs < he; ++hop) {
+    if (hop >= kMaxRounds) {
+      err |= kErrRounds;
+      return;
+    }
+    if (!ptr_ok(page, a.node, a.arena_bytes)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      page = parent_of(a, keys[hs], level, &err, true);
+      continue;
+    }
+    if (!lock_excl(a, page)) {
+      err |= kErrLock;
+      return;
+    }
+    const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+    const Hdr h = parse_hdr(w);
+    const uint64_t k0 = keys[hs];
+    if (h.leftmost == 0 || h.level != level || h.fver != h.rver_internal || k0 < h.lowest) {
+      unlock_excl(a, page);
+      page = parent_of(a, k0, level, &err, true);
+      continue;
+    }
+    // ops of this page: keys below its highest fence (all if it is the last)
+    uint32_t m = he;
+    if (h.sibling != 0) {
+      for (uint32_t c = hs; c < he; c += kWave) {
+        const uint32_t j = c + (uint32_t)lane_id();
+        const uint64_t mk = ballot(j < he && keys[j] >= h.highest);
+        if (mk) {
+          m = c + (uint32_t)ctz64(mk);
+          break;
+        }
+      }
+    }
+    if (m > hs) {
+      const Ops o{keys, ptrs, hs, m - hs};
+      const int na = internal_survivors(L, w, h.last_index + 1, o);
+      apply_internal(a, L, h, na, o, page, level, base, cap, err);
+    }
+    unlock_excl(a, page);
+    hs = m;
+    page = h.sibling;  // Tree.cpp:737-743
+  }
+}
+
+// The block's share of level `level`'s separators (emitted unordered by
+// the level below), sorted by key in LDS, cut into runs of one parent hint,
+// one wave per run.  Shares of ceil(n / nb) (at most kLvlSort a round):
+// the few separators of C5's upper levels spread over as many blocks.
+constexpr uint32_t kLvlSort = 1024;
+struct LvlLds {
+  uint64_t key[kLvlSort];
+  uint64_t ptr[kLvlSort];
+  uint64_t hint[kLvlSort];
+  uint32_t head[kLvlSort];
+};
+__device__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t* red,
+                            uint32_t n, uint32_t level, uint64_t base, uint64_t cap,
+                            uint32_t& err) {
+  const int t = threadIdx.x, wv = t >> 6;
+  const uint32_t b = blockIdx.x, nb = gridDim.x;
+  const uint32_t share = (n + nb - 1) / nb;
+  const uint32_t per = share < kLvlSort ? share : kLvlSort;
+  const uint64_t* gk = a.sep_key[level & 1];
+  const uint64_t* gp = a.sep_ptr[level & 1];
+  const uint64_t* gh = a.ipage[level & 1];
+  for (uint32_t c0 = b * per; c0 < n; c0 += nb * per) {
+    const uint32_t cnt = n - c0 < per ? n - c0 : per;
+    uint32_t m2 = 1;
+    while (m2 < cnt) m2 <<= 1;
+    for (uint32_t j = t; j < m2; j += kUpT) {
+      const bool v = j < cnt;
+      S.key[j] = v ? gk[c0 + j] : kKeyMax;
+      S.ptr[j] = v ? gp[c0 + j] : 0;
+      S.hint[j] = v ? gh[c0 + j] : 0;
+    }
+    __syncthreads();
+    // bitonic sort by key (keys of one level are distinct)
+    for (uint32_t k = 2; k <= m2; k <<= 1)
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        for (uint32_t i = t; i < m2; i += kUpT) {
+          const uint32_t l = i ^ jj;
+          if (l > i) {
+            const bool up = (i & k) == 0;
+            const uint64_t x = S.key[i], y = S.key[l];
+            if ((x > y) == up) {
+              S.key[i] = y;
+              S.key[l] = x;
+              const uint64_t p = S.ptr[i], q = S.hint[i];
+              S.ptr[i] = S.ptr[l];
+              S.hint[i] = S.hint[l];
+              S.ptr[l] = p;
+              S.hint[l] = q;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    // runs of one parent hint
+    uint32_t nh = 0;
+    for (uint32_t base_i = 0; base_i < cnt; base_i += kUpT) {
+      const uint32_t i = base_i + t;
+      const bool hd = i < cnt && (i == 0 || S.hint[i] != S.hint[i - 1]);
+      uint32_t th;
+      const uint32_t x = block_scan(hd ? 1u : 0u, red, &th);
+      if (hd) S.head[nh + x] = i;
+      nh += th;
+      __syncthreads();
+    }
+    for (uint32_t hx = wv; hx < nh; hx += kUpWaves) {
+      const uint32_t hs = S.head[hx];
+      const uint32_t he = hx + 1 < nh ? S.head[hx + 1] : cnt;
+      apply_run(a, L, S.key, S.ptr, hs, he, S.hint[hs], level, base, cap, err);
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
+// k_upper: one persistent launch per insert chunk, one 512-thread block per
+// CU (all resident: grid barriers).
+//   prologue  per-range prefix sums of the upsert kernel's new-page counts
+//   leaf      splits into <= kSmallSplit pages: one wave builds all of a
+//             split's pages, siblings first and page 0 last (it holds the old
+//             page's survivors, so no fan-in); larger splits: their sibling
+//             pages spread over every wave of the grid, page 0 after the
+//             fan-in of its builders.  Each new leaf's separator goes to
+//             position (its global new-page index): key order.
+//   --- grid barrier ---
+//   level 1   runs of separators with one parent, one wave per run: the
+//             parent's epoch lock word, its survivors and the run merged,
+//             rewritten in place or split (pages by an atomic bump past the
+//             leaf level's), new separators to level 2's list
+//   --- grid barrier ---
+//   level >=2 each block's share of the separators (emitted unordered),
+//             sorted in LDS, runs of one parent under its exclusive word
+//   (--- grid barrier --- after every level: the next level's count)
+//   deletes   Tree::del of the chunk's deletes (after every split)
+//   block 0   the superblock and its host mirror
 __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   __shared__ __attribute__((aligned(16))) WaveLds s_l[kUpWaves];
   __shared__ uint32_t s_red[kUpWaves];
   __shared__ uint32_t s_flag;
   __shared__ uint32_t s_list[kUpT];  // segment heads of one separator chunk
+  __shared__ __attribute__((aligned(16))) LvlLds s_lvl;  // levels >= 2: the block's share
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t b = blockIdx.x, nb = gridDim.x;
   const uint64_t W = (uint64_t)nb * kUpWaves;
@@ -613,30 +906,42 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   };
   stamp();
   Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
-  uint64_t cursor = sb->next_page;
-  const uint64_t cursor0 = cursor;
+  const uint64_t cursor0 = sb->next_page;
   uint32_t root_level = (uint32_t)sb->root_level;
   const uint64_t cap = sb->capacity_pages;
-  uint64_t made = 0;  // pages created by splits
   uint32_t err = 0;
   const uint32_t ns = *a.ns_dev;
   const uint32_t par = a.par;
-  // the other parity's range sums and split counts start the next batch at 0
+  // the other parity's counters and barrier words start the next chunk at 0
   for (uint64_t j = tid; j < (uint64_t)kMaxUpper; j += T) {
     ctl->leaf_np[par ^ 1][j] = 0;
     ctl->leaf_ns[par ^ 1][j] = 0;
+    ctl->leaf_nb[par ^ 1][j] = 0;
+  }
+  for (uint64_t j = tid; j < 8 * 16; j += T) {
+    (&ctl->xbar[par ^ 1][0][0])[j] = 0;
+    (&ctl->gen[par ^ 1][0][0])[j] = 0;
+  }
+  if (tid < 16) {
+    ctl->top[par ^ 1][tid] = 0;
+    ctl->lvl_sep[par ^ 1][tid] = 0;
+  }
+  if (tid == 0) {
+    ctl->abort[par ^ 1][0] = 0;
+    ctl->alloc[par ^ 1][0] = 0;
+    ctl->made[par ^ 1][0] = 0;
+    ctl->root_new[par ^ 1][0] = 0;
   }
   // leaf level: the upsert kernel left per-range new-page / split counts
   const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
   const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
-  // per-range prefixes of new pages and splits (every block alike): a wave
-  // finds its task's block range by them and its segment by a scan of that
-  // range's seg_np, so no block waits for another's list
+  const uint32_t v_nb = (uint32_t)t < nb ? ctl->leaf_nb[par][t] : 0u;
   __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
-  uint32_t total, nsplit;
+  uint32_t total, nsplit, nbig;
   {
     const uint32_t xnp = block_scan(v_np, s_red, &total);
     const uint32_t xns = block_scan(v_ns, s_red, &nsplit);
+    nbig = block_sum(v_nb, s_red);
     if ((uint32_t)t < nb) {
       s_pnp[t] = xnp;
       s_pns[t] = xns;
@@ -648,22 +953,20 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     __syncthreads();
   }
   bool ok = true;
-  uint32_t nsep = 0;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
-  const bool fits = cursor + total + (grow0 ? 1u : 0u) <= cap;
+  const bool fits = cursor0 + total + (grow0 ? 1u : 0u) <= cap;
+  // pages past the leaf level's: the internal levels' bump allocator
+  const uint64_t base = cursor0 + total + (grow0 ? 1u : 0u);
   if (total && !fits) {
     // arena exhausted: the flagged segments stay unapplied (reported)
     err |= kErrNoMem;
   } else if (total) {
-    // ---- P3: every wave of the grid takes new right siblings, then pages 0,
-    // from the whole split list: the splits of a block range vary (a few
-    // per block on average, several times that on some), and the slowest
-    // block held every other at the next barrier (block-local P3: 13 us of
-    // work, 19 us of barrier wait per C5 chunk, phase clock)
     stamp();
-    const uint64_t first = cursor;  // arena page of global new page 0
-    const uint64_t xroot = cursor + total;  // the root's left half (grow0)
-    for (uint32_t gp = (uint32_t)wid; ok && gp < total; gp += (uint32_t)W) {
+    const uint64_t first = cursor0;          // arena page of global new page 0
+    const uint64_t xroot = cursor0 + total;  // the root's left half (grow0)
+    const uint32_t ftag = fan_tag(a.batch, 0);
+    // (a) sibling pages of the large splits, over every wave (none in C5)
+    for (uint32_t gp = (uint32_t)wid; nbig && gp < total; gp += (uint32_t)W) {
       const uint32_t r = last_le(s_pnp, nb, gp);
       uint32_t r0, r1, g, before;
       block_range(ns, r, nb, r0, r1);
@@ -672,28 +975,32 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         err |= kErrPlan;
         continue;
       }
+      if (a.seg_P[g] <= kSmallSplit) continue;  // built whole by (b)
       const uint32_t pb = s_pnp[r] + before;
       const int p = (int)(gp - pb) + 1;
-      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
+      const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
       const Hdr h = parse_hdr(w);
       stage_page(L.page, w);
       wave_lds_sync();
+      const Ops o = stage_ops(L, o0);
       const int na = leaf_survivors(L, o);
       // the old page 0 has been read: its rewrite may go ahead
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) atomicAdd(a.leaf_rd + g, 1u);
+      if (lane == 0) fan_arrive(a.leaf_rd + g, ftag);
       const SplitPage sp{p, (int)a.seg_P[g], a.seg_T[g], first + pb,
                          new_ga(a.node, first + pb, p)};
       const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
       const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
       if (lane == 0) {
-        a.sep_key[0][gp] = low;
-        a.sep_ptr[0][gp] = sp.dest;
-        a.ipage[0][gp] = par_pg;
+        a.sep_key[1][gp] = low;
+        a.sep_ptr[1][gp] = sp.dest;
+        a.ipage[1][gp] = par_pg;
       }
     }
-    for (uint32_t k = (uint32_t)wid; ok && k < nsplit; k += (uint32_t)W) {
+    // (b) every split: a small one whole (siblings, then page 0), a large
+    // one's page 0 once its sibling builders have read the old page
+    for (uint32_t k = (uint32_t)wid; k < nsplit; k += (uint32_t)W) {
       const uint32_t r = last_le(s_pns, nb, k);
       uint32_t r0, r1, g, before;
       block_range(ns, r, nb, r0, r1);
@@ -705,45 +1012,50 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       const uint32_t pb = s_pnp[r] + before;
       const int P = (int)a.seg_P[g];
       const uint64_t page = a.seg_page[g];
-      if (!fan_in(a.leaf_rd + g, (uint32_t)(P - 1))) err |= kErrLock;
-      const Ops o{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
+      const bool small = (uint32_t)P <= kSmallSplit;
+      if (!small && !fan_in(a.leaf_rd + g, (uint32_t)(P - 1), ftag)) err |= kErrLock;
+      const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(page));
       const Hdr h = parse_hdr(w);
       if (h.fver != a.seg_ver[g] || h.fver != h.rver_leaf) err |= kErrPlan;
       stage_page(L.page, w);
       wave_lds_sync();
+      const Ops o = stage_ops(L, o0);
       const int na = leaf_survivors(L, o);
+      if (small) {
+        for (int p = 1; p < P; ++p) {
+          const SplitPage sp{p, P, a.seg_T[g], first + pb, new_ga(a.node, first + pb, p)};
+          const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
+          const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
+          if (lane == 0) {
+            const uint32_t gp = pb + (uint32_t)(p - 1);
+            a.sep_key[1][gp] = low;
+            a.sep_ptr[1][gp] = sp.dest;
+            a.ipage[1][gp] = par_pg;
+          }
+        }
+      }
       const uint64_t dest = grow0 ? ga_make(a.node, xroot * kPageSize) : page;
-      const SplitPage sp{0, P, a.seg_T[g], first + pb, dest};
-      (void)build_leaf_page(a, L, h, na, o, sp);
+      (void)build_leaf_page(a, L, h, na, o, SplitPage{0, P, a.seg_T[g], first + pb, dest});
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
-      if (lane == 0) a.leaf_rd[g] = 0;  // for the next batch
     }
-    cursor += total + (grow0 ? 1u : 0u);
     if (grow0) root_level = 1;
-    made += total;
-    nsep = total;
     stamp();
-    // the next level reads every block's separators
-    ok = ok && grid_sync(ctl, nb, &s_flag);
+    if (a.force_abort && b == 0 && t == 0)  // diagnostics: this launch stops here
+      __hip_atomic_store(&ctl->abort[par][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // level 1 reads every block's separators
+    ok = grid_sync(ctl, par, nb, &s_flag);
     stamp();
   }
 
-  // ---- internal levels ------------------------------------------------------
-  for (uint32_t level = 1; ok && nsep > 0; ++level) {
-    if (level > (uint32_t)kMaxLevelOfTree) {
-      err |= kErrRounds;
-      break;
-    }
-    const int cur = (int)((level - 1) & 1), nxt = cur ^ 1;
-    const uint64_t* skey = a.sep_key[cur];
-    const uint64_t* sptr = a.sep_ptr[cur];
-    const uint64_t* spg = a.ipage[cur];
-    const bool grow = level == root_level;
-    // ---- I1: segment heads of my separator range; plan each under its lock --
+  // ---- level 1: runs of separators with one parent -----------------------------
+  if (ok && total && fits) {
+    const uint64_t* skey = a.sep_key[1];
+    const uint64_t* sptr = a.sep_ptr[1];
+    const uint64_t* spg = a.ipage[1];
+    const uint32_t nsep = total;
     uint32_t r0, r1;
     block_range(nsep, b, nb, r0, r1);
-    uint32_t my_heads = 0, my_np = 0;
     for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
       const uint32_t i = c0 + (uint32_t)t;
       const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
@@ -755,174 +1067,77 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       for (uint32_t hx = (uint32_t)wv; hx < th; hx += kUpWaves) {
         const uint32_t hi = s_list[hx];
         const uint64_t page = spg[hi];
-        // segment end: first index past hi whose page differs
+        // the run's end: first index past hi whose page differs
         uint32_t e = hi + 1;
         for (;;) {
           const uint32_t j = e + (uint32_t)lane;
-          const bool diff = j >= nsep || spg[j] != page;
-          const uint64_t m = ballot(diff);
+          const uint64_t m = ballot(j >= nsep || spg[j] != page);
           if (m) {
             e += (uint32_t)ctz64(m);
             break;
           }
           e += kWave;
         }
-        const Ops o{skey, sptr, hi, e - hi};
-        uint32_t lk = 0, T2 = 0, P = 1, ver = ~0u;
         if (!ptr_ok(page, a.node, a.arena_bytes)) {
           err |= kErrBadPtr;
-        } else {
-          // the parent's word, held until the chunk retires (epoch tags)
-          if (lane == 0) lk = take_word(a.locks, a.num_locks, page, a.tag) ? 1u : 0u;
-          lk = rl32(lk, 0);
-          if (!lk) err |= kErrLock;
-          const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-          const Hdr h = parse_hdr(w);
-          const IntRec r = internal_record(w);
-          const int cnt = h.last_index + 1;
-          const bool hit = lane >= 3 && lane - 3 < cnt && op_contains(o, r.key);
-          const uint32_t M = (uint32_t)popc64(ballot(hit));
-          T2 = (uint32_t)cnt + (e - hi) - M;
-          P = T2 <= (uint32_t)(kInternalCardinality - 1)
-                  ? 1u
-                  : (T2 + 1 + kInternalSplitFill) / (kInternalSplitFill + 1);
-          ver = h.fver;
-          if (h.fver != h.rver_internal || h.leftmost == 0 || h.level != level) {
-            err |= kErrInconsistent;
-            P = 1;
-            T2 = 0;  // left untouched (see I3)
-          }
-          if (!lk) {
-            P = 1;
-            T2 = 0;
-          }
+          continue;
         }
-        if (lane == 0) {
-          a.h_end[hi] = e;
-          a.h_T[hi] = T2;
-          a.h_P[hi] = P;
-          a.h_ver[hi] = ver;
-          a.h_lk[hi] = lk;
+        // the parent's word, held until the chunk retires (epoch tags)
+        uint32_t lk = 0;
+        if (lane == 0) lk = take_word(a.locks, a.num_locks, page, a.tag) ? 1u : 0u;
+        if (!rl32(lk, 0)) {
+          err |= kErrLock;
+          continue;
         }
-        my_np += P - 1;  // wave-uniform
-      }
-      my_heads += th;
-      __syncthreads();
-    }
-    {
-      const uint32_t bn = block_sum(lane == 0 ? my_np : 0u, s_red);
-      if (t == 0) {
-        ctl->int_heads[b] = my_heads;
-        ctl->int_np[b] = bn;
-      }
-    }
-    stamp();
-    ok = grid_sync(ctl, nb, &s_flag);
-    stamp();
-    if (!ok) break;
-    // ---- I2: this block's dense segment list and new-page bases, at global
-    // positions (every block has the per-range counts now) -------------------
-    const uint32_t vh = (uint32_t)t < nb ? ctl->int_heads[t] : 0u;
-    const uint32_t vp = (uint32_t)t < nb ? ctl->int_np[t] : 0u;
-    const uint32_t tot = block_sum(vp, s_red);
-    const uint32_t h0 = block_sum((uint32_t)t < b ? vh : 0u, s_red);
-    const uint32_t p0 = block_sum((uint32_t)t < b ? vp : 0u, s_red);
-    if (cursor + tot + (grow ? 1u : 0u) > cap) {
-      // arena exhausted (every block sees the same totals): this level stays
-      // unapplied; B-link keeps every key reachable through the siblings
-      err |= kErrNoMem;
-      break;
-    }
-    uint32_t run_h = h0, run_p = p0;
-    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
-      const uint32_t i = c0 + (uint32_t)t;
-      const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
-      const uint32_t np = head ? a.h_P[i] - 1 : 0u;
-      uint32_t th, tp;
-      const uint32_t xh = block_scan(head ? 1u : 0u, s_red, &th);
-      const uint32_t xp = block_scan(np, s_red, &tp);
-      if (head) {
-        a.d_head[run_h + xh] = i;
-        a.d_base[run_h + xh] = run_p + xp;
-      }
-      run_h += th;
-      run_p += tp;
-    }
-    __syncthreads();  // the block's list is complete (workgroup scope)
-    stamp();
-    // ---- I3: this block's new pages, then page 0 of each of its segments ----
-    const uint64_t first = cursor;
-    const uint64_t xroot = cursor + tot;
-    for (uint32_t gp = p0 + (uint32_t)wv; gp < run_p; gp += kUpWaves) {
-      const uint32_t s = h0 + last_le(a.d_base + h0, run_h - h0, gp);
-      const uint32_t hi = a.d_head[s];
-      const uint32_t pb = a.d_base[s];
-      const int p = (int)(gp - pb) + 1;
-      const Ops o{skey, sptr, hi, a.h_end[hi] - hi};
-      const u32x4 w = load_page_slice(a.arena, ga_offset(spg[hi]));
-      const Hdr h = parse_hdr(w);
-      const int na = internal_survivors(L, w, h.last_index + 1, o);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) atomicAdd(a.int_rd + s, 1u);
-      const SplitPage sp{p, (int)a.h_P[hi], a.h_T[hi], first + pb, new_ga(a.node, first + pb, p)};
-      const uint64_t low = build_internal_page(a, L, h, na, o, sp, level);
-      const uint64_t par_pg = grow ? a.root : parent_of(a, low, level + 1, &err);
-      if (lane == 0) {
-        a.sep_key[nxt][gp] = low;
-        a.sep_ptr[nxt][gp] = sp.dest;
-        a.ipage[nxt][gp] = par_pg;
-      }
-    }
-    for (uint32_t s = h0 + (uint32_t)wv; s < run_h; s += kUpWaves) {
-      const uint32_t hi = a.d_head[s];
-      const uint64_t page = spg[hi];
-      const int P = (int)a.h_P[hi];
-      const uint32_t T2 = a.h_T[hi];
-      if (P > 1 && !fan_in(a.int_rd + s, (uint32_t)(P - 1))) err |= kErrLock;
-      if (T2 > 0) {  // 0: inconsistent or not locked, left untouched
-        const Ops o{skey, sptr, hi, a.h_end[hi] - hi};
         const u32x4 w = load_page_slice(a.arena, ga_offset(page));
         const Hdr h = parse_hdr(w);
-        if (h.fver != a.h_ver[hi] || h.fver != h.rver_internal) {
-          err |= kErrPlan;
-        } else {
-          const int na = internal_survivors(L, w, h.last_index + 1, o);
-          const bool rootsplit = grow && P > 1;
-          const uint64_t dest = rootsplit ? ga_make(a.node, xroot * kPageSize) : page;
-          const SplitPage sp{0, P, T2, first + a.d_base[s], dest};
-          (void)build_internal_page(a, L, h, na, o, sp, level);
-          if (rootsplit) write_new_root(a, L, dest, level + 1, h.fver);
+        if (h.fver != h.rver_internal || h.leftmost == 0 || h.level != 1) {
+          err |= kErrInconsistent;  // left untouched
+          continue;
         }
+        const Ops o = stage_ops(L, Ops{skey, sptr, hi, e - hi});
+        const int na = internal_survivors(L, w, h.last_index + 1, o);
+        apply_internal(a, L, h, na, o, page, 1, base, cap, err);
       }
-      if (lane == 0) a.int_rd[s] = 0;
+      __syncthreads();
     }
-    const bool grew = grow && tot > 0;
-    cursor += tot + (grew ? 1u : 0u);
-    if (grew) root_level = level + 1;
-    made += tot;
-    nsep = tot;
     stamp();
-    if (tot) {  // the next level reads every block's separators
-      ok = grid_sync(ctl, nb, &s_flag);
+    ok = grid_sync(ctl, par, nb, &s_flag);
+    stamp();
+    // ---- levels >= 2: the block's share, sorted, runs under exclusive words --
+    for (uint32_t level = 2; ok; ++level) {
+      const uint32_t n = __hip_atomic_load(&ctl->lvl_sep[par][level], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (n == 0) break;
+      if (level > (uint32_t)kMaxLevelOfTree) {
+        err |= kErrRounds;
+        break;
+      }
+      upper_level(a, L, s_lvl, s_red, n < a.sep_cap ? n : (uint32_t)a.sep_cap, level, base, cap,
+                  err);
+      stamp();
+      ok = grid_sync(ctl, par, nb, &s_flag);
       stamp();
     }
   }
   if (!ok) err |= kErrRounds;
   // the chunk's deletes, after every split (Tree::del, Tree.cpp:542-591):
-  // the keys are located afresh, so pages that moved right are followed.
-  // The last level skipped its barrier; a delete's walk must not meet a page
-  // another block is still rewriting, so wait for every block first.
+  // the keys are located afresh, so pages that moved right are followed; the
+  // last level ended with a grid barrier, so no page is still being written
   const uint64_t n_del = *a.n_del;
-  if (ok && n_del > 0 && total > 0) {
-    stamp();
-    ok = grid_sync(ctl, nb, &s_flag);
-    if (!ok) err |= kErrRounds;
-  }
   for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
   stamp();
   if (b == 0 && t == 0) {
-    // superblock (device-authoritative) and its host mirror
+    // superblock (device-authoritative) and its host mirror; with splits
+    // every block has passed the last barrier, so the counters are final
+    const uint64_t extra = total && fits ? ctl->alloc[par][0] : 0ull;
+    uint64_t cursor = total && fits ? base + extra : cursor0;
+    if (cursor > cap) cursor = cap;  // failed allocations used no page
+    const uint32_t rn = ctl->root_new[par][0];
+    if (grow0 && total && fits) root_level = 1;
+    if (rn > root_level) root_level = rn;
+    const uint64_t made = total && fits ? (uint64_t)total + ctl->made[par][0] : 0ull;
     sb->next_page = cursor;
     sb->root_level = root_level;
     sb->splits += made;
@@ -961,6 +1176,12 @@ uint32_t upper_blocks() {
     return (uint32_t)(n < kMaxUpper ? n : kMaxUpper);
   }();
   return nb;
+}
+
+bool upper_resident() {
+  int nb = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_upper, kUpT, 0) == hipSuccess &&
+         nb >= 1;
 }
 
 void launch_upper(const UpperArgs& a, hipStream_t s) {

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
                                                    uint32_t* __restrict__ gcount,
                                                    uint32_t* err, uint32_t* gate, uint32_t tag,
                                                    KeyRange kr, uint32_t* __restrict__ M,
-                                                   uint32_t* __restrict__ S) {
+                                                   uint32_t* __restrict__ S, int skip_pad) {
   // LDS hash table of the tile's distinct keys: slot -> (key, 1 + last index)
   constexpr int kSlots = 2 * kIsortTile;
   constexpr int PER = kIsortTile / kIT;
@@ -112,7 +112,9 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
     if (i >= n) continue;
     const uint64_t k = keys[i];
     if (k == kKeyMax) {
-      bad = true;  // kKeyMax cannot be stored (root highest is exclusive, Tree.h:150)
+      // kKeyMax cannot be stored (root highest is exclusive, Tree.h:150);
+      // a routed insert's slot padding (skip_pad) is no op at all
+      if (!skip_pad) bad = true;
       continue;
     }
     uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 50) & (kSlots - 1);
@@ -575,12 +577,13 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
                        uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
-                       hipStream_t s) {
+                       int skip_pad, hipStream_t s) {
   if (!n) return;
   const uint64_t tiles = (n + kIsortTile - 1) / kIsortTile;
   if (tiles > (uint64_t)kMaxTiles) M = S = nullptr;  // the coarse pass counts for itself
   hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)tiles), dim3(kIT), 0, s, keys, n, keys_out,
-                     idx_out, gcount, err, gate, tag, KeyRange{key_lo, key_bits}, M, S);
+                     idx_out, gcount, err, gate, tag, KeyRange{key_lo, key_bits}, M, S,
+                     skip_pad);
 }
 
 void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, uint64_t key_lo,

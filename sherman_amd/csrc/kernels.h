@@ -55,7 +55,33 @@ struct WalkArgs {
   uint64_t* locks;
   uint32_t num_locks;
   uint64_t lock_tag;
+  // GET (k_get_sum), nullable: the top of the tree replicated in LDS (the
+  // fences and page indices of every page of one upper level, launch_top):
+  // with no directory, each lane starts at the level page holding its key
+  const uint64_t* top_keys;
+  const uint32_t* top_pages;
+  uint32_t top_n;
+  // GET (k_get_sum), nullable: index statistics (kIdxStats words, added per
+  // wave): see IdxStat
+  uint64_t* stats;
 };
+// k_get_sum's index statistics (shm_index_stats)
+enum IdxStat {
+  kIdxGets = 0,        // queries walked
+  kIdxStartInternal,   // start page without a leaf summary (directory miss / descent)
+  kIdxRightMoves,      // B-link right turns
+  kIdxPageHops,        // pages walked from their own bytes (internal or unsummarised)
+  kIdxEntryReads,      // leaf entries read (fingerprint matches)
+  kIdxHits,            // queries found
+  kIdxStats
+};
+// top-of-tree table for the LDS replica: every page of the deepest level
+// whose page count fits max_n, in key order: keys[i] = its lowest fence,
+// pages[i] = its page index; *n_out = the count, *level_out its level
+void launch_top(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                uint32_t max_n, uint64_t* keys, uint32_t* pages, uint64_t* scratch,
+                uint32_t* n_out, uint32_t* err, hipStream_t s);
+constexpr uint32_t kTopMax = 4096;  // 48 KB of LDS per block
 
 // batched get walk with grouped page resolution (get.hip)
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
@@ -82,19 +108,32 @@ constexpr int kMaxUpper = 512;
 struct UpperCtl {
   // XCD-hierarchical grid barrier (insert.hip grid_sync), each word on a
   // 128 B line of its own: arrivals per XCD group, the XCD leaders' count,
-  // and the generation each leader publishes to its group (all monotonic)
-  uint64_t xbar[8][16];
-  uint64_t top[16];
-  uint64_t gen[8][16];
-  uint32_t abort;   // a barrier timed out: every block leaves (sticky)
+  // the generation each leader publishes to its group (monotonic within a
+  // launch) and the abort word (a barrier timed out: every block leaves).
+  // Double buffered by chunk parity: a launch uses set par and zeroes set
+  // par ^ 1 for the next one, so every launch starts from clean words even
+  // after one that aborted.
+  uint64_t xbar[2][8][16];
+  uint64_t top[2][16];
+  uint64_t gen[2][8][16];
+  uint32_t abort[2][32];
   uint32_t gate;    // tag of the last chunk rejected by its ordering (kKeyMax)
   // leaf split counts of the upsert kernel per k_upper block range, double
   // buffered by chunk parity (k_upper zeroes the other parity)
   uint32_t leaf_np[2][kMaxUpper];  // new pages
   uint32_t leaf_ns[2][kMaxUpper];  // split segments
-  uint32_t int_heads[kMaxUpper];   // internal level: segments per block range
-  uint32_t int_np[kMaxUpper];      // internal level: new pages per block range
+  uint32_t leaf_nb[2][kMaxUpper];  // new pages of splits into more than kSmallSplit pages
+  // internal levels (k_upper): pages allocated past the leaf level's, pages
+  // made, the root's level after growth, separators emitted for each level
+  // (all per parity, zeroed by the previous launch)
+  uint64_t alloc[2][16];
+  uint64_t made[2][16];
+  uint32_t root_new[2][32];
+  uint32_t lvl_sep[2][16];
 };
+// a leaf split into at most this many pages is built by one wave (pages
+// 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
+constexpr uint32_t kSmallSplit = 4;
 
 // in-place leaf upserts (upsert.hip)
 struct SegArgs {
@@ -158,8 +197,10 @@ struct UpperArgs {
   const uint32_t* seg_np;
   const uint32_t* seg_ver;
   const uint32_t* ns_dev;
-  uint32_t* leaf_rd;         // per segment: sibling builders that read page 0 (zero between chunks)
+  uint64_t* leaf_rd;         // per segment: sibling builders that read page 0 (tag << 32 | count)
   // internal levels: separators (key, child) and their target page, ping-pong
+  // by level parity (level 1: [1], level 2: [0], ...), sep_cap each
+  uint64_t sep_cap;
   uint64_t* sep_key[2];
   uint64_t* sep_ptr[2];
   uint64_t* ipage[2];
@@ -172,7 +213,7 @@ struct UpperArgs {
   // dense segment list of a level
   uint32_t* d_head;
   uint32_t* d_base;
-  uint32_t* int_rd;          // zero between chunks
+  uint64_t* int_rd;          // as leaf_rd, per internal segment (tag: chunk and level)
   uint64_t* pub;             // mapped host mirror {batch, next_page, root_level, splits} (nullable)
   // the chunk's deletes (Tree::del), applied after the splits
   const uint64_t* dk;
@@ -187,11 +228,16 @@ struct UpperArgs {
   // nullable: block 0 records the wall clock (100 MHz) at each phase end,
   // stamps[0] = count (tools/upper_stamps.py)
   uint64_t* stamps;
+  // diagnostics (shm__upper_force_abort): block 0 raises the abort word
+  // before the first grid barrier of this launch
+  uint32_t force_abort;
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins
 constexpr int kStampWords = kUpperStamps + 8 * 256;
 uint32_t upper_blocks();
+// k_upper's blocks (one per CU, 512 threads) fit the device at all
+bool upper_resident();
 void launch_upper(const UpperArgs& a, hipStream_t s);
 
 void launch_empty_leaf(uint8_t* arena, uint64_t page_off, uint8_t* sum, hipStream_t s);
@@ -225,7 +271,8 @@ void launch_partition_coarse(const uint64_t* keys, uint64_t n, const uint32_t* g
 // insert ordering (isort.hip).  Step 1: every 2048-op tile reduced to its
 // last writer per key (LDS hash table, atomic max of the op index); a kKeyMax
 // key rejects the chunk: gate = tag (k_bin_unique then emits nothing) and the
-// sticky error word gets kErrKeyMax.
+// sticky error word gets kErrKeyMax; with skip_pad, kKeyMax keys are slot
+// padding of a routed insert (shard.cpp) and are skipped instead.
 constexpr int kIsortTile = 2048;
 constexpr uint32_t kErrKeyMax = 1u << 31;
 // For batches of <= kMaxTiles tiles it also writes the coarse pass's tile
@@ -233,7 +280,7 @@ constexpr uint32_t kErrKeyMax = 1u << 31;
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
                        uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
-                       hipStream_t s);
+                       int skip_pad, hipStream_t s);
 // steps 3-4: per-bin last-writer dedup + sort (bins of <= 6144 ops in LDS,
 // larger ones by an LSD radix sort through global scratch kscr / iscr, n
 // words each), then uk / uv / dk at the bins' prefixes and (upserts, deletes)
@@ -286,14 +333,40 @@ void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64
 void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
                       uint64_t* out, uint8_t* found, hipStream_t s);
 // fixed-capacity get exchange (shard.cpp): keys straight into P runs of cap
-// slots (kKeyMax padding; spos[i] = input i's slot, ~0 and kErrOverflow in
-// *err when its run is full; cursor = P words of scratch), and the results
-// gathered back to input order
+// slots (kKeyMax padding; spos[i] = input i's slot, ~0 when its run is full;
+// cursor = P + 1 words: per-peer routed counts, then the overflow count).
+// An overflowed key goes to ovk / ovi (its input position) for the second
+// round; with ovk == nullptr it finds nothing and kErrOverflow goes to *err.
+// The results are gathered back to input order.
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
-                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint32_t* err,
-                        hipStream_t s);
+                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
+                        uint32_t* ovi, uint32_t* err, hipStream_t s);
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
                          uint8_t* found, hipStream_t s);
+// out[ovi[perm[j]]] = in[j], found likewise (the overflow round's results)
+void launch_route_ov_scatter(const uint64_t* in, const uint32_t* perm, const uint32_t* ovi,
+                             uint64_t m, uint64_t* out, uint8_t* found, hipStream_t s);
+// routed insert: the bucketed runs (cnt[p] keys of peer p, in order) packed
+// into P slot runs of cap (kKeyMax / 0 padding)
+void launch_route_pack(const uint64_t* kb, const uint64_t* vb, const uint64_t* cnt, uint32_t P,
+                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s);
+// routed range scans: shard p owns [b[p], b[p + 1]) (P <= 16; b[P] unused)
+struct ShardBounds {
+  uint64_t b[17];
+};
+// the P x cap piece matrix of n scans (empty pieces: lo = 1 > hi = 0)
+void launch_range_pieces(const uint64_t* from, const uint64_t* to, uint64_t n, uint64_t cap,
+                         uint32_t P, const ShardBounds& bnd, uint64_t* plo, uint64_t* phi,
+                         hipStream_t s);
+// rw[r] = sum of row r of rc, rw[P + p] = sum of row p of bc (P x cap
+// matrices); counts[j] = sum over p of bc[p][j], j < n
+void launch_range_sums(const uint64_t* rc, const uint64_t* bc, uint64_t n, uint64_t cap,
+                       uint32_t P, uint64_t* rw, uint64_t* counts, hipStream_t s);
+// scan j's pieces' values (bv at bsc[p][j], bc[p][j] of them) to
+// vals[offsets[j] ...] in shard order, bounded by vals_cap
+void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_t* bsc,
+                           uint64_t n, uint64_t cap, uint32_t P, const uint64_t* offsets,
+                           uint64_t* vals, uint64_t vals_cap, hipStream_t s);
 
 // ---- batched range scans (range.hip) -------------------------------------------
 struct RangeArgs {
@@ -330,7 +403,7 @@ void launch_range(const RangeArgs& a, hipStream_t s);
 void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 
 // ---- host read-backs (range.hip) ------------------------------------------------
-// dst[i] = src[i] for i < nw (<= 64, dst in mapped host memory), then a
+// dst[i] = src[i] for i < nw (<= 256, dst in mapped host memory), then a
 // system-scope release store of seq to *flag
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
                      uint32_t seq, hipStream_t s);

@@ -298,8 +298,8 @@ void launch_range(const RangeArgs& a, hipStream_t s) {
 // publishes the sequence number the host spins on
 __global__ void k_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
                            uint32_t seq) {
+  for (uint32_t l = threadIdx.x; l < nw; l += blockDim.x) dst[l] = src[l];
   const uint32_t l = threadIdx.x;
-  if (l < nw) dst[l] = src[l];
   __threadfence_system();
   __syncthreads();
   if (l == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

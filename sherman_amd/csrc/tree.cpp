@@ -87,11 +87,13 @@ struct shm_tree {
   uint32_t* pnew = nullptr;
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
-  uint32_t* leaf_rd = nullptr;
+  uint64_t* leaf_rd = nullptr;
+  bool force_abort = false;  // shm__upper_force_abort: the next chunk's k_upper stops
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   uint64_t* ipage[2] = {nullptr, nullptr};
   uint32_t *h_end = nullptr, *h_T = nullptr, *h_P = nullptr, *h_ver = nullptr, *h_lk = nullptr;
-  uint32_t *d_head = nullptr, *d_base = nullptr, *int_rd = nullptr;
+  uint32_t *d_head = nullptr, *d_base = nullptr;
+  uint64_t* int_rd = nullptr;
   uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
   uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
@@ -106,6 +108,17 @@ struct shm_tree {
   uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
   uint64_t dir_np = 0;
   bool dir_valid = false;
+  // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
+  // directory; launch_top), rebuilt with the same staleness rule
+  uint64_t* top_keys = nullptr;
+  uint32_t* top_pages = nullptr;
+  uint64_t* top_scratch = nullptr;
+  uint32_t top_n = 0;
+  uint64_t top_np = 0;
+  bool top_valid = false;
+  // index statistics of the get walk (shm_index_stats), when prof_stats
+  uint64_t* idx_stats = nullptr;
+  bool prof_stats = false;
   std::mutex mu;
   // profiling (shm_profile_*)
   bool prof_on = false;
@@ -262,6 +275,9 @@ dev::WalkArgs walk_args(shm_tree* t) {
 }
 
 bool use_leaf_dir(const shm_tree* t) { return (t->cfg.flags & SHM_FLAG_LEAF_DIR) != 0; }
+bool use_top(const shm_tree* t) {
+  return !use_leaf_dir(t) && (t->cfg.flags & SHM_FLAG_TOP_LDS) != 0;
+}
 
 // the superblock mirror k_upper publishes into h_pin (kPubWord): {chunk tag,
 // next_page, root_level, splits}; exact once the device is idle
@@ -308,6 +324,29 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
                        s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
+  return SHM_OK;
+}
+
+int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes);
+
+// the LDS replica's table (rebuilt like the directory, once the tree grew
+// by 1/32); one read-back of its size per rebuild
+int refresh_top(shm_tree* t, hipStream_t s) {
+  if (!use_top(t) || (t->top_valid && t->next_page <= t->top_np + t->top_np / 32)) return SHM_OK;
+  if (!t->top_keys) {
+    if (dalloc(&t->top_keys, dev::kTopMax) || dalloc(&t->top_pages, dev::kTopMax) ||
+        dalloc(&t->top_scratch, 4ull * dev::kTopMax))
+      return SHM_ENOMEM;
+  }
+  dev::launch_top(t->arena, t->arena_bytes, t->cfg.node_id, t->root, dev::kTopMax, t->top_keys,
+                  t->top_pages, t->top_scratch, reinterpret_cast<uint32_t*>(t->d_counts + 14),
+                  t->d_err, s);
+  HIP_OK(hipGetLastError());
+  const int rc = readback(t, s, t->d_counts + 14, sizeof(uint32_t));
+  if (rc) return rc;
+  t->top_n = (uint32_t)t->h_pin[0];
+  t->top_np = t->next_page;
+  t->top_valid = t->top_n > 0;
   return SHM_OK;
 }
 
@@ -472,9 +511,10 @@ int drain_profile(shm_tree* t) {
 //      chunk's deletes, superblock.
 // step 1: it reads only the batch and writes the insert workspace
 int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
-                 uint64_t n, uint32_t tag) {
+                 uint64_t n, uint32_t tag, bool skip_pad) {
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
-                         t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S, s);
+                         t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S,
+                         skip_pad ? 1 : 0, s);
   dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
                                t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
   dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
@@ -564,6 +604,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.seg_ver = t->seg_ver;
   u.ns_dev = d_ns;
   u.leaf_rd = t->leaf_rd;
+  u.sep_cap = t->sep_cap;
   for (int i = 0; i < 2; ++i) {
     u.sep_key[i] = t->sep_key[i];
     u.sep_ptr[i] = t->sep_ptr[i];
@@ -583,6 +624,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
+  u.force_abort = t->force_abort ? 1u : 0u;
+  t->force_abort = false;
   dev::launch_upper(u, s);
   DBG(s, "upper");
   HIP_OK(hipGetLastError());
@@ -595,14 +638,14 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
 }
 
 int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
-                 uint64_t n) {
+                 uint64_t n, bool skip_pad = false) {
   const uint32_t tag = ++t->chunks;
   shm_tree::ProfRec pr{};
   if (t->prof_on) {
     const int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
     if (rc) return rc;
   }
-  if (const int rc = insert_order(t, s, keys, vals, n, tag)) return rc;
+  if (const int rc = insert_order(t, s, keys, vals, n, tag, skip_pad)) return rc;
   // leaves of the upserts
   if (use_leaf_dir(t)) {
     const int rc = refresh_dir(t, s);
@@ -611,9 +654,13 @@ int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   return insert_apply(t, s, n, tag, pr);
 }
 
-// every chunk of one insert call, in order
+// every chunk of one insert call, in order.  A chunk holding kKeyMax is
+// rejected whole on the device (SHM_EINVAL at the next synchronising call);
+// the call's other chunks, before and after it, are applied (the host does
+// not wait between chunks).  skip_pad: kKeyMax keys are a routed insert's
+// slot padding and are skipped (shm__insert_batch_padded).
 int insert_all(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t n, void* stream,
-               bool sync) {
+               bool sync, bool skip_pad = false) {
   if (!t || (n && (!keys || !vals))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(stream);
@@ -623,7 +670,7 @@ int insert_all(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t
   int rc = SHM_OK;
   for (uint64_t off = 0; off < n && rc == SHM_OK; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
-    rc = insert_chunk(t, s, keys + off, vals + off, m);
+    rc = insert_chunk(t, s, keys + off, vals + off, m, skip_pad);
   }
   if (rc == SHM_OK) {
     t->batches += 1;
@@ -648,6 +695,7 @@ void free_all(shm_tree* t) {
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
   F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->dir); F(t->dir_hint); F(t->gcount); F(t->bins);
+  F(t->top_keys); F(t->top_pages); F(t->top_scratch); F(t->idx_stats);
   for (auto& r : t->prof_pending)
     for (hipEvent_t e : r.e)
       if (e) t->event_pool.push_back(e);
@@ -860,7 +908,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   // arena < 4 TB: the leaf directory holds 32-bit page indices
   if (cfg->arena_bytes < 4 * kPageSize || cfg->arena_bytes > (1ull << 42) ||
       cfg->max_batch == 0 ||
-      cfg->max_batch > (1ull << 31) || cfg->num_locks == 0 ||
+      cfg->max_batch >= (1ull << 24) || cfg->num_locks == 0 ||
       (cfg->sort_bits != 0 && cfg->sort_bits != kDefaultSortBits) || cfg->key_bits > 64)
     return SHM_EINVAL;
   shm_tree* t = new shm_tree();
@@ -874,6 +922,11 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
     return rc;
   };
   if (hipSetDevice(cfg->device) != hipSuccess) return fail(SHM_EIO);
+  // k_upper's grid barriers need one resident 512-thread block per CU
+  if (!dev::upper_resident()) {
+    fprintf(stderr, "sherman_amd: k_upper blocks do not fit a CU\n");
+    return fail(SHM_EIO);
+  }
   if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(SHM_EIO);
   t->cap_pages = cfg->arena_bytes / kPageSize;
@@ -955,8 +1008,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->bsum64, 0, sizeof(uint64_t) * (dev::seg_tiles(n) + 1), s) ||
       hipMemsetAsync(t->ctl, 0, sizeof(dev::UpperCtl), s) ||
       hipMemsetAsync(t->bins, 0, sizeof(uint32_t) * 4 * dev::kCoarse, s) ||
-      hipMemsetAsync(t->leaf_rd, 0, sizeof(uint32_t) * segcap, s) ||
-      hipMemsetAsync(t->int_rd, 0, sizeof(uint32_t) * t->sep_cap, s) ||
+      hipMemsetAsync(t->leaf_rd, 0, sizeof(uint64_t) * segcap, s) ||
+      hipMemsetAsync(t->int_rd, 0, sizeof(uint64_t) * t->sep_cap, s) ||
       hipMemsetAsync(t->part_S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->gws[1].S, 0, sizeof(uint32_t) * dev::kPartGroupWords, s) ||
       hipMemsetAsync(t->arena, 0, kPageSize, s) ||
@@ -1003,6 +1056,10 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
     if (dir_stale(t)) ord.make_exclusive();  // the rebuild rewrites what searches read
     const int rc = ord.rc ? ord.rc : refresh_dir(t, s);
     if (rc) return rc;
+  } else if (use_top(t)) {
+    if (!(t->top_valid && t->next_page <= t->top_np + t->top_np / 32)) ord.make_exclusive();
+    const int rc = ord.rc ? ord.rc : refresh_top(t, s);
+    if (rc) return rc;
   }
   return search_impl(t, s, ord, keys, n, vals_out, found_out);
 }
@@ -1023,6 +1080,12 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
     set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
+    if (use_top(t) && t->top_valid) {
+      a.top_keys = t->top_keys;
+      a.top_pages = t->top_pages;
+      a.top_n = t->top_n;
+    }
+    a.stats = t->prof_stats ? t->idx_stats : nullptr;
     bool gathered = false;
     shm_tree::ProfRec pr{};
     if (t->prof_on) {
@@ -1239,10 +1302,47 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   return range_launch(t, s, a);
 }
 
+// Library-internal, not part of include/sherman_amd.h (shard.cpp): a routed
+// insert's received slots, kKeyMax padding skipped, queued as
+// shm_insert_batch_async (n <= max_batch: one chunk)
+int shm__insert_batch_padded(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t n,
+                             void* stream) {
+  if (t && n > t->nmax) return SHM_E2BIG;
+  return insert_all(t, keys, vals, n, stream, false, true);
+}
+
+// Library-internal (shard.cpp): exclusive scan of n <= max_batch u64 words
+// on `stream`; tot_dev (device, 2 words) = {total, the tree's error word}
+int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tot_dev,
+                  void* stream) {
+  if (!t || !tot_dev || (n && (!in || !out))) return SHM_EINVAL;
+  if (n > t->nmax) return SHM_E2BIG;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(stream);
+  if (n == 0) {
+    HIP_OK(hipMemsetAsync(tot_dev, 0, 2 * sizeof(uint64_t), s));
+    return SHM_OK;
+  }
+  dev::launch_scan_u64_total(in, out, n, t->bsum64, scan_tag(t, s), t->d_err, tot_dev, t->d_err,
+                             s);
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
 // Library-internal, not part of include/sherman_amd.h: the tree's sticky
 // device error word (shard.cpp's kernels report into it, so the next
 // synchronising call on the tree returns their errors)
 uint32_t* shm__error_word(shm_tree* t) { return t ? t->d_err : nullptr; }
+
+// Diagnostics, not part of include/sherman_amd.h: the next insert chunk's
+// k_upper raises its abort word before its first grid barrier (the test of a
+// barrier timeout: the chunk reports SHM_EIO, later chunks run normally)
+int shm__upper_force_abort(shm_tree* t) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  t->force_abort = true;
+  return SHM_OK;
+}
 
 // Diagnostics, not part of include/sherman_amd.h: enable = 1 turns k_upper's
 // phase clock on, 0 off; out (nullable, kUpperStamps words) receives the last
@@ -1288,7 +1388,7 @@ int shm_stats(shm_tree* t, shm_stats_t* o) {
 
 int shm_read_words(shm_tree* t, const void* src, uint64_t bytes, void* host_out,
                    void* stream) {
-  if (!t || !src || !host_out || bytes == 0 || bytes > 256 || (bytes & 3)) return SHM_EINVAL;
+  if (!t || !src || !host_out || bytes == 0 || bytes > 1024 || (bytes & 3)) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   const int rc = readback(t, pick(stream), src, bytes);
   if (rc) return rc;
@@ -1338,6 +1438,7 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;
   t->dir_valid = false;  // contents changed: rebuild the leaf directory
+  t->top_valid = false;
   Order ord(t, t->stream, true);
   return write_superblock(t, t->stream);
 }
@@ -1362,7 +1463,31 @@ int shm_check(shm_tree* t, uint64_t* n_leaves, uint64_t* n_internal,
 int shm_profile_enable(shm_tree* t, int on) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
-  t->prof_on = on != 0;
+  t->prof_on = (on & 1) != 0;
+  const bool st = (on & 2) != 0;
+  if (st && !t->idx_stats) {
+    if (dalloc(&t->idx_stats, dev::kIdxStats)) return SHM_ENOMEM;
+    HIP_OK(hipMemset(t->idx_stats, 0, sizeof(uint64_t) * dev::kIdxStats));
+  }
+  t->prof_stats = st;
+  return SHM_OK;
+}
+
+int shm_index_stats(shm_tree* t, shm_index_stats_t* out, int reset) {
+  if (!t || !out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  memset(out, 0, sizeof(*out));
+  if (!t->idx_stats) return SHM_OK;
+  HIP_OK(hipDeviceSynchronize());
+  uint64_t v[dev::kIdxStats];
+  HIP_OK(hipMemcpy(v, t->idx_stats, sizeof(v), hipMemcpyDeviceToHost));
+  out->gets = v[dev::kIdxGets];
+  out->start_internal = v[dev::kIdxStartInternal];
+  out->right_moves = v[dev::kIdxRightMoves];
+  out->page_hops = v[dev::kIdxPageHops];
+  out->entry_reads = v[dev::kIdxEntryReads];
+  out->hits = v[dev::kIdxHits];
+  if (reset) HIP_OK(hipMemset(t->idx_stats, 0, sizeof(v)));
   return SHM_OK;
 }
 

@@ -211,6 +211,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
       const uint32_t r = (uint32_t)((gq * a.up_nb) / num_seg);
       atomicAdd(&a.ctl->leaf_np[a.par][r], P - 1);
       atomicAdd(&a.ctl->leaf_ns[a.par][r], 1u);
+      if (P > kSmallSplit) atomicAdd(&a.ctl->leaf_nb[a.par][r], P - 1);
     }
   }
   return err;

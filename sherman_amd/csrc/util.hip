@@ -410,14 +410,16 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
 // Peer p's keys go to slot run [p * cap, (p + 1) * cap) of the send buffer,
 // the rest of the run kKeyMax (a get of kKeyMax finds nothing).  A key's
 // place in its run comes from a per-peer cursor (one atomic per peer present
-// in a wave), so no bucketing pass, scan or pack is needed; the order inside
+// in a block), so no bucketing pass, scan or pack is needed; the order inside
 // a run does not matter, since spos[i] records where input i went and the
-// results are gathered back from the same places.
+// results are gathered back from the same places.  cursor[p] ends as the
+// number of keys routed to peer p (a run's overflow included), cursor[P] as
+// the number of overflowed keys.
 __global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t n, uint32_t* cursor,
                                                    uint32_t P) {
   const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (i == 0)
-    for (uint32_t p = 0; p < P; ++p) cursor[p] = 0;
+    for (uint32_t p = 0; p <= P; ++p) cursor[p] = 0;
   if (2 * i + 1 < n) {
     *reinterpret_cast<u32x4*>(out + 2 * i) = u32x4{~0u, ~0u, ~0u, ~0u};
   } else if (2 * i < n) {
@@ -428,7 +430,11 @@ __global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t n, ui
 // A block places 4096 keys (16 per thread): per round and wave, ranks among
 // the lanes of one owner by ballots (as k_route_scatter); per owner, ONE
 // global cursor claim for the whole block (a cursor word claimed per wave
-// serialises ~16 K atomics on one address per batch: 270 us at world 1)
+// serialises ~16 K atomics on one address per batch: 270 us at world 1).
+// A key past its run's capacity goes to the overflow list (ovk[j] = key,
+// ovi[j] = its input position; one claim per wave and round) and the
+// shard's second round returns its value (shard.cpp); without an overflow
+// list (ovk == nullptr) it finds nothing and kErrOverflow is reported.
 constexpr int kSlotPer = 16;
 constexpr int kSlotTile = kT * kSlotPer;
 
@@ -436,7 +442,8 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
                                                     uint32_t P, uint64_t cap,
                                                     uint32_t* __restrict__ cursor,
                                                     uint64_t* __restrict__ out,
-                                                    uint32_t* __restrict__ spos, uint32_t* err) {
+                                                    uint32_t* __restrict__ spos, uint64_t* ovk,
+                                                    uint32_t* ovi, uint32_t* err) {
   constexpr int kW = kT / kWave;
   __shared__ uint32_t wc[kSlotPer][kW][kRouteMaxShards];
   const int t = threadIdx.x, w = t >> 6, lane = lane_id();
@@ -478,34 +485,48 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
   bool over = false;
 #pragma unroll
   for (int r = 0; r < kSlotPer; ++r) {
-    if (own[r] == ~0u) continue;
     const uint64_t i = base + (uint64_t)r * kT + t;
-    const uint32_t pos = wc[r][w][own[r]] + rank[r];
-    if (pos < cap) {
-      const uint64_t x = (uint64_t)own[r] * cap + pos;
-      out[x] = kk[r];
-      spos[i] = (uint32_t)x;
-    } else {  // this peer's run is full: reported, the key finds nothing
-      spos[i] = ~0u;
-      over = true;
+    bool ov = false;
+    if (own[r] != ~0u) {
+      const uint32_t pos = wc[r][w][own[r]] + rank[r];
+      if (pos < cap) {
+        const uint64_t x = (uint64_t)own[r] * cap + pos;
+        out[x] = kk[r];
+        spos[i] = (uint32_t)x;
+      } else {  // this peer's run is full
+        spos[i] = ~0u;
+        ov = true;
+      }
     }
+    const uint64_t om = ballot(ov);  // wave-uniform
+    if (om && ovk) {
+      uint32_t ob = 0;
+      if (lane == 0) ob = atomicAdd(cursor + P, (uint32_t)popc64(om));
+      ob = rl32(ob, 0);
+      if (ov) {
+        const uint32_t j = ob + (uint32_t)popc64(om & lanemask_lt());
+        ovk[j] = kk[r];
+        ovi[j] = (uint32_t)i;
+      }
+    }
+    over |= ov;
   }
-  if (over) atomicOr(err, kErrOverflow);
+  if (over && !ovk) atomicOr(err, kErrOverflow);
 }
 
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
-                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint32_t* err,
-                        hipStream_t s) {
+                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
+                        uint32_t* ovi, uint32_t* err, hipStream_t s) {
   const uint64_t slots = (uint64_t)P * cap;
   hipLaunchKernelGGL(k_route_fill, grid1((slots + 1) / 2 + 1), dim3(kT), 0, s, out, slots, cursor,
                      P);
   if (n)
     hipLaunchKernelGGL(k_route_slots, grid1(n, kSlotTile), dim3(kT), 0, s, keys, n, P, cap, cursor,
-                       out, spos, err);
+                       out, spos, ovk, ovi, err);
 }
 
-// out[i] = in[spos[i]] (0 for a key cut by a full run), found[i] = out[i] != 0
-// (Tree.cpp:445-448)
+// out[i] = in[spos[i]] (0 for a key cut by a full run: the overflow round
+// fills it afterwards), found[i] = out[i] != 0 (Tree.cpp:445-448)
 __global__ void k_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n,
                                uint64_t* out, uint8_t* found) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -518,6 +539,139 @@ __global__ void k_route_gather(const uint64_t* in, const uint32_t* spos, uint64_
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
                          uint8_t* found, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_route_gather, grid1(n), dim3(kT), 0, s, in, spos, n, out, found);
+}
+
+// the overflow round's results: out[ovi[perm[j]]] = in[j] (perm: the
+// overflow list's bucketing permutation), found likewise
+__global__ void k_route_ov_scatter(const uint64_t* in, const uint32_t* perm, const uint32_t* ovi,
+                                   uint64_t m, uint64_t* out, uint8_t* found) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t i = ovi[perm[j]];
+  const uint64_t v = in[j];
+  out[i] = v;
+  if (found) found[i] = v != kValueNull ? 1 : 0;
+}
+void launch_route_ov_scatter(const uint64_t* in, const uint32_t* perm, const uint32_t* ovi,
+                             uint64_t m, uint64_t* out, uint8_t* found, hipStream_t s) {
+  if (m)
+    hipLaunchKernelGGL(k_route_ov_scatter, grid1(m), dim3(kT), 0, s, in, perm, ovi, m, out, found);
+}
+
+// Routed insert: the stably bucketed keys (and values) of peer p, run
+// [sum(cnt[< p]), + cnt[p]), packed into slot run [p * cap, (p + 1) * cap):
+// the first min(cnt[p], cap) in bucket (= input) order, the rest kKeyMax
+// padding (the receiver's insert skips it).  The overflow (cnt[p] > cap)
+// stays in kb / vb for the shard's second round.
+__global__ __launch_bounds__(kT) void k_route_pack(const uint64_t* kb, const uint64_t* vb,
+                                                   const uint64_t* cnt, uint32_t P, uint64_t cap,
+                                                   uint64_t* pk, uint64_t* pv) {
+  const uint64_t x = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (x >= (uint64_t)P * cap) return;
+  const uint32_t p = (uint32_t)(x / cap);
+  const uint64_t j = x - (uint64_t)p * cap;
+  uint64_t off = 0;
+  for (uint32_t q = 0; q < p; ++q) off += cnt[q];
+  const bool real = j < cnt[p];
+  pk[x] = real ? kb[off + j] : kKeyMax;
+  pv[x] = real ? vb[off + j] : kValueNull;
+}
+void launch_route_pack(const uint64_t* kb, const uint64_t* vb, const uint64_t* cnt, uint32_t P,
+                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s) {
+  const uint64_t slots = (uint64_t)P * cap;
+  if (slots) hipLaunchKernelGGL(k_route_pack, grid1(slots), dim3(kT), 0, s, kb, vb, cnt, P, cap, pk, pv);
+}
+
+// ---- routed range scans (shard.cpp shm_shard_range_query) -------------------
+// Piece (p, j) of the P x cap piece matrix = scan j's overlap with shard p,
+// [max(from, lo_p), min(to, hi_p)], or empty (1, 0) where it misses the shard
+// (or j >= n); row p goes to rank p.  bnd: shard p owns [bnd[p], bnd[p + 1]),
+// bnd[P] = 0 standing for 2^64.
+__global__ __launch_bounds__(kT) void k_range_pieces(const uint64_t* from, const uint64_t* to,
+                                                     uint64_t n, uint64_t cap, uint32_t P,
+                                                     ShardBounds bnd, uint64_t* plo,
+                                                     uint64_t* phi) {
+  const uint64_t x = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (x >= (uint64_t)P * cap) return;
+  const uint32_t p = (uint32_t)(x / cap);
+  const uint64_t j = x - (uint64_t)p * cap;
+  uint64_t lo = 1, hi = 0;
+  if (j < n) {
+    const uint64_t f = from[j], t = to[j];
+    const uint64_t slo = bnd.b[p];
+    const uint64_t shi = p + 1 < P ? bnd.b[p + 1] - 1 : kKeyMax;  // inclusive top
+    if (f <= t && f <= shi && t >= slo) {
+      lo = f > slo ? f : slo;
+      hi = t < shi ? t : shi;
+    }
+  }
+  plo[x] = lo;
+  phi[x] = hi;
+}
+void launch_range_pieces(const uint64_t* from, const uint64_t* to, uint64_t n, uint64_t cap,
+                         uint32_t P, const ShardBounds& bnd, uint64_t* plo, uint64_t* phi,
+                         hipStream_t s) {
+  const uint64_t m = (uint64_t)P * cap;
+  if (m) hipLaunchKernelGGL(k_range_pieces, grid1(m), dim3(kT), 0, s, from, to, n, cap, P, bnd, plo, phi);
+}
+
+// Sums after the counts came back: blocks [0, P) sum row r of rc (the values
+// this rank, as scanner, sends rank r) into rw[r]; blocks [P, 2P) row p of
+// bc (the values it receives from shard p) into rw[P + p]; the rest give
+// counts[j] = sum over p of bc[p][j] for j < n (scan j's total).
+__global__ __launch_bounds__(kT) void k_range_sums(const uint64_t* rc, const uint64_t* bc,
+                                                   uint64_t n, uint64_t cap, uint32_t P,
+                                                   uint64_t* rw, uint64_t* counts) {
+  const uint32_t b = blockIdx.x;
+  if (b < 2 * P) {
+    const uint64_t* row = (b < P ? rc : bc) + (uint64_t)(b % P) * cap;
+    uint64_t v = 0;
+    for (uint64_t j = threadIdx.x; j < cap; j += kT) v += row[j];
+    uint64_t tot;
+    (void)block_scan<uint64_t>(v, &tot);
+    if (threadIdx.x == 0) rw[b] = tot;
+    return;
+  }
+  const uint64_t j = (uint64_t)(b - 2 * P) * kT + threadIdx.x;
+  if (j >= n) return;
+  uint64_t c = 0;
+  for (uint32_t p = 0; p < P; ++p) c += bc[(uint64_t)p * cap + j];
+  counts[j] = c;
+}
+void launch_range_sums(const uint64_t* rc, const uint64_t* bc, uint64_t n, uint64_t cap,
+                       uint32_t P, uint64_t* rw, uint64_t* counts, hipStream_t s) {
+  const uint32_t blocks = 2 * P + (uint32_t)((n + kT - 1) / kT);
+  hipLaunchKernelGGL(k_range_sums, dim3(blocks), dim3(kT), 0, s, rc, bc, n, cap, P, rw, counts);
+}
+
+// Scan j's values, in shard order (= key order across shards): piece (p, j)
+// holds bc[p][j] values at bv[bsc[p][j]] (bsc: exclusive scan of bc in
+// row-major order, the layout of the received value runs); they go to
+// vals[offsets[j] + sum of its earlier pieces], values past vals_cap dropped.
+// One wave per scan.
+__global__ __launch_bounds__(kT) void k_range_assemble(const uint64_t* bv, const uint64_t* bc,
+                                                       const uint64_t* bsc, uint64_t n,
+                                                       uint64_t cap, uint32_t P,
+                                                       const uint64_t* offsets, uint64_t* vals,
+                                                       uint64_t vals_cap) {
+  const uint64_t j = ((uint64_t)blockIdx.x * kT + threadIdx.x) / kWave;
+  if (j >= n) return;
+  const int lane = lane_id();
+  uint64_t dst = offsets[j];
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t c = bc[(uint64_t)p * cap + j];
+    const uint64_t src = bsc[(uint64_t)p * cap + j];
+    for (uint64_t k = (uint64_t)lane; k < c; k += kWave)
+      if (dst + k < vals_cap) vals[dst + k] = bv[src + k];
+    dst += c;
+  }
+}
+void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_t* bsc,
+                           uint64_t n, uint64_t cap, uint32_t P, const uint64_t* offsets,
+                           uint64_t* vals, uint64_t vals_cap, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_range_assemble, grid1(n * kWave), dim3(kT), 0, s, bv, bc, bsc, n, cap, P,
+                       offsets, vals, vals_cap);
 }
 
 }  // namespace dev

@@ -27,11 +27,10 @@ the GPU box, gloo in the CPU tests):
 object with the same five methods works (the multi-rank CPU tests plug in an
 oracle-backed shard to check the exchange logic itself).
 
-With `cshard` (a sherman_amd.CShard) the get and insert routes run in C++
-behind the C-ABI (include/sherman_amd.h shm_shard_*, csrc/shard.cpp) over
-their own RCCL communicators, and this class only forwards to them; the
-Python exchange below remains the logic the CPU tests check and the range
-route.
+With `cshard` (a sherman_amd.CShard) the get, insert and range routes run in
+C++ behind the C-ABI (include/sherman_amd.h shm_shard_*, csrc/shard.cpp)
+over their own RCCL communicators, and this class only forwards to them; the
+Python exchange below remains the logic the gloo tests check.
 """
 import torch
 
@@ -164,6 +163,14 @@ class ShardRouter:
         # written by the same un-permute pass
         self.local.route_unpermute(back, perm, vals_out, found=found_out)
 
+    def synchronize(self):
+        """Status of every routed batch (the C shard first applies what its
+        last insert left for the next call)."""
+        if self.cshard is not None:
+            self.cshard.synchronize()
+        else:
+            self.local.synchronize()
+
     def insert(self, keys, vals):
         """Batched insert (value 0 deletes) of this rank's (key, value) pairs."""
         if self.cshard is not None:
@@ -182,17 +189,20 @@ class ShardRouter:
         # status surfaces at the shard's next synchronising call)
         getattr(self.local, "insert_batch_async", self.local.insert_batch)(rk, rv)
 
-    def range_query(self, lo, hi):
+    def range_query(self, lo, hi, n_cap=None):
         """Batched range scans [lo_i, hi_i] (inclusive, u64 held as int64).
         Returns (counts[n] int64, values): scan i's values are
         values[sum(counts[:i]) : sum(counts[:i+1])], in key order across shards
-        (leaf order, then slot order, inside a shard).
+        (leaf order, then slot order, inside a shard).  n_cap (C shard only):
+        the same on every rank, >= n (shm_shard_range_query).
 
         Every scan is cut into P pieces, piece s = its overlap with shard s
         (empty, lo > hi, where it misses the shard), and row s of the P x n
         piece matrix goes to rank s: no bucketing and no key-count exchange.
         Host synchronisations: the ranks' scan counts (the receive splits) and
         the ranks' value totals (the value splits), each one read-back."""
+        if self.cshard is not None:
+            return self.cshard.range_query(lo, hi, n_cap)
         n, dev, P = lo.numel(), lo.device, self.world
         bnd = shard_bounds(P, dev)
         first = bnd[:P]

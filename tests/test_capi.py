@@ -47,7 +47,7 @@ def test_config_layout_and_defaults():
     assert cfg.key_lo == 0 and cfg.key_bits == 64
     assert cfg.flags == shm.SHM_FLAG_LEAF_DIR | shm.SHM_FLAG_AUTO_SORT_GETS
     assert cfg.max_batch == 1 << 20 and cfg.num_locks == 16384  # kNumOfLock (Common.h:87-93)
-    assert shm.lib().shm_abi_version() == 5
+    assert shm.lib().shm_abi_version() == shm.ABI_VERSION == 6
     assert shm.lib().shm_strerror(shm.SHM_EINVAL).startswith(b"invalid")
 
 
@@ -63,6 +63,10 @@ def test_create_rejects_bad_config_without_touching_gpu():
     assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
     L.shm_config_init(ctypes.byref(cfg))
     cfg.key_bits = 65
+    assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
+    # the insert ordering's bin counts are 24-bit fields (isort.hip bin_prefix)
+    L.shm_config_init(ctypes.byref(cfg))
+    cfg.max_batch = 1 << 24
     assert L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)) == shm.SHM_EINVAL
     assert L.shm_tree_destroy(None) == shm.SHM_EINVAL
 

@@ -121,8 +121,10 @@ def test_slot_routed_get_p_shards_on_one_gpu(P):
     ncclAllToAll hands each rank -- and the results gathered back
     (shm__route_gather).  Every key lands in its owner's run, the runs'
     tails are kKeyMax, and the gathered values equal the unsharded dict.  A
-    too-small capacity cuts the overflowing keys (they find nothing) and
-    reports kErrOverflow."""
+    too-small capacity puts the overflowing keys on the overflow list (key
+    and input position: what shm_shard_search_end's second round answers,
+    test_local_group_p8_routed_paths); without a list they find nothing and
+    kErrOverflow is reported."""
     import ctypes
 
     import sherman_amd as shm
@@ -132,7 +134,8 @@ def test_slot_routed_get_p_shards_on_one_gpu(P):
     L.shm__route_slots.restype = ctypes.c_int
     L.shm__route_slots.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                    ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
-                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p]
     L.shm__route_gather.restype = ctypes.c_int
     L.shm__route_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -160,12 +163,17 @@ def test_slot_routed_get_p_shards_on_one_gpu(P):
     want = dict(zip(keys.tolist(), vals.tolist()))
     exp = np.array([want.get(int(x), 0) for x in q], dtype=U64)
 
-    for cap, overflow in (((n + n // 4) // P + 256, False), (n // (2 * P), True)):
-        cursor = torch.zeros(P, dtype=torch.int32, device=dev)
+    for cap, overflow, listed in (((n + n // 4) // P + 256, False, True),
+                                  (n // (2 * P), True, True), (n // (2 * P), True, False)):
+        cursor = torch.zeros(P + 1, dtype=torch.int32, device=dev)
         slots = torch.empty(P * cap, dtype=torch.int64, device=dev)
         spos = torch.empty(n, dtype=torch.int32, device=dev)
+        ovk = torch.zeros(n, dtype=torch.int64, device=dev)
+        ovi = torch.zeros(n, dtype=torch.int32, device=dev)
         rc = L.shm__route_slots(trees[0].h, qd.data_ptr(), n, P, cap, cursor.data_ptr(),
-                                slots.data_ptr(), spos.data_ptr(), None)
+                                slots.data_ptr(), spos.data_ptr(),
+                                ovk.data_ptr() if listed else None,
+                                ovi.data_ptr() if listed else None, None)
         assert rc == 0
         res = torch.empty_like(slots)
         for p in range(P):
@@ -191,7 +199,17 @@ def test_slot_routed_get_p_shards_on_one_gpu(P):
             assert np.all(sl[p, c:] == U64((1 << 64) - 1))  # kKeyMax padding
         assert np.array_equal(o[placed], exp[placed])
         assert np.all(o[~placed] == 0) and np.array_equal(f, (o != 0).astype(np.uint8))
-        if overflow:
+        cur = cursor.cpu().numpy()
+        assert np.array_equal(cur[:P], np.bincount(qo, minlength=P))  # routed per peer
+        if listed:
+            # the overflow list: exactly the cut inputs, each with its key
+            m = int(cur[P])
+            assert m == int((~placed).sum())
+            oi = ovi.cpu().numpy().view(np.uint32)[:m]
+            assert np.array_equal(np.sort(oi), np.flatnonzero(~placed).astype(np.uint32))
+            assert np.array_equal(ovk.cpu().numpy().view(U64)[:m], q[oi])
+            trees[0].synchronize()  # nothing reported: the second round answers them
+        elif overflow:
             with pytest.raises(shm.ShermanError):
                 trees[0].synchronize()  # kErrOverflow reported by the next sync
     for t in trees:

@@ -144,6 +144,26 @@ def test_golden_zipf_and_op_mix():
         assert got.tolist() == case["ops"]
 
 
+@pytest.mark.skipif(not os.path.isdir("/root/reference/test"),
+                    reason="the reference checkout is not on this machine")
+def test_golden_zipf_is_the_reference_generator():
+    """The golden zipf draws equal the REFERENCE's own test/zipf.h, compiled
+    by path (oracle/Makefile `ref`, tests/golden/make_zipf_ref.py), and so
+    does the oracle's restatement on further (n, theta, seed) cases — among
+    them C3's and C5's generators (theta 0.99 over 2^26 and 2^31 items)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rc = subprocess.run([sys.executable, os.path.join(root, "tests", "golden",
+                                                      "make_zipf_ref.py")])
+    assert rc.returncode == 0
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    from make_zipf_ref import reference_draws
+    for n, theta, seed in [(64 << 20, 0.99, 0x5EED0007), (1 << 31, 0.99, 12345),
+                           (4000, 0.99, 1), (1 << 20, 0.3, 99), (10, 0.0, 3)]:
+        assert zipf_fill(n, theta, seed, 2000).tolist() == reference_draws(n, theta, seed, 2000)
+
+
 def test_golden_tree_fixture():
     """Reference-rule tree built by the oracle: digest of the search answers
     for a fixed stream (regression pin for the restatement)."""
