@@ -91,7 +91,10 @@ def parse():
                    help="steps of the per-batch latency pass (default: --steps)")
     p.add_argument("--streams", type=int, default=2, choices=(1, 2),
                    help="c2, N=1: consecutive batches alternate over this many HIP "
-                        "streams, so one batch's ordering overlaps the previous walk")
+                        "streams, so one batch's ordering overlaps the previous walk; "
+                        "c5, N=1: 2 = scans and inserts on their own streams, so the "
+                        "inserts' ordering runs beside the scans (the library still "
+                        "orders the inserts' tree changes after the scans)")
     p.add_argument("--sim-world", type=int, default=1,
                    help="N=1 only: build and query shard --sim-rank of a SIM-WORLD-way "
                         "range partition (the per-GPU work of an N-GPU run, no exchange)")
@@ -322,17 +325,23 @@ def main():
             n_cap = int(nc.item())
         scan_out = {}
         applied = [0]  # batches applied so far (all step loops)
+        s_scan = s_ins = None
+        if route is None and args.streams == 2:
+            s_scan, s_ins = torch.cuda.Stream(), torch.cuda.Stream()
+            s_scan.wait_stream(torch.cuda.current_stream())
+            s_ins.wait_stream(torch.cuda.current_stream())
 
         def step(i):
             lo, hi, pk, pv = mixed[applied[0] % n_c5]
             applied[0] += 1
             if route is None and args.async_scans:
                 # scans queued without a host wait; the batch's inserts queue
-                # behind them; every step's total is checked after the run
-                scan_out["r"] = pr = tree.range_query_batch_async(lo, hi)
+                # behind them (their ordering beside them, on their own
+                # stream); every step's total is checked after the run
+                scan_out["r"] = pr = tree.range_query_batch_async(lo, hi, stream=s_scan)
                 if pr.tot is not None:  # only the (total, error) words stay alive
                     scan_out.setdefault("all", []).append((pr.tot, pr.vals.numel()))
-                tree.insert_batch_async(pk, pv)
+                tree.insert_batch_async(pk, pv, stream=s_ins)
             elif route is None:
                 scan_out["r"] = PendingRange(None, *tree.range_query_batch(lo, hi))
                 tree.insert_batch_async(pk, pv)
@@ -531,7 +540,8 @@ def main():
                 "tree_height": st["height"],
                 "pages": st["pages_used"],
                 "get_order": args.sort,
-                "streams": (len(outs) if args.workload == "c2" else 1),
+                "streams": (len(outs) if args.workload == "c2" else
+                            args.streams if args.workload == "c5" and world == 1 else 1),
                 "rccl_groups": (len(outs) if args.workload == "c2" and world > 1 else None),
                 "router": router_kind,
                 "start": args.start,

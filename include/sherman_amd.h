@@ -320,6 +320,13 @@ int shm_shard_range_values(shm_shard *s, uint64_t *vals_out, uint64_t vals_cap, 
  * then shm_synchronize the local tree: the status of every routed batch. */
 int shm_shard_synchronize(shm_shard *s);
 
+/* Tree::lock_bench (include/Tree.h:60, src/Tree.cpp:310-321) for a batch:
+ * take and release lock[CityHash64(keys[i]) % num_locks] of the HBM lock
+ * table (atomicCAS, try_lock_addr / unlock_addr, Tree.cpp:205-264); keys
+ * sharing a word take it in turn.  Ordered like an insert; a spin past its
+ * bound is reported at the next synchronising call. */
+int shm_lock_bench(shm_tree *t, const uint64_t *keys, uint64_t n, void *stream);
+
 /* workload generators on device (test/benchmark.cpp:43-46, zipf.h) ----------- */
 /* keys[j] = CityHash64(i) + 1 (mod keyspace if keyspace != 0), i = first + j */
 int shm_gen_keys(shm_tree *t, uint64_t first, uint64_t n, uint64_t keyspace,

@@ -145,6 +145,7 @@ _SIGNATURES = [
      [vp, vp, vp, u64, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
     ("shm_shard_synchronize", ctypes.c_int, [vp]),
     ("shm_shard_range_values", ctypes.c_int, [vp, vp, u64, vp]),
+    ("shm_lock_bench", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_gen_keys", ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     ("shm_hash_keys", ctypes.c_int, [vp, vp, u64, u64, vp, vp]),
 ]
@@ -469,6 +470,11 @@ class Tree:
             return
         _check(lib().shm_route_unpermute(self.h, _ptr(vals_in), _ptr(perm), vals_in.numel(),
                                          _ptr(out), _stream_ptr(stream)), "unpermute")
+
+    def lock_bench(self, keys, stream=None):
+        """Tree::lock_bench for every key: its lock word taken and released."""
+        _check(lib().shm_lock_bench(self.h, _ptr(keys), keys.numel(), _stream_ptr(stream)),
+               "lock_bench")
 
     def hash_keys(self, ids, out, keyspace=0, stream=None):
         _check(lib().shm_hash_keys(self.h, _ptr(ids), ids.numel(), keyspace, _ptr(out),

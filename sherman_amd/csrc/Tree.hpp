@@ -8,6 +8,9 @@
 //   void del(const Key&, ...)                   del(k[, cxt, coro_id])
 //   uint64_t range_query(from, to, Value* buf)  range_query(from, to, buf[, cxt, coro_id])
 //   void print_and_check_tree(...)              print_and_check_tree([cxt, coro_id])
+//   void lock_bench(const Key&, ...)            lock_bench(k[, cxt, coro_id])
+//   void index_cache_statistics()               index_cache_statistics() (the leaf directory's)
+//   void clear_statistics()                     clear_statistics()
 //   (new) batched forms on device pointers      search_batch / insert_batch / mixed_batch
 //
 // The coroutine arguments are accepted and ignored, so call sites of the
@@ -56,7 +59,7 @@ class Tree {
         hipMalloc(&d_keys_, 2 * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&d_vals_, 2 * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&d_found_, 8) != hipSuccess) {
-      shm_tree_destroy(t_);
+      release();  // whichever of them were allocated
       throw Error(SHM_ENOMEM, "staging buffers");
     }
   }
@@ -65,12 +68,7 @@ class Tree {
     shm_config_init(&c);
     return c;
   }
-  ~Tree() {
-    (void)hipFree(d_keys_);
-    (void)hipFree(d_vals_);
-    (void)hipFree(d_found_);
-    if (t_) shm_tree_destroy(t_);
-  }
+  ~Tree() { release(); }
   Tree(const Tree&) = delete;
   Tree& operator=(const Tree&) = delete;
 
@@ -119,8 +117,11 @@ class Tree {
     uint64_t *d_out = nullptr, *d_off = nullptr;
     if (hipMalloc(&d_out, cnt * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&d_off, sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(d_off, 0, sizeof(uint64_t)) != hipSuccess)
+        hipMemset(d_off, 0, sizeof(uint64_t)) != hipSuccess) {
+      if (d_out) (void)hipFree(d_out);
+      if (d_off) (void)hipFree(d_off);
       throw Error(SHM_ENOMEM, "range buffers");
+    }
     int s = shm_range_query(t_, d_from, d_to, 1, d_cnt, d_off, d_out, nullptr);
     if (s == SHM_OK &&
         hipMemcpy(buffer, d_out, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -169,6 +170,31 @@ class Tree {
     check(shm_stats(t_, &s), "stats");
     return s;
   }
+  // Tree::lock_bench (Tree.cpp:310-321): take and release k's lock word
+  void lock_bench(const Key& k, CoroContext* cxt = nullptr, int coro_id = 0) {
+    (void)cxt;
+    (void)coro_id;
+    stage(k, nullptr);
+    check(shm_lock_bench(t_, d_keys_, 1, nullptr), "lock_bench");
+    check(shm_synchronize(t_), "lock_bench");
+  }
+  // Tree::index_cache_statistics / clear_statistics (Tree.cpp:1175-1185):
+  // the index here is the leaf directory (or the LDS replica); its counters
+  // are collected while enable_statistics(true)
+  void enable_statistics(bool on) { check(shm_profile_enable(t_, on ? 2 : 0), "statistics"); }
+  void index_cache_statistics() {
+    shm_index_stats_t s;
+    check(shm_index_stats(t_, &s, 0), "index statistics");
+    const double g = s.gets ? (double)s.gets : 1.0;
+    printf("index: %llu gets, %.4f start off a leaf, %.4f right moves, %.4f page hops, "
+           "%.3f entry reads per get, %llu hits\n",
+           (unsigned long long)s.gets, s.start_internal / g, s.right_moves / g, s.page_hops / g,
+           s.entry_reads / g, (unsigned long long)s.hits);
+  }
+  void clear_statistics() {
+    shm_index_stats_t s;
+    check(shm_index_stats(t_, &s, 1), "clear statistics");
+  }
   shm_tree* handle() { return t_; }
 
   const uint64_t tree_id;  // include/Tree.h:67 (one tree per handle here)
@@ -179,6 +205,15 @@ class Tree {
       throw Error(SHM_EIO, "stage key");
     if (v && hipMemcpy(d_vals_, v, sizeof(*v), hipMemcpyHostToDevice) != hipSuccess)
       throw Error(SHM_EIO, "stage value");
+  }
+  void release() {
+    if (d_keys_) (void)hipFree(d_keys_);
+    if (d_vals_) (void)hipFree(d_vals_);
+    if (d_found_) (void)hipFree(d_found_);
+    d_keys_ = d_vals_ = nullptr;
+    d_found_ = nullptr;
+    if (t_) shm_tree_destroy(t_);
+    t_ = nullptr;
   }
   shm_tree* t_ = nullptr;
   uint64_t* d_keys_ = nullptr;

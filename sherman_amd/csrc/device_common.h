@@ -348,7 +348,7 @@ __device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f
 
 // A leaf's summary line read whole (one 128 B request): false if it does not
 // describe a current leaf; else its highest fence, sibling and the slots
-// whose 16-bit fingerprint equals k's (bit s for slot s)
+// whose 8-bit fingerprint equals k's (bit s for slot s)
 struct SumLine {
   uint64_t highest, cand;
 };

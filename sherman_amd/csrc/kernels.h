@@ -368,6 +368,11 @@ void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_
                            uint64_t n, uint64_t cap, uint32_t P, const uint64_t* offsets,
                            uint64_t* vals, uint64_t vals_cap, hipStream_t s);
 
+// Tree::lock_bench over the HBM lock table: each key's word taken (atomicCAS
+// to tag | 1) and released (tag), bounded spins (kErrLock)
+void launch_lock_bench(const uint64_t* keys, uint64_t n, uint64_t* locks, uint32_t num_locks,
+                       uint64_t tag, uint32_t* err, hipStream_t s);
+
 // ---- batched range scans (range.hip) -------------------------------------------
 struct RangeArgs {
   const uint8_t* arena;

@@ -154,6 +154,11 @@ struct shm_tree {
   hipEvent_t ex_ev = nullptr;       // last exclusive call
   hipStream_t ex_s = nullptr;
   bool ex_valid = false;
+  // the last insert chunk (its ordering workspace): a later insert's
+  // ordering on another stream waits for this, not for every exclusive call
+  hipEvent_t ins_ev = nullptr;
+  hipStream_t ins_s = nullptr;
+  bool ins_valid = false;
   hipEvent_t gws_ev[2] = {nullptr, nullptr};  // last user of each get workspace
   hipStream_t gws_s[2] = {nullptr, nullptr};
   bool gws_valid[2] = {false, false};
@@ -637,21 +642,40 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   return SHM_OK;
 }
 
-int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
-                 uint64_t n, bool skip_pad = false) {
-  const uint32_t tag = ++t->chunks;
-  shm_tree::ProfRec pr{};
+// the chunk's ordering (step 1): its tag, profile record started
+int insert_begin(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
+                 uint64_t n, bool skip_pad, uint32_t* tag, shm_tree::ProfRec& pr) {
+  *tag = ++t->chunks;
   if (t->prof_on) {
     const int rc = prof_begin(t, s, shm_tree::kProfInsert, n, 4, pr);
     if (rc) return rc;
   }
-  if (const int rc = insert_order(t, s, keys, vals, n, tag, skip_pad)) return rc;
-  // leaves of the upserts
+  return insert_order(t, s, keys, vals, n, *tag, skip_pad);
+}
+
+// steps 2-5 once the device state may change (the leaf directory current)
+int insert_finish(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag, shm_tree::ProfRec& pr) {
   if (use_leaf_dir(t)) {
     const int rc = refresh_dir(t, s);
     if (rc) return rc;
   }
-  return insert_apply(t, s, n, tag, pr);
+  const int rc = insert_apply(t, s, n, tag, pr);
+  if (rc == SHM_OK) {
+    if (!t->ins_ev) t->ins_ev = new_event();
+    if (t->ins_ev && hipEventRecord(t->ins_ev, s) == hipSuccess) {
+      t->ins_s = s;
+      t->ins_valid = true;
+    }
+  }
+  return rc;
+}
+
+int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
+                 uint64_t n, bool skip_pad = false) {
+  uint32_t tag = 0;
+  shm_tree::ProfRec pr{};
+  if (const int rc = insert_begin(t, s, keys, vals, n, skip_pad, &tag, pr)) return rc;
+  return insert_finish(t, s, n, tag, pr);
 }
 
 // every chunk of one insert call, in order.  A chunk holding kKeyMax is
@@ -664,13 +688,28 @@ int insert_all(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t
   if (!t || (n && (!keys || !vals))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(stream);
+  // The first chunk's ordering reads only the batch and writes the insert
+  // workspace, so it is queued before this call's cross-stream wait: it
+  // waits for the previous insert (the workspace's last user) but not for,
+  // e.g., the range scans just issued on another stream, and runs beside
+  // them.  (An ordered search's workspace aliases the insert workspace:
+  // not with SHM_FLAG_SORT_GETS.)
+  const bool early = n > 0 && !(t->cfg.flags & SHM_FLAG_SORT_GETS);
+  uint32_t tag0 = 0;
+  shm_tree::ProfRec pr0{};
+  const uint64_t m0 = std::min(t->nmax, n);
+  if (early) {
+    if (t->ins_valid && t->ins_s != s) HIP_OK(hipStreamWaitEvent(s, t->ins_ev, 0));
+    if (const int rc = insert_begin(t, s, keys, vals, m0, skip_pad, &tag0, pr0)) return rc;
+  }
   Order ord(t, s, true);
   if (ord.rc) return ord.rc;
   mirror(t);
   int rc = SHM_OK;
   for (uint64_t off = 0; off < n && rc == SHM_OK; off += t->nmax) {
     const uint64_t m = std::min(t->nmax, n - off);
-    rc = insert_chunk(t, s, keys + off, vals + off, m, skip_pad);
+    rc = off == 0 && early ? insert_finish(t, s, m0, tag0, pr0)
+                           : insert_chunk(t, s, keys + off, vals + off, m, skip_pad);
   }
   if (rc == SHM_OK) {
     t->batches += 1;
@@ -707,6 +746,7 @@ void free_all(shm_tree* t) {
   }
   for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
   if (t->ex_ev) (void)hipEventDestroy(t->ex_ev);
+  if (t->ins_ev) (void)hipEventDestroy(t->ins_ev);
   for (hipEvent_t e : t->gws_ev)
     if (e) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -1548,6 +1588,21 @@ int shm_route_unpermute_found(shm_tree* t, const uint64_t* in, const uint32_t* p
   if (!t || (n && (!in || !perm || !out || !found_out))) return SHM_EINVAL;
   dev::launch_unpermute(in, perm, n, out, found_out, pick(stream));
   HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
+int shm_lock_bench(shm_tree* t, const uint64_t* keys, uint64_t n, void* stream) {
+  if (!t || (n && !keys)) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(stream);
+  Order ord(t, s, true);  // the lock words: no chunk may hold them meanwhile
+  if (ord.rc) return ord.rc;
+  // the tag of the last chunk issued: every word is free for it once that
+  // chunk has retired (stream order)
+  dev::launch_lock_bench(keys, n, t->locks, t->cfg.num_locks, (uint64_t)t->chunks << 32, t->d_err,
+                         s);
+  HIP_OK(hipGetLastError());
+  t->err_pending = true;
   return SHM_OK;
 }
 

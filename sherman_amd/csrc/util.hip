@@ -674,5 +674,39 @@ void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_
                        offsets, vals, vals_cap);
 }
 
+// ---- Tree::lock_bench (src/Tree.cpp:310-321): take and release the lock word
+// of each key, lock[CityHash64(key) % num_locks], as try_lock_addr /
+// unlock_addr do (Tree.cpp:205-264) on the HBM lock table: a word is free
+// when it holds <= tag (the epoch tags of the insert chunks, insert.hip),
+// taken as tag | 1 by atomicCAS, released by storing tag.  Lanes of one wave
+// that share a word take it in turn (a lane releases in the iteration it
+// acquired, so the wave never waits on itself).  Spins are bounded.
+__global__ __launch_bounds__(kT) void k_lock_bench(const uint64_t* keys, uint64_t n,
+                                                   uint64_t* locks, uint32_t num_locks,
+                                                   uint64_t tag, uint32_t* err) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  bool done = i >= n;
+  unsigned long long* w = nullptr;
+  if (!done)
+    w = reinterpret_cast<unsigned long long*>(locks) + cityhash64_u64(keys[i]) % num_locks;
+  const unsigned long long mine = (unsigned long long)(tag | 1ull);
+  for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
+    if (!done) {
+      const unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur <= (unsigned long long)tag && atomicCAS(w, cur, mine) == cur) {
+        __hip_atomic_store(w, (unsigned long long)tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
+      }
+    }
+    if (!ballot(!done)) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (!done) atomicOr(err, kErrLock);
+}
+void launch_lock_bench(const uint64_t* keys, uint64_t n, uint64_t* locks, uint32_t num_locks,
+                       uint64_t tag, uint32_t* err, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_lock_bench, grid1(n), dim3(kT), 0, s, keys, n, locks, num_locks, tag, err);
+}
+
 }  // namespace dev
 }  // namespace shm

@@ -47,6 +47,16 @@ int main() {
   tree.check_tree(&leaves, &internal, &keys);
   CHECK(keys == N - 1);
   tree.print_and_check_tree(cxt, 0);
+  // the remaining members of the reference's Tree (include/Tree.h:58-63)
+  for (uint64_t i = 1; i < 64; ++i) tree.lock_bench(i, cxt, 0);
+  tree.clear_statistics();
+  tree.enable_statistics(true);
+  for (uint64_t i = 1; i < 200; ++i) CHECK(tree.search(i, v) && v == i * 3);
+  tree.index_cache_statistics();
+  tree.enable_statistics(false);
+  tree.insert(5, 55);  // the lock words are free again after lock_bench
+  CHECK(tree.search(5, v) && v == 55);
+  tree.insert(5, 15);
   std::printf("tree_test ok: %lu keys, %lu leaves, %lu internal pages, height %u\n",
               (unsigned long)keys, (unsigned long)leaves, (unsigned long)internal,
               tree.stats().height);

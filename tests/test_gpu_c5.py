@@ -14,7 +14,8 @@ stream on real GPU shards against ONE unsharded CPU oracle.
     rank-major order (routed inserts, sherman_amd/shard.py);
   * world 1 over RCCL ("nccl") and world 2 over gloo with two trees sharing
     the GPU (RCCL refuses two ranks on one device; the driver's 8-GPU run
-    covers RCCL at world > 1).
+    covers RCCL at world > 1), and world 1 through the C-ABI shard
+    (sherman_amd.CShard: routed inserts and range scans in C++, shm_shard_*).
 
 Checked: per scan the oracle's values (a multiset: slot order inside a leaf
 and leaf boundaries after batched splits may differ), the final key->value
@@ -66,7 +67,7 @@ def op_values(rank, b, n):
     return (np.arange(n, dtype=U64) + U64((rank * ROUNDS + b) * BATCH + 1))
 
 
-def gpu_worker(rank, world, port, outdir, backend):
+def gpu_worker(rank, world, port, outdir, backend, cabi=False):
     import sherman_amd as shm
     from oracle.pyoracle import to_key  # noqa: F401  (same generator family)
     from sherman_amd.shard import ShardRouter, owner_of, shard_range
@@ -79,7 +80,10 @@ def gpu_worker(rank, world, port, outdir, backend):
     lo, bits = shard_range(rank, world)
     tree = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 17, device=0, node_id=rank,
                     key_lo=lo, key_bits=bits)
-    router = ShardRouter(tree, world, dist)
+    cs = shm.CShard(tree, world, rank, dist) if cabi else None
+    router = ShardRouter(tree, world, dist, cshard=cs)
+    # routed scans through the C shard: one piece-matrix width on every rank
+    n_cap = max(int(c5_batch(r, b, world)[0].sum()) for r in range(world) for b in range(ROUNDS))
     # preload this rank's shard of key(1 .. N_PRE * world)
     total = N_PRE * world
     keys = torch.empty(total, dtype=torch.int64, device=dev)
@@ -98,19 +102,21 @@ def gpu_worker(rank, world, port, outdir, backend):
         kh = k.cpu().numpy().view(U64)
         slo, shi = scan_bounds(kh[is_scan], world)
         counts, svals = router.range_query(torch.from_numpy(slo.view(np.int64)).to(dev),
-                                           torch.from_numpy(shi.view(np.int64)).to(dev))
+                                           torch.from_numpy(shi.view(np.int64)).to(dev), n_cap)
         ik = torch.from_numpy(kh[~is_scan].view(np.int64)).to(dev)
         iv = torch.from_numpy(op_values(rank, b, int((~is_scan).sum())).view(np.int64)).to(dev)
         router.insert(ik, iv)
         out[f"scounts{b}"] = counts.cpu().numpy()
         out[f"svals{b}"] = svals.cpu().numpy()
         out[f"keys{b}"] = kh
-    tree.synchronize()
+    router.synchronize()
     st = tree.check()  # raises on a broken invariant
     from test_gpu_shard import tree_contents
     ck, cv = tree_contents(tree)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), ck=ck, cv=cv,
              grew=np.array([tree.stats()["pages_used"] - pages0, st["keys"]]), **out)
+    if cs is not None:
+        cs.close()
     tree.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -155,9 +161,11 @@ def verify(d, world):
     ref.close()
 
 
-@pytest.mark.parametrize("backend,world", [("nccl", 1), ("gloo", 2)])
-def test_c5_stream_on_gpu_shards_matches_unsharded_oracle(backend, world):
+@pytest.mark.parametrize("backend,world,cabi", [("nccl", 1, False), ("gloo", 2, False),
+                                                ("nccl", 1, True)])
+def test_c5_stream_on_gpu_shards_matches_unsharded_oracle(backend, world, cabi):
     assert torch.cuda.is_available(), "GPU test without a GPU"
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(gpu_worker, args=(world, free_port(), d, backend), nprocs=world, join=True)
+        mp.spawn(gpu_worker, args=(world, free_port(), d, backend, cabi), nprocs=world,
+                 join=True)
         verify(d, world)

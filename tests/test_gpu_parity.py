@@ -969,6 +969,27 @@ def test_get_start_modes_and_index_stats(lib_ok, start):
     t.close()
 
 
+def test_lock_bench_contended_words(lib_ok):
+    """Tree::lock_bench (Tree.cpp:310-321) over the HBM lock table: 2^17 keys
+    on 100 distinct lock words (lanes of one wave contend for one word)
+    finish without a lock error, and every word is free afterwards (an
+    insert that takes the words of its pages succeeds)."""
+    t = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 14)
+    orc = OracleTree(64 << 20)
+    ks = hashed_keys(1, 20001)
+    gpu_insert(t, ks, ks + U64(1))
+    orc.apply_batch(ks, ks + U64(1))
+    rng = np.random.default_rng(3)
+    t.lock_bench(dev(rng.integers(1, 101, 1 << 17).astype(U64)))
+    t.synchronize()
+    more = hashed_keys(30001, 40001)
+    gpu_insert(t, more, more + U64(2))
+    orc.apply_batch(more, more + U64(2))
+    compare_contents(t, orc)
+    orc.close()
+    t.close()
+
+
 def test_pending_range_waits_for_its_issue_stream(lib_ok):
     """range_query_batch_async issued on a side stream (stream=None there
     means that stream) and .result() called outside it: the result waits for
