@@ -517,7 +517,7 @@ __global__ __launch_bounds__(1024) void k_top(const uint8_t* arena, uint64_t are
           const uint32_t* d = reinterpret_cast<const uint32_t*>(pg);
           const uint64_t leftmost = (uint64_t)((d[2] >> 8) | (d[3] << 24)) |
                                     ((uint64_t)((d[3] >> 8) | (d[4] << 24)) << 32);
-          const int cnt = (int)(int16_t)(d[4] >> 16) + 1;
+          const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
           c = leftmost ? 1u + (uint32_t)(cnt < 0 ? 0 : cnt) : 0u;
           if (!leftmost || pg[kOffLevel] <= 1) atomicOr(&s_stop, 1u);  // children are leaves
         }
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(1024) void k_top(const uint8_t* arena, uint64_t are
         const uint32_t* d = reinterpret_cast<const uint32_t*>(pg);
         leftmost = (uint64_t)((d[2] >> 8) | (d[3] << 24)) |
                    ((uint64_t)((d[3] >> 8) | (d[4] << 24)) << 32);
-        const int cnt = (int)(int16_t)(d[4] >> 16) + 1;
+        const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
         c = 1u + (uint32_t)(cnt < 0 ? 0 : cnt);
         lowest = cur_k[j];
       }

@@ -964,6 +964,10 @@ def test_get_start_modes_and_index_stats(lib_ok, start):
         else:
             assert st["start_internal"] == probe.size, st
             assert st["page_hops"] >= probe.size * (1 if start == "lds" else 2), st
+            # the replica's page is the one holding k (no walk along a level)
+            hops = t.stats()["height"] - (2 if start == "lds" else 1)
+            assert st["page_hops"] <= probe.size * hops, (st, hops)
+        assert st["right_moves"] < probe.size // 10, st
     assert t.stats()["height"] >= 3
     orc.close()
     t.close()
