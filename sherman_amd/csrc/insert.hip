@@ -62,8 +62,10 @@ struct WaveLds {
   uint64_t a_key[kWave];
   uint64_t a_val[kWave];
   uint32_t a_ver[kWave];
-  uint64_t o_key[kWave];  // a segment's ops staged (stage_ops)
+  uint64_t o_key[kWave];  // a segment's ops staged (stage_ops); propagate's run
   uint64_t o_val[kWave];
+  uint64_t r_key[kWave];  // separators a direct propagation made (the next run)
+  uint64_t r_ptr[kWave];
 };
 
 __device__ __forceinline__ uint32_t lock_index(uint64_t page, uint32_t n) {
@@ -97,7 +99,7 @@ __device__ __forceinline__ bool op_contains(const Ops& o, uint64_t key) {
 
 // Surviving entries of the staged leaf (valid, not overwritten by an op),
 // sorted by key into L.a_* ; returns their count.
-__device__ int leaf_survivors(WaveLds& L, const Ops& o) {
+__device__ __forceinline__ int leaf_survivors(WaveLds& L, const Ops& o) {
   const int lane = lane_id();
   const LeafEnt e = leaf_entry(L.page, lane < kLeafCardinality ? lane : 0);
   bool keep = lane < kLeafCardinality && e.val != kValueNull;
@@ -116,7 +118,7 @@ __device__ int leaf_survivors(WaveLds& L, const Ops& o) {
 }
 
 // Surviving records of an internal page (lane slice w), in key order.
-__device__ int internal_survivors(WaveLds& L, const u32x4 w, int cnt, const Ops& o) {
+__device__ __forceinline__ int internal_survivors(WaveLds& L, const u32x4 w, int cnt, const Ops& o) {
   const int lane = lane_id();
   const IntRec r = internal_record(w);
   bool keep = lane >= 3 && lane - 3 < cnt;
@@ -173,7 +175,7 @@ __device__ __forceinline__ uint64_t new_ga(uint16_t node, uint64_t first_new, in
 
 // Write leaf page p of the split (survivors in L.a_*); returns its lowest
 // fence (the separator of p > 0, copied up as in Tree.cpp:939-950).
-__device__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
+__device__ __forceinline__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
                                     const Ops& o, const SplitPage& s) {
   const int lane = lane_id();
   const uint32_t base = s.T / (uint32_t)s.P, rem = s.T % (uint32_t)s.P;
@@ -204,7 +206,7 @@ __device__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds& L, const Hdr& h
 // Internal page p of the split: q = T - (P - 1) records stay, one record per
 // extra page is pushed up (its ptr becomes that page's leftmost, its key the
 // separator, Tree.cpp:779-793).  Returns the page's lowest fence.
-__device__ uint64_t build_internal_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
+__device__ __forceinline__ uint64_t build_internal_page(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
                                         const Ops& o, const SplitPage& s, uint32_t level) {
   const int lane = lane_id();
   const uint32_t q = s.T - (uint32_t)(s.P - 1);
@@ -252,7 +254,7 @@ __device__ uint64_t build_internal_page(const UpperArgs& a, WaveLds& L, const Hd
 // The root page becomes the new internal root one level up, {leftmost = X}
 // with no records (update_new_root, Tree.cpp:126-149); the level's separators
 // are then inserted into it by the next level.
-__device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint32_t level,
+__device__ __forceinline__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint32_t level,
                                uint32_t old_fver) {
   wave_lds_sync();
   init_page_image(L.page, (old_fver + 1) & 0xFF, x, 0, level, -1, kKeyMin, kKeyMax);
@@ -269,7 +271,7 @@ __device__ void write_new_root(const UpperArgs& a, WaveLds& L, uint64_t x, uint3
 // (665-685), one wave.  0 on an inconsistency (error bits in *err).
 // soft: a starting point only (the caller re-checks under the page's lock):
 // a failure returns 0 without error bits
-__device__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err,
+__device__ __forceinline__ uint64_t parent_of(const UpperArgs& a, uint64_t k, uint32_t level, uint32_t* err,
                               bool soft = false) {
   uint32_t scratch = 0;
   if (soft) err = &scratch;
@@ -376,7 +378,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* red, uint32
 // generation a barrier completes is derived from the value an arrival
 // returns.  Bounded: a spin past kBarrierSpins sets the abort word, which
 // releases every other block too; returns false then.
-__device__ bool grid_sync(UpperCtl* ctl, uint32_t par, uint32_t nb, uint32_t* flag) {
+__device__ __forceinline__ bool grid_sync(UpperCtl* ctl, uint32_t par, uint32_t nb, uint32_t* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -445,7 +447,7 @@ __device__ __forceinline__ void block_range(uint32_t n, uint32_t b, uint32_t nb,
 // false: the running sum of seg_np passes j) or being its j-th split
 // (by_split: the j-th segment with seg_np > 0), one wave; before = the new
 // pages of the range's segments ahead of it.  g = r1 if the counts disagree.
-__device__ void find_seg(const uint32_t* np, uint32_t r0, uint32_t r1, uint32_t j, bool by_split,
+__device__ __forceinline__ void find_seg(const uint32_t* np, uint32_t r0, uint32_t r1, uint32_t j, bool by_split,
                          uint32_t& g, uint32_t& before) {
   const int lane = lane_id();
   uint32_t run_c = 0, run_np = 0;
@@ -518,7 +520,7 @@ __device__ __forceinline__ uint32_t fan_tag(uint64_t batch, uint32_t level) {
 // r = f) and write back that 18 B entry, then release.  Keys are unique in a
 // batch, so two waves never touch one entry; they may share a page and
 // serialise on its word.
-__device__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_t& err) {
+__device__ __forceinline__ void delete_key(const UpperArgs& a, uint64_t k, uint32_t* lp, uint32_t& err) {
   const int lane = lane_id();
   uint64_t ptr = a.root;
   if (a.dir) ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
@@ -665,9 +667,12 @@ __device__ __forceinline__ void emit_sep(const UpperArgs& a, uint32_t lvl, uint6
     err |= kErrPlan;
     return;
   }
-  a.sep_key[lvl & 1][j] = key;
-  a.sep_ptr[lvl & 1][j] = child;
-  a.ipage[lvl & 1][j] = parent;
+  // selects, not a[lvl & 1]: a runtime index into the kernel argument
+  // would copy it to scratch
+  const bool odd = (lvl & 1) != 0;
+  (odd ? a.sep_key[1] : a.sep_key[0])[j] = key;
+  (odd ? a.sep_ptr[1] : a.sep_ptr[0])[j] = child;
+  (odd ? a.ipage[1] : a.ipage[0])[j] = parent;
 }
 
 // the page's lock word held exclusively (tag | 1, as the deletes take it;
@@ -706,23 +711,39 @@ __device__ __forceinline__ void unlock_excl(const UpperArgs& a, uint64_t page) {
 // last (Tree.cpp:699-826 for a batch of separators), new separators emitted
 // to the next level; the root splits into a fresh page X and becomes the new
 // root one level up (update_new_root, Tree.cpp:126-149).
-__device__ void apply_internal(const UpperArgs& a, WaveLds& L, const Hdr& h, int na, const Ops& o,
-                               uint64_t page, uint32_t level, uint64_t base, uint64_t cap,
-                               uint32_t& err) {
+// direct (propagate): the new separators go to the wave's L.r_* from index
+// nout on (the next level's run, in key order) instead of the level's list.
+// Returns nout plus the separators it put there.
+__device__ __forceinline__ uint32_t apply_internal(const UpperArgs& a, WaveLds& L, const Hdr& h, int na,
+                                   const Ops& o, uint64_t page, uint32_t level, uint64_t base,
+                                   uint64_t cap, uint32_t& err, bool direct = false,
+                                   uint32_t nout = 0) {
   const uint32_t T2 = (uint32_t)na + o.nb;
   const uint32_t P = T2 <= (uint32_t)(kInternalCardinality - 1)
                          ? 1u
                          : (T2 + 1 + kInternalSplitFill) / (kInternalSplitFill + 1);
   if (P == 1) {
     (void)build_internal_page(a, L, h, na, o, SplitPage{0, 1, T2, 0, page}, level);
-    return;
+    return nout;
   }
   const bool grow = page == a.root;
   const uint64_t first = alloc_pages(a, base, cap, P - 1 + (grow ? 1u : 0u), err);
-  if (first == ~0ull) return;  // no room: the page stays as it was (reported)
+  if (first == ~0ull) return nout;  // no room: the page stays as it was (reported)
   for (uint32_t p = 1; p < P; ++p) {
     const SplitPage sp{(int)p, (int)P, T2, first, new_ga(a.node, first, (int)p)};
     const uint64_t low = build_internal_page(a, L, h, na, o, sp, level);
+    if (direct) {
+      if (nout >= (uint32_t)kWave) {
+        err |= kErrPlan;  // cannot happen from runs of <= kSmallSplit - 1
+      } else {
+        if (lane_id() == 0) {
+          L.r_key[nout] = low;
+          L.r_ptr[nout] = sp.dest;
+        }
+        ++nout;
+      }
+      continue;
+    }
     const uint64_t par = grow ? a.root : parent_of(a, low, level + 1, &err);
     emit_sep(a, level + 1, low, sp.dest, par, err);
   }
@@ -732,6 +753,7 @@ __device__ void apply_internal(const UpperArgs& a, WaveLds& L, const Hdr& h, int
     write_new_root(a, L, dest0, level + 1, h.fver);
     if (lane_id() == 0) atomicMax(&a.ctl->root_new[a.par][0], level + 1);
   }
+  return nout;
 }
 
 // Level >= 2: a run of separators (sorted keys [hs, he) of the block's LDS
@@ -742,13 +764,16 @@ __device__ void apply_internal(const UpperArgs& a, WaveLds& L, const Hdr& h, int
 // word.  The ops below the page's highest fence go in; the rest move right
 // (B-link); a page no longer at `level` (the root grew, or a page another
 // wave has just created is not visible yet) is found again from the root.
-__device__ void apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
-                          const uint64_t* ptrs, uint32_t hs, uint32_t he, uint64_t page,
-                          uint32_t level, uint64_t base, uint64_t cap, uint32_t& err) {
+// direct: as apply_internal; returns the separators made (direct only).
+__device__ __forceinline__ uint32_t apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
+                              const uint64_t* ptrs, uint32_t hs, uint32_t he, uint64_t page,
+                              uint32_t level, uint64_t base, uint64_t cap, uint32_t& err,
+                              bool direct = false) {
+  uint32_t nout = 0;
   for (int hop = 0; hs < he; ++hop) {
     if (hop >= kMaxRounds) {
       err |= kErrRounds;
-      return;
+      return nout;
     }
     if (!ptr_ok(page, a.node, a.arena_bytes)) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -757,7 +782,7 @@ __device__ void apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
     }
     if (!lock_excl(a, page)) {
       err |= kErrLock;
-      return;
+      return nout;
     }
     const u32x4 w = load_page_slice(a.arena, ga_offset(page));
     const Hdr h = parse_hdr(w);
@@ -782,11 +807,41 @@ __device__ void apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
     if (m > hs) {
       const Ops o{keys, ptrs, hs, m - hs};
       const int na = internal_survivors(L, w, h.last_index + 1, o);
-      apply_internal(a, L, h, na, o, page, level, base, cap, err);
+      nout = apply_internal(a, L, h, na, o, page, level, base, cap, err, direct, nout);
     }
     unlock_excl(a, page);
     hs = m;
     page = h.sibling;  // Tree.cpp:737-743
+  }
+  return nout;
+}
+
+// Direct propagation (every split of the chunk small): the separators one
+// wave made, L.r_*[0, n) in key order, go into `level` at once under the
+// parents' exclusive words, and the separators that makes go one level up,
+// by the same wave, until a level takes its run in place -- the reference's
+// recursive internal_page_store (Tree.cpp:699-826, 804-812), a run at a time.
+// No list and no grid barrier: waves meet only on a shared parent's word.
+// A run of <= kSmallSplit - 1 separators splits each page it touches at most
+// once, so every level's run stays that short (the 64-entry LDS bound).
+__device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32_t n, uint32_t level,
+                          uint64_t base, uint64_t cap, uint32_t& err) {
+  for (; n; ++level) {
+    if (level > (uint32_t)kMaxLevelOfTree) {
+      err |= kErrRounds;
+      return;
+    }
+    const int lane = lane_id();
+    wave_lds_sync();
+    if ((uint32_t)lane < n) {
+      L.o_key[lane] = L.r_key[lane];
+      L.o_val[lane] = L.r_ptr[lane];
+    }
+    wave_lds_sync();
+    // the parent: a header walk from the root (a hint; apply_run re-checks
+    // it under the word and moves right or relocates)
+    const uint64_t hint = parent_of(a, L.o_key[0], level, &err, true);
+    n = apply_run(a, L, L.o_key, L.o_val, 0, n, hint, level, base, cap, err, true);
   }
 }
 
@@ -801,16 +856,17 @@ struct LvlLds {
   uint64_t hint[kLvlSort];
   uint32_t head[kLvlSort];
 };
-__device__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t* red,
+__device__ __forceinline__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t* red,
                             uint32_t n, uint32_t level, uint64_t base, uint64_t cap,
                             uint32_t& err) {
   const int t = threadIdx.x, wv = t >> 6;
   const uint32_t b = blockIdx.x, nb = gridDim.x;
   const uint32_t share = (n + nb - 1) / nb;
   const uint32_t per = share < kLvlSort ? share : kLvlSort;
-  const uint64_t* gk = a.sep_key[level & 1];
-  const uint64_t* gp = a.sep_ptr[level & 1];
-  const uint64_t* gh = a.ipage[level & 1];
+  const bool odd = (level & 1) != 0;
+  const uint64_t* gk = odd ? a.sep_key[1] : a.sep_key[0];
+  const uint64_t* gp = odd ? a.sep_ptr[1] : a.sep_ptr[0];
+  const uint64_t* gh = odd ? a.ipage[1] : a.ipage[0];
   for (uint32_t c0 = b * per; c0 < n; c0 += nb * per) {
     const uint32_t cnt = n - c0 < per ? n - c0 : per;
     uint32_t m2 = 1;
@@ -871,8 +927,13 @@ __device__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t*
 //             split's pages, siblings first and page 0 last (it holds the old
 //             page's survivors, so no fan-in); larger splits: their sibling
 //             pages spread over every wave of the grid, page 0 after the
-//             fan-in of its builders.  Each new leaf's separator goes to
-//             position (its global new-page index): key order.
+//             fan-in of its builders.
+//   direct    (every split small, C5's chunks) the wave then takes its
+//             split's separators up itself (propagate): parents under their
+//             exclusive words, a parent's split going one level further, the
+//             root growing in place -- no list, no grid barrier
+//   otherwise each new leaf's separator goes to position (its global
+//             new-page index) of level 1's list: key order
 //   --- grid barrier ---
 //   level 1   runs of separators with one parent, one wave per run: the
 //             parent's epoch lock word, its survivors and the run merged,
@@ -882,9 +943,13 @@ __device__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t*
 //   level >=2 each block's share of the separators (emitted unordered),
 //             sorted in LDS, runs of one parent under its exclusive word
 //   (--- grid barrier --- after every level: the next level's count)
-//   deletes   Tree::del of the chunk's deletes (after every split)
-//   block 0   the superblock and its host mirror
-__global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
+//   deletes   Tree::del of the chunk's deletes (after every split: a grid
+//             barrier in the direct case too)
+//   last      the last block to finish: the superblock and its host mirror
+// 4 waves per SIMD (<= 128 VGPRs): two blocks fit a CU, so the persistent
+// launches of two processes sharing a GPU can be resident together
+__global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void k_upper(
+    UpperArgs a) {
   __shared__ __attribute__((aligned(16))) WaveLds s_l[kUpWaves];
   __shared__ uint32_t s_red[kUpWaves];
   __shared__ uint32_t s_flag;
@@ -931,6 +996,7 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     ctl->alloc[par ^ 1][0] = 0;
     ctl->made[par ^ 1][0] = 0;
     ctl->root_new[par ^ 1][0] = 0;
+    ctl->done[par ^ 1][0] = 0;
   }
   // leaf level: the upsert kernel left per-range new-page / split counts
   const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
@@ -953,6 +1019,9 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
     __syncthreads();
   }
   bool ok = true;
+  // every split small (C5's chunks): each wave takes its separators up
+  // itself (propagate), no level list, no grid barrier
+  const bool direct = nbig == 0 && !a.no_direct;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
   const bool fits = cursor0 + total + (grow0 ? 1u : 0u) <= cap;
   // pages past the leaf level's: the internal levels' bump allocator
@@ -1026,6 +1095,13 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
         for (int p = 1; p < P; ++p) {
           const SplitPage sp{p, P, a.seg_T[g], first + pb, new_ga(a.node, first + pb, p)};
           const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
+          if (direct) {  // the wave's run for level 1
+            if (lane == 0) {
+              L.r_key[p - 1] = low;
+              L.r_ptr[p - 1] = sp.dest;
+            }
+            continue;
+          }
           const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
           if (lane == 0) {
             const uint32_t gp = pb + (uint32_t)(p - 1);
@@ -1038,18 +1114,20 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
       const uint64_t dest = grow0 ? ga_make(a.node, xroot * kPageSize) : page;
       (void)build_leaf_page(a, L, h, na, o, SplitPage{0, P, a.seg_T[g], first + pb, dest});
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
+      if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err);
     }
     if (grow0) root_level = 1;
     stamp();
     if (a.force_abort && b == 0 && t == 0)  // diagnostics: this launch stops here
       __hip_atomic_store(&ctl->abort[par][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // level 1 reads every block's separators
-    ok = grid_sync(ctl, par, nb, &s_flag);
+    // level 1 reads every block's separators; with direct propagation only
+    // the deletes wait for the splits
+    if (!direct || *a.n_del || a.force_abort) ok = grid_sync(ctl, par, nb, &s_flag);
     stamp();
   }
 
   // ---- level 1: runs of separators with one parent -----------------------------
-  if (ok && total && fits) {
+  if (ok && total && fits && !direct) {
     const uint64_t* skey = a.sep_key[1];
     const uint64_t* sptr = a.sep_ptr[1];
     const uint64_t* spg = a.ipage[1];
@@ -1128,16 +1206,32 @@ __global__ __launch_bounds__(kUpT) void k_upper(UpperArgs a) {
   for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
   stamp();
-  if (b == 0 && t == 0) {
-    // superblock (device-authoritative) and its host mirror; with splits
-    // every block has passed the last barrier, so the counters are final
-    const uint64_t extra = total && fits ? ctl->alloc[par][0] : 0ull;
+  // the last block to finish writes the superblock: every block's
+  // allocations and root growth are in the counters by then
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t d = __hip_atomic_fetch_add(&ctl->done[par][0], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    s_flag = d == nb - 1;
+  }
+  __syncthreads();
+  if (s_flag && t == 0) {
+    // superblock (device-authoritative) and its host mirror
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint64_t extra = total && fits ? __hip_atomic_load(&ctl->alloc[par][0], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0ull;
     uint64_t cursor = total && fits ? base + extra : cursor0;
     if (cursor > cap) cursor = cap;  // failed allocations used no page
-    const uint32_t rn = ctl->root_new[par][0];
+    const uint32_t rn =
+        __hip_atomic_load(&ctl->root_new[par][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (grow0 && total && fits) root_level = 1;
     if (rn > root_level) root_level = rn;
-    const uint64_t made = total && fits ? (uint64_t)total + ctl->made[par][0] : 0ull;
+    const uint64_t made =
+        total && fits ? (uint64_t)total + __hip_atomic_load(&ctl->made[par][0], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                      : 0ull;
     sb->next_page = cursor;
     sb->root_level = root_level;
     sb->splits += made;

@@ -130,6 +130,7 @@ struct UpperCtl {
   uint64_t made[2][16];
   uint32_t root_new[2][32];
   uint32_t lvl_sep[2][16];
+  uint32_t done[2][32];  // blocks finished: the last one writes the superblock
 };
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
@@ -231,6 +232,9 @@ struct UpperArgs {
   // diagnostics (shm__upper_force_abort): block 0 raises the abort word
   // before the first grid barrier of this launch
   uint32_t force_abort;
+  // diagnostics (SHM_UPPER_LISTS=1 in the environment): never propagate
+  // directly, every chunk through the level lists and grid barriers
+  uint32_t no_direct;
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins

@@ -630,6 +630,11 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
   u.force_abort = t->force_abort ? 1u : 0u;
+  static const bool lists_only = [] {
+    const char* e = getenv("SHM_UPPER_LISTS");
+    return e && e[0] == '1';
+  }();
+  u.no_direct = lists_only ? 1u : 0u;
   t->force_abort = false;
   dev::launch_upper(u, s);
   DBG(s, "upper");
