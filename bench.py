@@ -287,6 +287,12 @@ def main():
                 pend[c + 1] = routes[(c + 1) % nstr].search_begin(qs[(c + 1) % N_BATCHES])
             with on(c):
                 routes[c % nstr].search_end(pend.pop(c), v, f)
+
+        def done_streams(i):
+            # where step i's batch completes (N > 1: every stream, the latest)
+            if routes[0] is None:
+                return [streams[i % nstr] or torch.cuda.current_stream()]
+            return [sx or torch.cuda.current_stream() for sx in streams]
     elif args.workload == "c5":
         from sherman_amd import PendingRange
         from sherman_amd.shard import umin
@@ -298,7 +304,7 @@ def main():
         # pair, warmup, timed, latency and profile steps): a batch applied a
         # second time would find its new keys already stored and turn their
         # inserts into updates, leaving the timed steps with few splits
-        n_c5 = 2 + args.warmup + args.steps + args.profile_steps + (
+        n_c5 = 2 + args.warmup + args.steps + args.profile_steps + 2 * (
             args.latency_steps if args.latency_steps is not None else args.steps)
         mixed = []
         for b in range(n_c5):
@@ -348,6 +354,12 @@ def main():
             else:
                 scan_out["r"] = PendingRange(None, *route.range_query(lo, hi, n_cap))
                 route.insert(pk, pv)
+
+        def done_streams(i):
+            # the library orders the inserts after the scans: the insert stream
+            # completes the step
+            return [s_ins if (route is None and args.async_scans and s_ins is not None)
+                    else torch.cuda.current_stream()]
     else:
         zipf = Zipf(n_keys, args.theta, dev)
         mixed, c3_ids = [], []
@@ -369,6 +381,9 @@ def main():
             # insert is checked after the timed steps)
             gk, pk, pv = mixed[i % N_BATCHES]
             tree.mixed_batch(gk, vals[:gk.numel()], found[:gk.numel()], pk, pv)
+
+        def done_streams(i):
+            return [torch.cuda.current_stream()]
 
     # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
     cpu = parity = None
@@ -448,6 +463,11 @@ def main():
     else:
         one = step
     lat = latency_pass(one, args, dist)
+    # per-op latency under load: the timed steps' pipelining, 100 ns buckets
+    # (test/benchmark.cpp:207-249)
+    depth = (len(outs) if args.workload == "c2" else
+             2 if args.workload == "c5" and world == 1 and args.streams == 2 else 1)
+    op_lat = op_latency_pass(step, done_streams, batch, depth, args, dist)
     if dist is not None:
         lt = torch.tensor(lat, dtype=torch.float64, device=dev)
         dist.all_reduce(lt, op=dist.ReduceOp.MAX)
@@ -583,6 +603,7 @@ def main():
             "parity_vs_oracle": parity,
             "batch_latency_us": dict(zip(("p50", "p90", "p95", "p99", "p99.9", "max"),
                                          [round(x, 1) for x in lat])),
+            "op_latency_us": op_lat,
             "cluster_sum_mops": round(cluster_sum, 2),
         }
         if idx is not None:
@@ -745,6 +766,74 @@ def latency_pass(one, args, dist):
         us.append((time.perf_counter() - t0) * 1e6)
     us = np.array(us)
     return [float(np.percentile(us, q)) for q in (50, 90, 95, 99, 99.9)] + [float(us.max())]
+
+
+LATENCY_BUCKET_US = 0.1  # test/benchmark.cpp: latency[thread][i], i = 100 ns windows
+
+
+def op_latency_pass(step, done_streams, batch, depth, args, dist):
+    """Per-op latency histogram under the timed condition (test/benchmark.cpp:
+    207-249 records each op's latency in 100 ns windows and prints p50 / p90 /
+    p95 / p99 / p99.9 from the cumulative counts).  The steps run pipelined
+    as in the timed region, closed-loop with `depth` batches in flight (a
+    batch is issued once the batch `depth` before it has completed, as each
+    of the reference's client threads issues its next op after the last
+    one returns; an open loop would only measure the queue the host
+    builds); an op's latency is its batch's completion (a HIP
+    event on the stream that finishes the step, on the device clock) minus
+    the host time its step was issued (both relative to one idle-device
+    origin).  Every op of a batch shares it, so each batch adds `batch` ops
+    to its window.  Max over ranks at N > 1 (per percentile)."""
+    import numpy as np
+    import torch
+    n = args.latency_steps if args.latency_steps is not None else args.steps
+    if n <= 0:
+        return None
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    e0.synchronize()
+    t0 = time.perf_counter()
+    issue, done = [], []
+    for i in range(n):
+        if i >= depth:
+            # closed loop, as the reference's client threads: at most `depth`
+            # batches in flight (the timed steps' streams), the next one
+            # issued once the oldest completes
+            for e in done[i - depth]:
+                e.synchronize()
+        issue.append((time.perf_counter() - t0) * 1e6)
+        step(i)
+        evs = []
+        for sx in done_streams(i):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(sx)
+            evs.append(e)
+        done.append(evs)
+    torch.cuda.synchronize()
+    lat = np.array([max(e0.elapsed_time(e) for e in evs) * 1e3 - t for evs, t in zip(done, issue)])
+    lat = np.maximum(lat, 0.0)
+    win = np.floor(lat / LATENCY_BUCKET_US).astype(np.int64)
+    hist = np.bincount(win) * batch  # ops per 100 ns window
+    cum = np.cumsum(hist)
+    tot = int(cum[-1])
+    pct = []
+    for num, den in ((1, 2), (9, 10), (95, 100), (99, 100), (999, 1000)):
+        th = tot * num // den
+        pct.append(float(np.searchsorted(cum, th) * LATENCY_BUCKET_US))
+    pct.append(float(win.max() * LATENCY_BUCKET_US))
+    if dist is not None:
+        lt = torch.tensor(pct, dtype=torch.float64, device="cuda")
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        pct = lt.tolist()
+    out = dict(zip(("p50", "p90", "p95", "p99", "p99.9", "max"), [round(x, 1) for x in pct]))
+    out.update({"bucket_us": LATENCY_BUCKET_US, "ops": tot, "in_flight": depth,
+                "condition": "the timed steps' pipelining, closed loop with in_flight batches "
+                             "queued; op latency = batch completion (device event) - step issue "
+                             "(host)"})
+    return out
 
 
 def _oracle_on_gpu_image(tree, spare_bytes=0):

@@ -82,6 +82,60 @@ __global__ __launch_bounds__(256) void k_mix(const uint4* buf, uint64_t n, uint6
   if (acc == 0x12345678u) atomicAdd(sink, 1u);
 }
 
+// k_mix with G independent gets' worth of requests per lane (3 G in flight)
+template <int G>
+__global__ __launch_bounds__(256) void k_mixg(const uint4* buf, uint64_t n, uint64_t salt,
+                                              uint32_t* sink) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t dl = (64ull << 20) / 128, sl = (128ull << 20) / 128, el = (2ull << 30) / 128;
+  const uint4* dir = buf;
+  const uint4* sum = buf + (64ull << 20) / 16;
+  const uint4* ent = buf + (192ull << 20) / 16;
+  uint4 a[G], b[G][4], c[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint64_t j = i * G + g;
+    a[g] = dir[(mix(j * 3 ^ salt) % dl) * 8];
+    const uint64_t sline = mix(j * 3 + 1 ^ salt) % sl;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) b[g][w] = sum[sline * 8 + w];
+    c[g] = ent[(mix(j * 3 + 2 ^ salt) % el) * 8];
+  }
+  uint32_t acc = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) acc ^= a[g].x ^ b[g][0].y ^ b[g][1].z ^ b[g][2].w ^ b[g][3].x ^ c[g].y;
+  if (acc == 0x12345678u) atomicAdd(sink, 1u);
+}
+
+// the walk's dependent chain: directory entry -> summary line -> entry, each
+// address derived from the previous load's data (the buffer holds a hash
+// pattern, so the chain stays random), one chain per lane
+__global__ __launch_bounds__(256) void k_chain(const uint4* buf, uint64_t n, uint64_t salt,
+                                               uint32_t* sink) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t dl = (64ull << 20) / 128, sl = (128ull << 20) / 128, el = (2ull << 30) / 128;
+  const uint4* dir = buf;
+  const uint4* sum = buf + (64ull << 20) / 16;
+  const uint4* ent = buf + (192ull << 20) / 16;
+  const uint4 a = dir[(mix(i ^ salt) % dl) * 8];
+  const uint64_t sline = mix(i ^ ((uint64_t)a.x << 32) ^ a.y) % sl;
+  const uint4 b0 = sum[sline * 8], b1 = sum[sline * 8 + 1], b2 = sum[sline * 8 + 2],
+              b3 = sum[sline * 8 + 3];
+  const uint64_t eline = mix(i ^ ((uint64_t)(b0.x ^ b3.w) << 32) ^ b1.y ^ b2.z) % el;
+  const uint4 c = ent[eline * 8];
+  if ((c.x ^ c.y) == 0x12345678u) atomicAdd(sink, 1u);
+}
+
+__global__ void k_fill_hash(uint4* buf, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = mix(i);
+    buf[i] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(h * 3), (uint32_t)(h >> 7));
+  }
+}
+
 template <class F>
 void timed(const char* name, double reads, int bytes, uint64_t buffer, F launch) {
   hipEvent_t a, b;
@@ -136,5 +190,17 @@ int main() {
   const dim3 g((unsigned)((n + 255) / 256));
   timed("k_mix dir64M+sum128M(64B)+ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
         [&](uint64_t salt) { k_mix<<<g, 256>>>(buf, n, salt, sink); });
+  const dim3 g2((unsigned)((n / 2 + 255) / 256)), g4((unsigned)((n / 4 + 255) / 256));
+  timed("k_mixg<2> dir64M+sum128M(64B)+ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
+        [&](uint64_t salt) { k_mixg<2><<<g2, 256>>>(buf, n / 2, salt, sink); });
+  timed("k_mixg<4> dir64M+sum128M(64B)+ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
+        [&](uint64_t salt) { k_mixg<4><<<g4, 256>>>(buf, n / 4, salt, sink); });
+  // the dependent chain reads hash data: fill the walk's regions first
+  k_fill_hash<<<4096, 256>>>(buf, ((2ull << 30) + (192ull << 20)) / 16);
+  CK(hipDeviceSynchronize());
+  timed("k_chain dir64M->sum128M(64B)->ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
+        [&](uint64_t salt) { k_chain<<<g, 256>>>(buf, n, salt, sink); });
+  timed("k_chain 1Mi lanes", (double)ns * 3, 0, (2ull << 30) + (192ull << 20),
+        [&](uint64_t salt) { k_chain<<<dim3((unsigned)((ns + 255) / 256)), 256>>>(buf, ns, salt, sink); });
   return 0;
 }
