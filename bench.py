@@ -83,6 +83,14 @@ def parse():
                    help="on: order get batches by key and walk whole pages "
                         "(SHM_FLAG_SORT_GETS, k_get); auto / off: the leaf-summary walk "
                         "(k_get_sum, default)")
+    p.add_argument("--scan-out", choices=("slots", "compact"), default="slots",
+                   help="c5, N=1: slots = a buffer of --slot-cap values per scan "
+                        "(shm_range_query_slots, the reference's per-call buffer, one "
+                        "pass); compact = values packed in scan order "
+                        "(shm_range_query_batch_async: count, scan, fill)")
+    p.add_argument("--slot-cap", type=int, default=256,
+                   help="c5 slotted scans: values per scan buffer (every timed step is "
+                        "checked to have no scan past it)")
     p.add_argument("--sync-scans", dest="async_scans", action="store_false",
                    help="c5, N=1: range scans read their total back before the "
                         "batch's inserts are queued (default: async, checked after)")
@@ -337,10 +345,26 @@ def main():
             s_scan.wait_stream(torch.cuda.current_stream())
             s_ins.wait_stream(torch.cuda.current_stream())
 
+        slots = route is None and args.async_scans and args.scan_out == "slots"
+        if slots:
+            # two per-scan buffers, alternating (a step's scans never overwrite
+            # the previous step's results); ordered on the scans' stream
+            sbuf = [(torch.empty((n_cap, args.slot_cap), dtype=torch.int64, device=dev),
+                     torch.empty(n_cap, dtype=torch.int64, device=dev)) for _ in range(2)]
+
         def step(i):
             lo, hi, pk, pv = mixed[applied[0] % n_c5]
             applied[0] += 1
-            if route is None and args.async_scans:
+            if slots:
+                # one pass: each scan's values into its own buffer; every
+                # step's (scans past the slot, error bits) is checked after the run
+                sv, sc = sbuf[applied[0] % 2]
+                pr = tree.range_query_slots(lo, hi, args.slot_cap, stream=s_scan, vals=sv,
+                                            counts=sc)
+                scan_out["r"] = SlotsResult(pr)
+                scan_out.setdefault("slots", []).append(pr.status)
+                tree.insert_batch_async(pk, pv, stream=s_ins)
+            elif route is None and args.async_scans:
                 # scans queued without a host wait; the batch's inserts queue
                 # behind them (their ordering beside them, on their own
                 # stream); every step's total is checked after the run
@@ -441,6 +465,10 @@ def main():
             total, err = (int(x) for x in tot.cpu().tolist())
             # every timed step's values fit its buffer, with no device error
             assert err == 0 and total <= cap, (total, cap, err)
+        for status in scan_out.pop("slots", []):
+            ovf, err = (int(x) for x in status.cpu().tolist())
+            # no scan of any step passed its slot, no device error
+            assert err == 0 and ovf == 0, (ovf, err)
         c, _ = scan_out["r"].result()
         hit_rate = float(c.float().mean().item())  # mean values per scan
     else:
@@ -634,6 +662,9 @@ def main():
             ach = ins_per_launch * ALG_BYTES_PER_INSERT / (ins_ms * 1e-3) / 1e9 if ins_ms else 0.0
             out["config"]["hit_rate"] = None
             out["config"]["values_per_scan"] = round(hit_rate, 2)
+            out["config"]["scan_out"] = (("slots of %d values" % args.slot_cap)
+                                         if world == 1 and args.async_scans and
+                                         args.scan_out == "slots" else "compact")
             out["roofline"].update({
                 "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
                 "kernel": "insert_batch chunk (ordering + locate + k_leaf_upsert + splits)",
@@ -647,6 +678,13 @@ def main():
                 "traffic": (_profile_traffic("pmc_insert.json", "hbm_bytes_per_chunk",
                                              batch, args.keys_log2)
                             if args.start == "dir" else None)})
+            rf = out["roofline"]
+            # the bytes the chunk really moves (PMC) over its measured time:
+            # the real-traffic fraction beside the survey's 1074 B per op
+            rf["traffic_GBps"] = (round(rf["traffic"] / (ins_ms * 1e-3) / 1e9, 1)
+                                  if rf["traffic"] and ins_ms else None)
+            rf["traffic_frac"] = (round(rf["traffic_GBps"] / HBM_PEAK_GBS, 4)
+                                  if rf["traffic_GBps"] else None)
         if args.workload == "c3":
             # whole-step algorithmic rate (gets as walked, inserts 1074 B per op)
             step_s = elapsed / args.steps
@@ -766,6 +804,17 @@ def latency_pass(one, args, dist):
         us.append((time.perf_counter() - t0) * 1e6)
     us = np.array(us)
     return [float(np.percentile(us, q)) for q in (50, 90, 95, 99, 99.9)] + [float(us.max())]
+
+
+class SlotsResult:
+    """A slotted scan batch read in the compact form (counts, values in scan
+    order), as the parity legs compare it."""
+
+    def __init__(self, pend):
+        self.pend = pend
+
+    def result(self):
+        return self.pend.packed()
 
 
 LATENCY_BUCKET_US = 0.1  # test/benchmark.cpp: latency[thread][i], i = 100 ns windows

@@ -179,6 +179,19 @@ int shm_range_query_batch_async(shm_tree *t, const uint64_t *from, const uint64_
                                 uint64_t n, uint64_t *counts_out, uint64_t *offsets_out,
                                 uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_dev,
                                 void *stream);
+/* Tree::range_query(from, to, Value *buffer) for a batch, each scan with a
+ * buffer of its own, as the reference's caller passes one per call
+ * (src/Tree.cpp:461-540, include/Tree.h:53): scan i's values, in leaf then
+ * slot order, go to vals_out[i * slot_cap ...] (at most slot_cap of them) and
+ * counts_out[i] = its number of matches (the reference's return value; more
+ * than slot_cap means the buffer was too small and holds the first
+ * slot_cap).  One pass over the leaves, no host synchronisation, any n.
+ * status_dev (device, 2 words, nullable) receives {scans whose count passed
+ * slot_cap, this call's device error bits} when the call completes on
+ * `stream`. */
+int shm_range_query_slots(shm_tree *t, const uint64_t *from, const uint64_t *to,
+                          uint64_t n, uint64_t slot_cap, uint64_t *counts_out,
+                          uint64_t *vals_out, uint64_t *status_dev, void *stream);
 
 /* introspection / images (host pointers) ------------------------------------- */
 int shm_stats(shm_tree *t, shm_stats_t *out);

@@ -119,6 +119,7 @@ _SIGNATURES = [
      [vp, vp, vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
     ("shm_range_query_batch_async", ctypes.c_int,
      [vp, vp, vp, u64, vp, vp, vp, u64, vp, vp]),
+    ("shm_range_query_slots", ctypes.c_int, [vp, vp, vp, u64, u64, vp, vp, vp, vp]),
     ("shm_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmStats)]),
     ("shm_dump_image", ctypes.c_int, [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_load_image", ctypes.c_int, [vp, vp, u64, u64]),
@@ -244,6 +245,44 @@ class PendingRange:
         return self.counts, self.vals
 
 
+class PendingSlots:
+    """Result of Tree.range_query_slots: (counts, vals[n, slot_cap]) once the
+    scans have run; .result() raises SHM_EIO on a device error and
+    SHM_ENOSPC when some scan's count passed slot_cap (its buffer then holds
+    its first slot_cap values)."""
+
+    def __init__(self, tree, counts, vals, slot_cap, status, done):
+        self.tree, self.counts, self.slot_cap = tree, counts, slot_cap
+        self.vals = vals.view(-1)[:counts.numel() * slot_cap].view(counts.numel(), slot_cap)
+        self.status, self.done = status, done
+
+    def check(self):
+        """(scans over slot_cap, error bits) once the scans have run."""
+        if self.done is not None:
+            self.done.synchronize()
+        ovf, err = (int(x) for x in self.status.cpu().tolist())
+        return ovf, err
+
+    def result(self):
+        ovf, err = self.check()
+        if err:
+            self.tree.synchronize()  # raises the device error
+            raise ShermanError(SHM_EIO, "range_query_slots")
+        if ovf:
+            raise ShermanError(SHM_ENOSPC, "range_query_slots: %d scans passed slot_cap %d"
+                               % (ovf, self.slot_cap))
+        return self.counts, self.vals
+
+    def packed(self):
+        """(counts, values concatenated in scan order): the compact form."""
+        import torch
+        c, v = self.result()
+        if c.numel() == 0:
+            return c, v.view(-1)[:0]
+        mask = torch.arange(self.slot_cap, device=c.device)[None, :] < c[:, None]
+        return c, v[mask]
+
+
 class Tree:
     """One shard's B+tree in HBM (reference: class Tree, include/Tree.h:42)."""
 
@@ -363,6 +402,30 @@ class Tree:
                                                  _ptr(offs), _ptr(vals), cap, _ptr(tot), sp),
                "range_query_batch_async")
         return PendingRange(self, counts, vals, tot, _record_on(sp, dev))
+
+    def range_query_slots(self, lo, hi, slot_cap, stream=None, vals=None, counts=None,
+                          status=None):
+        """Batched scans with a buffer per scan (shm_range_query_slots, the
+        reference's Tree::range_query(from, to, buffer) per scan): queued on
+        `stream` without a host wait.  Returns PendingSlots: .result() gives
+        (counts, vals[n, slot_cap]); scan i's first min(counts[i], slot_cap)
+        values are vals[i, :counts[i]].  vals / counts / status may be passed
+        in (reused buffers)."""
+        import torch
+        n = lo.numel()
+        dev = lo.device
+        if counts is None:
+            counts = torch.empty(n, dtype=torch.int64, device=dev)
+        if vals is None:
+            vals = torch.empty((n, slot_cap), dtype=torch.int64, device=dev)
+        if status is None:
+            status = torch.empty(2, dtype=torch.int64, device=dev)
+        assert vals.numel() >= n * slot_cap and counts.numel() >= n
+        sp = _stream_ptr(stream)
+        _check(lib().shm_range_query_slots(self.h, _ptr(lo), _ptr(hi), n, slot_cap, _ptr(counts),
+                                           _ptr(vals), _ptr(status), sp),
+               "range_query_slots")
+        return PendingSlots(self, counts[:n], vals, slot_cap, status, _record_on(sp, dev))
 
     # -- reference single-op API (Tree.h:47-54) -------------------------------
     def _dev(self, name, n):

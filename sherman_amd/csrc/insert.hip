@@ -266,6 +266,15 @@ __device__ __forceinline__ void write_new_root(const UpperArgs& a, WaveLds& L, u
   if (lane_id() == 0) clear_leaf_sum(a.sum, ga_offset(a.root));
 }
 
+// The directory's page of `level` (1 or 2) on the path of k's prefix
+// (k_leaf_dir records them), 0 when there is none: a B-link starting point
+__device__ __forceinline__ uint64_t dir_hint_page(const UpperArgs& a, uint64_t k, uint32_t level) {
+  if (!a.dir_hint || level < 1 || level > 2 || !dir_covers(a.dir_lo, a.dir_shift, a.dir_n, k))
+    return 0;
+  const uint32_t pg = a.dir_hint[(uint64_t)(level - 1) * a.dir_n + ((k - a.dir_lo) >> a.dir_shift)];
+  return pg ? dir_page_ga(pg, a.node) : 0ull;
+}
+
 // The page of `level` whose fences hold k: header walk from the root with
 // page_search's sibling rule (Tree.cpp:593-663) and internal_page_search
 // (665-685), one wave.  0 on an inconsistency (error bits in *err).
@@ -683,9 +692,11 @@ __device__ __forceinline__ bool lock_excl(const UpperArgs& a, uint64_t page) {
     unsigned long long* wd =
         reinterpret_cast<unsigned long long*>(a.locks) + lock_index(page, a.num_locks);
     const unsigned long long mine = (unsigned long long)(a.tag | 1ull);
+    // one round trip: max(word, tag | 1) returns a free value (<= tag: an
+    // earlier chunk's, or this chunk's shared / handed-back hold) exactly
+    // when this wave took it; tag | 1 back means another wave holds it
     for (uint32_t spin = 0; spin < kMaxLockSpins; ++spin) {
-      const unsigned long long cur = __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur <= (unsigned long long)a.tag && atomicCAS(wd, cur, mine) == cur) {
+      if (atomicMax(wd, mine) <= (unsigned long long)a.tag) {
         got = 1;
         break;
       }
@@ -825,7 +836,7 @@ __device__ __forceinline__ uint32_t apply_run(const UpperArgs& a, WaveLds& L, co
 // A run of <= kSmallSplit - 1 separators splits each page it touches at most
 // once, so every level's run stays that short (the 64-entry LDS bound).
 __device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32_t n, uint32_t level,
-                          uint64_t base, uint64_t cap, uint32_t& err) {
+                          uint64_t base, uint64_t cap, uint32_t& err, uint64_t hint1 = 0) {
   for (; n; ++level) {
     if (level > (uint32_t)kMaxLevelOfTree) {
       err |= kErrRounds;
@@ -838,9 +849,12 @@ __device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32
       L.o_val[lane] = L.r_ptr[lane];
     }
     wave_lds_sync();
-    // the parent: a header walk from the root (a hint; apply_run re-checks
-    // it under the word and moves right or relocates)
-    const uint64_t hint = parent_of(a, L.o_key[0], level, &err, true);
+    // the parent: level 1 starts straight at the directory's level-1 page
+    // for the run's prefix (read before the leaf builds); otherwise a header
+    // walk.  Either is a hint: apply_run re-checks it under the word and
+    // moves right or relocates
+    const uint64_t hint =
+        level == 1 && hint1 ? hint1 : parent_of(a, L.o_key[0], level, &err, true);
     n = apply_run(a, L, L.o_key, L.o_val, 0, n, hint, level, base, cap, err, true);
   }
 }
@@ -1090,6 +1104,8 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       stage_page(L.page, w);
       wave_lds_sync();
       const Ops o = stage_ops(L, o0);
+      // the level-1 parent's directory hint, in flight during the builds
+      const uint64_t hint1 = direct ? dir_hint_page(a, o.key[o.st], 1) : 0ull;
       const int na = leaf_survivors(L, o);
       if (small) {
         for (int p = 1; p < P; ++p) {
@@ -1114,7 +1130,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       const uint64_t dest = grow0 ? ga_make(a.node, xroot * kPageSize) : page;
       (void)build_leaf_page(a, L, h, na, o, SplitPage{0, P, a.seg_T[g], first + pb, dest});
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
-      if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err);
+      if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err, grow0 ? 0ull : hint1);
     }
     if (grow0) root_level = 1;
     stamp();

@@ -406,6 +406,9 @@ struct RangeArgs {
   // per-page occupancy bound (nullable, layout.h): a sibling leaf's bytes
   // past its last possibly valid slot are not read
   const uint8_t* leaf_hw;
+  // slotted scans (shm_range_query_slots, nullable): {scans whose count
+  // passed stage_cap, this launch's error bits}, zeroed before the launch
+  uint64_t* status;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // x[i] += c for i < n

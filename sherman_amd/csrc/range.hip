@@ -282,8 +282,15 @@ __global__ __launch_bounds__(kRangeWaves* kWave) void k_range(RangeArgs a) {
     cap = out < a.vals_cap ? a.vals_cap - out : 0;
   }
   const uint64_t cnt = range_walk(a, act, lo, hi, lp, li, dst, cap, nullptr, 0, err);
-  if (has && !copied && li == 0) a.counts[Q] = cnt;
-  if (err) atomicOr(a.err, err);
+  if (has && !copied && li == 0) {
+    a.counts[Q] = cnt;
+    if (a.status && cnt > a.stage_cap)
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.status), 1ull);
+  }
+  if (err) {
+    atomicOr(a.err, err);
+    if (a.status) atomicOr(reinterpret_cast<unsigned long long*>(a.status + 1), (unsigned long long)err);
+  }
 }
 
 void launch_range(const RangeArgs& a, hipStream_t s) {

@@ -1347,6 +1347,28 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   return range_launch(t, s, a);
 }
 
+// one pass: the count walk with the caller's per-scan buffers as its staging
+int shm_range_query_slots(shm_tree* t, const uint64_t* from, const uint64_t* to, uint64_t n,
+                          uint64_t slot_cap, uint64_t* counts_out, uint64_t* vals_out,
+                          uint64_t* status_dev, void* stream) {
+  if (!t || (n && (!from || !to || !counts_out)) || slot_cap >= (1ull << 32))
+    return SHM_EINVAL;
+  if (slot_cap && n && !vals_out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  hipStream_t s = pick(stream);
+  Order ord(t, s, true);  // the directory refresh
+  if (ord.rc) return ord.rc;
+  if (status_dev) HIP_OK(hipMemsetAsync(status_dev, 0, 2 * sizeof(uint64_t), s));
+  if (n == 0) return SHM_OK;
+  if (const int rc = range_prepare(t, s)) return rc;
+  dev::RangeArgs a = range_args(t, from, to, n, counts_out, nullptr, nullptr);
+  a.stage = slot_cap ? vals_out : nullptr;
+  a.stage_cap = (uint32_t)slot_cap;
+  a.status = status_dev;
+  t->err_pending = true;
+  return range_launch(t, s, a);
+}
+
 // Library-internal, not part of include/sherman_amd.h (shard.cpp): a routed
 // insert's received slots, kKeyMax padding skipped, queued as
 // shm_insert_batch_async (n <= max_batch: one chunk)

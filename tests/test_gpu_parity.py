@@ -318,6 +318,65 @@ def test_range_query_vs_oracle(lib_ok, max_batch, cap, leaf_dir):
     t.close()
 
 
+def test_range_query_slots_vs_oracle(lib_ok):
+    """shm_range_query_slots (a buffer per scan, Tree::range_query(from, to,
+    buffer) batched): every scan's count and its values in the reference's
+    leaf / slot order over the same pages, against the oracle's contents;
+    scans longer than slot_cap keep their first slot_cap values, report the
+    full count and are counted in the status; more scans than max_batch in
+    one call; an empty batch; the buffers past each scan's values untouched."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 10)
+    orc = OracleTree(256 << 20)
+    ks = hashed_keys(1, 50001)
+    gpu_insert(t, ks, ks + U64(9))
+    orc.apply_batch(ks, ks + U64(9))
+    rng = np.random.default_rng(29)
+    n = 3000  # > max_batch: any n in one call
+    lo = rng.integers(0, 1 << 63, n, dtype=np.uint64) * U64(2)
+    span = (U64(1) << U64(50)) * rng.integers(0, 64, n).astype(U64)
+    span[::101] = U64(1) << U64(58)  # ~780 keys: past the slot
+    hi = lo + span
+    hi[hi < lo] = U64((1 << 64) - 1)
+    lo[1], hi[1] = U64(5), U64(4)  # empty (from > to)
+    lo[2], hi[2] = U64(0), U64((1 << 64) - 1)  # whole key space
+    cap = 200
+    vals = torch.full((n, cap), 0x5A5A, dtype=torch.int64, device="cuda")
+    pend = t.range_query_slots(dev(lo), dev(hi), cap, vals=vals)
+    ovf, err = pend.check()
+    assert err == 0
+    counts = pend.counts.cpu().numpy()
+    hv = vals.cpu().numpy().view(np.uint64)
+    img, root = t.dump_image()
+    same_pages = OracleTree(image=img, root_ptr=root)
+    n_over = 0
+    for i in range(n):
+        ref, c = orc.range_query(int(lo[i]), int(hi[i]), cap=60000)
+        assert counts[i] == c, i
+        m = min(c, cap)
+        ref_img, c_img = same_pages.range_query(int(lo[i]), int(hi[i]), cap=60000)
+        assert c_img == c and np.array_equal(hv[i, :m], ref_img[:m]), i
+        if c <= cap:
+            assert np.array_equal(np.sort(hv[i, :m]), np.sort(ref)), i
+        assert (hv[i, m:] == U64(0x5A5A)).all(), i  # nothing past the scan's values
+        n_over += c > cap
+    assert n_over >= 20 and ovf == n_over and counts[2] == ks.size and counts[1] == 0
+    with pytest.raises(shm.ShermanError):
+        pend.result()  # SHM_ENOSPC: some scans passed the slot
+    # the compact form of a batch that fits
+    sel = counts <= cap
+    p2 = t.range_query_slots(dev(lo[sel]), dev(hi[sel]), cap)
+    c2, v2 = p2.packed()
+    sc, sv = t.range_query_batch(dev(lo[sel]), dev(hi[sel]))
+    assert np.array_equal(c2.cpu().numpy(), sc.cpu().numpy())
+    assert np.array_equal(host(v2), host(sv))
+    # an empty batch still clears the status
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    c0, v0 = t.range_query_slots(e, e, cap).result()
+    assert c0.numel() == 0
+    t.check()
+    t.close()
+
+
 def test_range_query_async_matches_sync_and_reports_overflow(lib_ok):
     """shm_range_query_batch_async: the scans queued before an insert see the
     pre-insert tree and equal the synchronous call's (counts and values in the

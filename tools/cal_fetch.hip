@@ -187,6 +187,10 @@ int main() {
   run<4, 16, 1>(buf, small / 128, n, sink, "k_rand<4,16,1> 64MiB 16B");
   run<1, 64, 1>(buf, small / 128, n, sink, "k_rand<1,64,1> 64MiB 64B");
   run<3, 16, 2>(buf, big / 128, ns, sink, "k_rand<3,16,2> 16GiB 16B short");
+  // more reads in flight per lane, and an Infinity-Cache-sized region
+  run<8, 16, 1>(buf, small / 128, n, sink, "k_rand<8,16,1> 64MiB 16B");
+  run<4, 16, 3>(buf, (192ull << 20) / 128, n, sink, "k_rand<4,16,3> 192MiB 16B");
+  run<4, 16, 4>(buf, (2ull << 30) / 128, n, sink, "k_rand<4,16,4> 2GiB 16B");
   const dim3 g((unsigned)((n + 255) / 256));
   timed("k_mix dir64M+sum128M(64B)+ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
         [&](uint64_t salt) { k_mix<<<g, 256>>>(buf, n, salt, sink); });
