@@ -88,6 +88,12 @@ def parse():
                         "(shm_range_query_slots, the reference's per-call buffer, one "
                         "pass); compact = values packed in scan order "
                         "(shm_range_query_batch_async: count, scan, fill)")
+    p.add_argument("--pipeline", type=int, default=0, choices=(0, 1),
+                   help="c3 / c5 (N=1; c5 with slotted scans on 2 streams): 1 = each "
+                        "batch's insert ordering is queued one step ahead on its own "
+                        "stream (shm_insert_order), so it runs beside the previous "
+                        "batch's gets / scans and tree changes (shm_insert_apply); 0 = "
+                        "shm_mixed_batch (c3) / shm_insert_batch_async (c5)")
     p.add_argument("--slot-cap", type=int, default=256,
                    help="c5 slotted scans: values per scan buffer (every timed step is "
                         "checked to have no scan past it)")
@@ -351,18 +357,41 @@ def main():
             # the previous step's results); ordered on the scans' stream
             sbuf = [(torch.empty((n_cap, args.slot_cap), dtype=torch.int64, device=dev),
                      torch.empty(n_cap, dtype=torch.int64, device=dev)) for _ in range(2)]
+            # {scans past the slot, error bits} of every step, accumulated on
+            # the device (zeroed here, checked after the timed steps)
+            slot_status = torch.zeros(2, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+
+        pipe = slots and args.pipeline and s_ins is not None
+        ticket = [None]  # the ordered, not yet applied batch (pipeline)
+        if pipe:
+            # scans and tree changes on one stream (s_scan), the orderings on
+            # their own (s_ins): batch i + 1 is ordered while batch i applies
+            s_main, s_ord = s_scan or torch.cuda.current_stream(), s_ins
 
         def step(i):
             lo, hi, pk, pv = mixed[applied[0] % n_c5]
             applied[0] += 1
-            if slots:
+            if pipe:
+                if ticket[0] is None:  # the first batch of the run
+                    ticket[0] = tree.insert_order(pk, pv, stream=s_ord)
+                sv, sc = sbuf[applied[0] % 2]
+                pr = tree.range_query_slots(lo, hi, args.slot_cap, stream=s_main, vals=sv,
+                                            counts=sc, status=slot_status)
+                scan_out["r"] = SlotsResult(pr)
+                scan_out["slots"] = slot_status
+                _, _, nk, nv = mixed[applied[0] % n_c5]  # the next step's batch
+                nxt = tree.insert_order(nk, nv, stream=s_ord)
+                tree.insert_apply(ticket[0], stream=s_main)
+                ticket[0] = nxt
+            elif slots:
                 # one pass: each scan's values into its own buffer; every
                 # step's (scans past the slot, error bits) is checked after the run
                 sv, sc = sbuf[applied[0] % 2]
                 pr = tree.range_query_slots(lo, hi, args.slot_cap, stream=s_scan, vals=sv,
-                                            counts=sc)
+                                            counts=sc, status=slot_status)
                 scan_out["r"] = SlotsResult(pr)
-                scan_out.setdefault("slots", []).append(pr.status)
+                scan_out["slots"] = slot_status
                 tree.insert_batch_async(pk, pv, stream=s_ins)
             elif route is None and args.async_scans:
                 # scans queued without a host wait; the batch's inserts queue
@@ -381,7 +410,9 @@ def main():
 
         def done_streams(i):
             # the library orders the inserts after the scans: the insert stream
-            # completes the step
+            # (pipeline: the scans' stream, which applies) completes the step
+            if pipe:
+                return [s_main]
             return [s_ins if (route is None and args.async_scans and s_ins is not None)
                     else torch.cuda.current_stream()]
     else:
@@ -399,15 +430,36 @@ def main():
                 c3_ids.append(ids[is_get].contiguous())
         del keys_local
 
+        c3_pipe = args.pipeline and world == 1
+        c3n = [0]  # batches issued so far (all step loops; the pipeline's order)
+        c3_ticket = [None]
+        if c3_pipe:
+            # gets and tree changes on one stream, the orderings on their own:
+            # batch i + 1 is ordered while batch i's gets and inserts run
+            c3_main, c3_ord = torch.cuda.Stream(), torch.cuda.Stream()
+            c3_main.wait_stream(torch.cuda.current_stream())
+            c3_ord.wait_stream(torch.cuda.current_stream())
+
         def step(i):
-            # one mixed batch (shm_mixed_batch): the gets see the state before
-            # its inserts; queued without a host wait (the status of every
-            # insert is checked after the timed steps)
-            gk, pk, pv = mixed[i % N_BATCHES]
-            tree.mixed_batch(gk, vals[:gk.numel()], found[:gk.numel()], pk, pv)
+            # one mixed batch: the gets see the state before its inserts;
+            # queued without a host wait (the status of every insert is
+            # checked after the timed steps)
+            if not c3_pipe:  # shm_mixed_batch
+                gk, pk, pv = mixed[i % N_BATCHES]
+                tree.mixed_batch(gk, vals[:gk.numel()], found[:gk.numel()], pk, pv)
+                return
+            gk, pk, pv = mixed[c3n[0] % N_BATCHES]
+            c3n[0] += 1
+            if c3_ticket[0] is None:
+                c3_ticket[0] = tree.insert_order(pk, pv, stream=c3_ord)
+            tree.search_batch(gk, vals[:gk.numel()], found[:gk.numel()], stream=c3_main)
+            _, nk, nv = mixed[c3n[0] % N_BATCHES]
+            nxt = tree.insert_order(nk, nv, stream=c3_ord)
+            tree.insert_apply(c3_ticket[0], stream=c3_main)
+            c3_ticket[0] = nxt
 
         def done_streams(i):
-            return [torch.cuda.current_stream()]
+            return [c3_main if c3_pipe else torch.cuda.current_stream()]
 
     # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
     cpu = parity = None
@@ -465,14 +517,15 @@ def main():
             total, err = (int(x) for x in tot.cpu().tolist())
             # every timed step's values fit its buffer, with no device error
             assert err == 0 and total <= cap, (total, cap, err)
-        for status in scan_out.pop("slots", []):
-            ovf, err = (int(x) for x in status.cpu().tolist())
-            # no scan of any step passed its slot, no device error
+        if "slots" in scan_out:
+            ovf, err = (int(x) for x in scan_out["slots"].cpu().tolist())
+            # no scan of any step so far passed its slot, no device error
             assert err == 0 and ovf == 0, (ovf, err)
         c, _ = scan_out["r"].result()
         hit_rate = float(c.float().mean().item())  # mean values per scan
     else:
-        n_get = mixed[(args.steps - 1) % N_BATCHES][0].numel()
+        last_b = (c3n[0] - 1) if c3_pipe else (args.steps - 1)  # the last step's batch
+        n_get = mixed[last_b % N_BATCHES][0].numel()
         hit_rate = float(found[:n_get].float().mean().item())
 
     # ---- per-batch latency (untimed pass): HIP events around each step on
@@ -662,6 +715,9 @@ def main():
             ach = ins_per_launch * ALG_BYTES_PER_INSERT / (ins_ms * 1e-3) / 1e9 if ins_ms else 0.0
             out["config"]["hit_rate"] = None
             out["config"]["values_per_scan"] = round(hit_rate, 2)
+            out["config"]["insert_pipeline"] = bool(world == 1 and args.async_scans and
+                                                    args.scan_out == "slots" and
+                                                    args.pipeline and args.streams == 2)
             out["config"]["scan_out"] = (("slots of %d values" % args.slot_cap)
                                          if world == 1 and args.async_scans and
                                          args.scan_out == "slots" else "compact")
@@ -690,6 +746,7 @@ def main():
             step_s = elapsed / args.steps
             b0 = mixed[0]
             alg = (b0[0].numel() * bpg + b0[1].numel() * ALG_BYTES_PER_INSERT)
+            out["config"]["insert_pipeline"] = bool(args.pipeline and world == 1)
             out["roofline"]["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
             out["roofline"]["step_frac"] = round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4)
         print(json.dumps(out), flush=True)

@@ -142,6 +142,21 @@ int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
  * handle (shm_synchronize, shm_insert_batch, shm_del_batch) as above. */
 int shm_insert_batch_async(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
                            uint64_t n, void *stream);
+/* shm_insert_batch_async of one chunk (n <= max_batch) split in two calls,
+ * so a caller can order the next batch while this one applies:
+ * shm_insert_order queues the batch's ordering (last writer per key, sorted,
+ * upserts / deletes split; it reads only keys / vals and touches no tree
+ * state) on `stream` and returns a ticket; shm_insert_apply queues the tree
+ * changes of that ticket (locate, leaf upserts, splits, parent levels,
+ * deletes) on its own stream, ordered like any insert (after every earlier
+ * call on the handle, before every later one).  At most two tickets are
+ * outstanding (SHM_EAGAIN), applied oldest first (else SHM_EINVAL); other
+ * insert calls are refused (SHM_EINVAL) while a ticket is outstanding.
+ * Errors are reported as for shm_insert_batch_async.  Tree::insert
+ * (src/Tree.cpp:353-403) for a batch, as shm_insert_batch_async. */
+int shm_insert_order(shm_tree *t, const uint64_t *keys, const uint64_t *vals, uint64_t n,
+                     void *stream, uint32_t *ticket);
+int shm_insert_apply(shm_tree *t, uint32_t ticket, void *stream);
 /* One mixed batch of gets and inserts (the reference benchmark's op stream,
  * test/benchmark.cpp:165-188, cut into batches): the gets see the tree as it
  * was before the batch's inserts, the inserts apply as shm_insert_batch_async
@@ -186,9 +201,10 @@ int shm_range_query_batch_async(shm_tree *t, const uint64_t *from, const uint64_
  * counts_out[i] = its number of matches (the reference's return value; more
  * than slot_cap means the buffer was too small and holds the first
  * slot_cap).  One pass over the leaves, no host synchronisation, any n.
- * status_dev (device, 2 words, nullable) receives {scans whose count passed
- * slot_cap, this call's device error bits} when the call completes on
- * `stream`. */
+ * status_dev (device, 2 words, nullable): the call ADDS the number of scans
+ * whose count passed slot_cap to status_dev[0] and ORs its device error bits
+ * into status_dev[1] when it completes on `stream` (the caller zeroes the
+ * pair; several batches may accumulate into one, checked once). */
 int shm_range_query_slots(shm_tree *t, const uint64_t *from, const uint64_t *to,
                           uint64_t n, uint64_t slot_cap, uint64_t *counts_out,
                           uint64_t *vals_out, uint64_t *status_dev, void *stream);

@@ -112,6 +112,8 @@ _SIGNATURES = [
     ("shm_search_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
     ("shm_insert_batch", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_insert_batch_async", ctypes.c_int, [vp, vp, vp, u64, vp]),
+    ("shm_insert_order", ctypes.c_int, [vp, vp, vp, u64, vp, ctypes.POINTER(u32)]),
+    ("shm_insert_apply", ctypes.c_int, [vp, u32, vp]),
     ("shm_mixed_batch", ctypes.c_int, [vp, vp, u64, vp, vp, vp, vp, u64, vp]),
     ("shm_del_batch", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_range_query", ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp, vp]),
@@ -247,7 +249,7 @@ class PendingRange:
 
 class PendingSlots:
     """Result of Tree.range_query_slots: (counts, vals[n, slot_cap]) once the
-    scans have run; .result() raises SHM_EIO on a device error and
+    scans have run; .result() raises the device error, if any, and
     SHM_ENOSPC when some scan's count passed slot_cap (its buffer then holds
     its first slot_cap values)."""
 
@@ -257,17 +259,14 @@ class PendingSlots:
         self.status, self.done = status, done
 
     def check(self):
-        """(scans over slot_cap, error bits) once the scans have run."""
+        """Scans over slot_cap once the scans have run (device errors raise)."""
         if self.done is not None:
             self.done.synchronize()
-        ovf, err = (int(x) for x in self.status.cpu().tolist())
-        return ovf, err
+        self.tree.synchronize()  # raises a device error of the queued calls
+        return int((self.counts > self.slot_cap).sum().item())
 
     def result(self):
-        ovf, err = self.check()
-        if err:
-            self.tree.synchronize()  # raises the device error
-            raise ShermanError(SHM_EIO, "range_query_slots")
+        ovf = self.check()
         if ovf:
             raise ShermanError(SHM_ENOSPC, "range_query_slots: %d scans passed slot_cap %d"
                                % (ovf, self.slot_cap))
@@ -344,6 +343,19 @@ class Tree:
         _check(lib().shm_insert_batch_async(self.h, _ptr(keys), _ptr(vals), keys.numel(),
                                             _stream_ptr(stream)), "insert_batch_async")
 
+    def insert_order(self, keys, vals, stream=None):
+        """shm_insert_order: queue one chunk's ordering (n <= max_batch) on
+        `stream`; returns the ticket for insert_apply.  keys / vals must stay
+        alive until the ordering has run."""
+        t = u32(0)
+        _check(lib().shm_insert_order(self.h, _ptr(keys), _ptr(vals), keys.numel(),
+                                      _stream_ptr(stream), ctypes.byref(t)), "insert_order")
+        return int(t.value)
+
+    def insert_apply(self, ticket, stream=None):
+        """shm_insert_apply: queue the tree changes of an ordered chunk."""
+        _check(lib().shm_insert_apply(self.h, ticket, _stream_ptr(stream)), "insert_apply")
+
     def mixed_batch(self, get_keys, vals_out, found_out, ins_keys, ins_vals, stream=None):
         """One mixed batch (shm_mixed_batch): the gets see the tree before the
         batch's inserts; the inserts are queued as insert_batch_async."""
@@ -409,8 +421,9 @@ class Tree:
         reference's Tree::range_query(from, to, buffer) per scan): queued on
         `stream` without a host wait.  Returns PendingSlots: .result() gives
         (counts, vals[n, slot_cap]); scan i's first min(counts[i], slot_cap)
-        values are vals[i, :counts[i]].  vals / counts / status may be passed
-        in (reused buffers)."""
+        values are vals[i, :counts[i]].  vals / counts may be passed in
+        (reused buffers); status (2 device words, zeroed by the caller)
+        accumulates {scans past slot_cap, error bits} over calls."""
         import torch
         n = lo.numel()
         dev = lo.device
@@ -418,8 +431,6 @@ class Tree:
             counts = torch.empty(n, dtype=torch.int64, device=dev)
         if vals is None:
             vals = torch.empty((n, slot_cap), dtype=torch.int64, device=dev)
-        if status is None:
-            status = torch.empty(2, dtype=torch.int64, device=dev)
         assert vals.numel() >= n * slot_cap and counts.numel() >= n
         sp = _stream_ptr(stream)
         _check(lib().shm_range_query_slots(self.h, _ptr(lo), _ptr(hi), n, slot_cap, _ptr(counts),

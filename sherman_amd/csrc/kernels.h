@@ -46,7 +46,7 @@ struct WalkArgs {
   // lock_tag) and records out_slot[i] = bit 31 | slot; any other op gets 0
   // and marks its leaf out_new[page] = out_new_tag (staged whole by the upsert)
   uint32_t* out_slot;
-  uint32_t* out_new;
+  uint8_t* out_new;      // byte marks: new_mark(out_new_tag)
   uint32_t out_new_tag;
   // nullable: set to out_new_tag when any op marked a page (a wave stores
   // it once): the segmentation skips a chunk of updates only
@@ -135,6 +135,14 @@ struct UpperCtl {
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
 constexpr uint32_t kSmallSplit = 4;
+
+// a chunk's byte mark in the per-page new-key array (tree.cpp pnew): 1..255,
+// repeating every 255 chunks (the host clears the array when it wraps).  One
+// byte per page keeps the array L2-sized (1.9 MB at C2's 1.9 M pages), so the
+// segmentation's per-run lookups hit L2
+__host__ __device__ __forceinline__ uint8_t new_mark(uint32_t tag) {
+  return (uint8_t)(tag % 255u + 1u);
+}
 
 // in-place leaf upserts (upsert.hip)
 struct SegArgs {
@@ -312,7 +320,7 @@ inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
 // gets a new key; otherwise there are no staged segments)
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag,
+                    uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
@@ -406,8 +414,8 @@ struct RangeArgs {
   // per-page occupancy bound (nullable, layout.h): a sibling leaf's bytes
   // past its last possibly valid slot are not read
   const uint8_t* leaf_hw;
-  // slotted scans (shm_range_query_slots, nullable): {scans whose count
-  // passed stage_cap, this launch's error bits}, zeroed before the launch
+  // slotted scans (shm_range_query_slots, nullable): += scans whose count
+  // passed stage_cap, |= this launch's error bits (the caller zeroes them)
   uint64_t* status;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);

@@ -84,7 +84,7 @@ struct shm_tree {
   // upsert staging verdicts: per op the slot it overwrites (k_locate), per
   // page the last chunk tag that brought it a new key
   uint32_t* oslot = nullptr;
-  uint32_t* pnew = nullptr;
+  uint8_t* pnew = nullptr;  // per page: dev::new_mark(tag) of the last chunk that gave it a new key
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
   uint64_t* leaf_rd = nullptr;
@@ -154,11 +154,28 @@ struct shm_tree {
   hipEvent_t ex_ev = nullptr;       // last exclusive call
   hipStream_t ex_s = nullptr;
   bool ex_valid = false;
-  // the last insert chunk (its ordering workspace): a later insert's
-  // ordering on another stream waits for this, not for every exclusive call
-  hipEvent_t ins_ev = nullptr;
-  hipStream_t ins_s = nullptr;
-  bool ins_valid = false;
+  // insert ordering pipeline.  The ordering of chunk `tag` writes the op
+  // buffers of parity tag & 1 (uk / uv / dk / counts, op_keys() below),
+  // which the apply of chunk tag - 2 read last (app_ev); every ordering
+  // reuses the ordering scratch (ka .. bins), so it follows the previous
+  // ordering (ord_ev).  A later chunk's ordering may therefore run on
+  // another stream beside this chunk's apply.
+  hipEvent_t app_ev[2] = {nullptr, nullptr};
+  hipStream_t app_s[2] = {nullptr, nullptr};
+  bool app_valid[2] = {false, false};
+  hipEvent_t ord_ev = nullptr;
+  hipStream_t ord_s = nullptr;
+  bool ord_valid = false;
+  // chunks ordered by shm_insert_order and not yet applied, oldest first
+  struct Pending {
+    uint32_t tag;
+    uint64_t n;
+    ProfRec pr;
+    hipEvent_t ev;  // the ordering done (on s)
+    hipStream_t s;
+  };
+  Pending pend[2];
+  int n_pend = 0;
   hipEvent_t gws_ev[2] = {nullptr, nullptr};  // last user of each get workspace
   hipStream_t gws_s[2] = {nullptr, nullptr};
   bool gws_valid[2] = {false, false};
@@ -501,6 +518,22 @@ int drain_profile(shm_tree* t) {
   return SHM_OK;
 }
 
+// the op buffers of chunk tag's parity (the ordering's outputs)
+uint64_t* op_keys(shm_tree* t, uint32_t tag) { return t->uk + (uint64_t)(tag & 1u) * t->nmax; }
+uint64_t* op_vals(shm_tree* t, uint32_t tag) { return t->uv + (uint64_t)(tag & 1u) * t->nmax; }
+uint64_t* op_dels(shm_tree* t, uint32_t tag) { return t->dk + (uint64_t)(tag & 1u) * t->nmax; }
+// {upserts, deletes} of the chunk (k_bin_unique)
+uint64_t* op_counts(shm_tree* t, uint32_t tag) { return t->d_counts + 16 * (tag & 1u); }
+
+int record(shm_tree* t, hipEvent_t* ev, hipStream_t* es, bool* valid, hipStream_t s) {
+  if (!*ev) *ev = new_event();
+  if (!*ev) return SHM_EIO;
+  HIP_OK(hipEventRecord(*ev, s));
+  *es = s;
+  *valid = true;
+  return SHM_OK;
+}
+
 // One insert chunk (n <= nmax ops), issued without a host wait:
 //   1. ordering: k_tile_dedup, coarse partition, k_bin_unique
 //      -> uk / uv (upserts, key order, last writer) and dk (deletes); counts
@@ -517,6 +550,11 @@ int drain_profile(shm_tree* t) {
 // step 1: it reads only the batch and writes the insert workspace
 int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
                  uint64_t n, uint32_t tag, bool skip_pad) {
+  // the scratch's last user (the previous ordering) and the op buffers'
+  // (the apply of tag - 2), when they ran on another stream
+  if (t->ord_valid && t->ord_s != s) HIP_OK(hipStreamWaitEvent(s, t->ord_ev, 0));
+  const uint32_t p = tag & 1u;
+  if (t->app_valid[p] && t->app_s[p] != s) HIP_OK(hipStreamWaitEvent(s, t->app_ev[p], 0));
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
                          t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S,
                          skip_pad ? 1 : 0, s);
@@ -524,27 +562,32 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                                t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
   dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
                          reinterpret_cast<uint64_t*>(t->bins + 2 * dev::kCoarse), t->kb, t->ic,
-                         t->uk, t->uv, t->dk, t->d_counts, t->d_err, t->part_S, &t->ctl->gate,
+                         op_keys(t, tag), op_vals(t, tag), op_dels(t, tag), op_counts(t, tag),
+                         t->d_err, t->part_S, &t->ctl->gate,
                          tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, s);
   DBG(s, "ordering");
-  return SHM_OK;
+  return record(t, &t->ord_ev, &t->ord_s, &t->ord_valid, s);
 }
 
 // steps 2-5 on the ordered chunk of tag (the leaf directory is current)
 int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
+  // the byte marks repeat every 255 chunks: clear them when they wrap, so
+  // no page still carries this chunk's mark from 255 chunks ago
+  if (dev::new_mark(tag) == 1) HIP_OK(hipMemsetAsync(t->pnew, 0, t->cap_pages, s));
   dev::WalkArgs w = walk_args(t);
-  w.keys = t->uk;
+  uint64_t* const cnt = op_counts(t, tag);
+  w.keys = op_keys(t, tag);
   w.n = n;
-  w.n_dev = t->d_counts + 0;
+  w.n_dev = cnt + 0;
   w.out_page = t->pages;
   w.target_level = 0;
   w.out_slot = t->oslot;
   w.out_new = t->pnew;
   w.out_new_tag = tag;
   w.any_new = reinterpret_cast<uint32_t*>(t->d_counts + 10);
-  w.vals = t->uv;
+  w.vals = op_vals(t, tag);
   w.locks = t->locks;
   w.num_locks = t->cfg.num_locks;
   w.lock_tag = lock_tag;
@@ -552,7 +595,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_segment(t->pages, n, t->d_counts + 0, t->seg_lb, t->seg_start, t->seg_end,
+  dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
                       t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
@@ -560,8 +603,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.arena = t->arena;
   a.arena_bytes = t->arena_bytes;
   a.node = t->cfg.node_id;
-  a.op_key = t->uk;
-  a.op_val = t->uv;
+  a.op_key = op_keys(t, tag);
+  a.op_val = op_vals(t, tag);
   a.seg_start = t->seg_start;
   a.seg_end = t->seg_end;
   a.seg_page = t->seg_page;
@@ -598,8 +641,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.par = tag & 1u;
   u.err = t->d_err;
   u.ctl = t->ctl;
-  u.op_key = t->uk;
-  u.op_val = t->uv;
+  u.op_key = op_keys(t, tag);
+  u.op_val = op_vals(t, tag);
   u.seg_start = t->seg_start;
   u.seg_end = t->seg_end;
   u.seg_page = t->seg_page;
@@ -624,8 +667,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.d_base = t->d_base;
   u.int_rd = t->int_rd;
   u.pub = reinterpret_cast<uint64_t*>(t->h_pin_dev) + kPubWord / 2;
-  u.dk = t->dk;
-  u.n_del = t->d_counts + 1;
+  u.dk = op_dels(t, tag);
+  u.n_del = cnt + 1;
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
@@ -665,14 +708,9 @@ int insert_finish(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag, shm_tree
     if (rc) return rc;
   }
   const int rc = insert_apply(t, s, n, tag, pr);
-  if (rc == SHM_OK) {
-    if (!t->ins_ev) t->ins_ev = new_event();
-    if (t->ins_ev && hipEventRecord(t->ins_ev, s) == hipSuccess) {
-      t->ins_s = s;
-      t->ins_valid = true;
-    }
-  }
-  return rc;
+  if (rc != SHM_OK) return rc;
+  const uint32_t p = tag & 1u;
+  return record(t, &t->app_ev[p], &t->app_s[p], &t->app_valid[p], s);
 }
 
 int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
@@ -692,19 +730,19 @@ int insert_all(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t
                bool sync, bool skip_pad = false) {
   if (!t || (n && (!keys || !vals))) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
+  if (t->n_pend) return SHM_EINVAL;  // chunks ordered by shm_insert_order come first
   hipStream_t s = pick(stream);
   // The first chunk's ordering reads only the batch and writes the insert
   // workspace, so it is queued before this call's cross-stream wait: it
-  // waits for the previous insert (the workspace's last user) but not for,
-  // e.g., the range scans just issued on another stream, and runs beside
-  // them.  (An ordered search's workspace aliases the insert workspace:
-  // not with SHM_FLAG_SORT_GETS.)
+  // waits for the workspace's last users (insert_order) but not for, e.g.,
+  // the range scans just issued on another stream, and runs beside them.
+  // (An ordered search's workspace aliases the insert workspace: not with
+  // SHM_FLAG_SORT_GETS.)
   const bool early = n > 0 && !(t->cfg.flags & SHM_FLAG_SORT_GETS);
   uint32_t tag0 = 0;
   shm_tree::ProfRec pr0{};
   const uint64_t m0 = std::min(t->nmax, n);
   if (early) {
-    if (t->ins_valid && t->ins_s != s) HIP_OK(hipStreamWaitEvent(s, t->ins_ev, 0));
     if (const int rc = insert_begin(t, s, keys, vals, m0, skip_pad, &tag0, pr0)) return rc;
   }
   Order ord(t, s, true);
@@ -751,7 +789,11 @@ void free_all(shm_tree* t) {
   }
   for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
   if (t->ex_ev) (void)hipEventDestroy(t->ex_ev);
-  if (t->ins_ev) (void)hipEventDestroy(t->ins_ev);
+  for (hipEvent_t e : t->app_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (t->ord_ev) (void)hipEventDestroy(t->ord_ev);
+  for (auto& pd : t->pend)
+    if (pd.ev) (void)hipEventDestroy(pd.ev);
   for (hipEvent_t e : t->gws_ev)
     if (e) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
@@ -991,9 +1033,9 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->ia, n);
   rc |= dalloc(&t->ib, n);
   rc |= dalloc(&t->ic, n);
-  rc |= dalloc(&t->uk, n);
-  rc |= dalloc(&t->uv, n);
-  rc |= dalloc(&t->dk, n);
+  rc |= dalloc(&t->uk, 2 * n);  // two parities (op_keys)
+  rc |= dalloc(&t->uv, 2 * n);
+  rc |= dalloc(&t->dk, 2 * n);
   rc |= dalloc(&t->pages, segcap);
   rc |= dalloc(&t->seg_lb, dev::seg_tiles(segcap) + 1);
   rc |= dalloc(&t->bsum64, dev::seg_tiles(n) + 1);
@@ -1060,7 +1102,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->arena, 0, kPageSize, s) ||
       hipMemsetAsync(t->leaf_hw, kLeafHwFull, t->cap_pages, s) ||
       hipMemsetAsync(t->sum, 0, t->cap_pages * kSumBytes, s) ||
-      hipMemsetAsync(t->pnew, 0, sizeof(uint32_t) * t->cap_pages, s))
+      hipMemsetAsync(t->pnew, 0, t->cap_pages, s))
     return fail(SHM_EIO);
   // Tree::Tree (Tree.cpp:44-60): empty leaf root
   t->next_page = 1;
@@ -1192,6 +1234,7 @@ int shm_mixed_batch(shm_tree* t, const uint64_t* get_keys, uint64_t n_get, uint6
   if (!t || (n_get && (!get_keys || !vals_out)) || (n_ins && (!ins_keys || !ins_vals)))
     return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
+  if (t->n_pend && n_ins) return SHM_EINVAL;  // apply the ordered chunks first
   hipStream_t s = pick(stream);
   mirror(t);
   Order ord(t, s, true);
@@ -1219,6 +1262,61 @@ int shm_insert_batch(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
 int shm_insert_batch_async(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
                            uint64_t n, void* stream) {
   return insert_all(t, keys, vals, n, stream, false);
+}
+
+// Split insert (one chunk): the ordering on one stream, the tree phase
+// later on another, so a caller can order chunk i + 1 while chunk i applies.
+int shm_insert_order(shm_tree* t, const uint64_t* keys, const uint64_t* vals, uint64_t n,
+                     void* stream, uint32_t* ticket) {
+  if (!t || !ticket || (n && (!keys || !vals))) return SHM_EINVAL;
+  if (n > t->nmax) return SHM_E2BIG;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (t->n_pend >= 2) return SHM_EAGAIN;  // two op-buffer parities
+  hipStream_t s = pick(stream);
+  // with SHM_FLAG_SORT_GETS an ordered search shares the ordering scratch:
+  // the ordering is then ordered like an exclusive call
+  const bool sorted = (t->cfg.flags & SHM_FLAG_SORT_GETS) != 0;
+  Order ord(t, s, sorted);
+  if (ord.rc) return ord.rc;
+  shm_tree::Pending& pd = t->pend[t->n_pend];
+  pd.pr = shm_tree::ProfRec{};
+  if (const int rc = insert_begin(t, s, keys, vals, n, false, &pd.tag, pd.pr)) return rc;
+  pd.n = n;
+  pd.s = s;
+  if (!pd.ev) pd.ev = new_event();
+  if (!pd.ev) return SHM_EIO;
+  HIP_OK(hipEventRecord(pd.ev, s));
+  ++t->n_pend;
+  *ticket = pd.tag;
+  return SHM_OK;
+}
+
+int shm_insert_apply(shm_tree* t, uint32_t ticket, void* stream) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (!t->n_pend || t->pend[0].tag != ticket) return SHM_EINVAL;  // oldest first
+  const shm_tree::Pending pd = t->pend[0];
+  hipStream_t s = pick(stream);
+  Order ord(t, s, true);
+  if (ord.rc) return ord.rc;
+  if (pd.s != s) HIP_OK(hipStreamWaitEvent(s, pd.ev, 0));
+  // the slot is free once its apply is queued (the buffers' reuse waits for
+  // app_ev on the device)
+  std::swap(t->pend[0], t->pend[1]);
+  --t->n_pend;
+  mirror(t);
+  shm_tree::ProfRec pr = pd.pr;
+  if (t->prof_on) {
+    // the profile times the apply alone (the ordering ran earlier, elsewhere)
+    if (!pr.e[0]) {
+      if (const int rc = prof_begin(t, s, shm_tree::kProfInsert, pd.n, 4, pr)) return rc;
+    } else {
+      HIP_OK(hipEventRecord(pr.e[0], s));
+    }
+  }
+  const int rc = insert_finish(t, s, pd.n, pd.tag, pr);
+  if (rc == SHM_OK) t->batches += 1;
+  return rc;
 }
 
 int shm_del_batch(shm_tree* t, const uint64_t* keys, uint64_t n, void* stream) {
@@ -1358,7 +1456,6 @@ int shm_range_query_slots(shm_tree* t, const uint64_t* from, const uint64_t* to,
   hipStream_t s = pick(stream);
   Order ord(t, s, true);  // the directory refresh
   if (ord.rc) return ord.rc;
-  if (status_dev) HIP_OK(hipMemsetAsync(status_dev, 0, 2 * sizeof(uint64_t), s));
   if (n == 0) return SHM_OK;
   if (const int rc = range_prepare(t, s)) return rc;
   dev::RangeArgs a = range_args(t, from, to, n, counts_out, nullptr, nullptr);

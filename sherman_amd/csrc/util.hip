@@ -56,12 +56,12 @@ __device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, u
 }
 }  // namespace
 
-// Only segments whose page gets a new key (pnew[page] == tag, set by
+// Only segments whose page gets a new key (pnew[page] == new_mark(tag), set by
 // k_locate) need the upsert and split kernels: the others were applied in
 // place by k_locate.  The list holds just those ("staged" segments), so the
 // later kernels' grids and block ranges cover only them.
-__device__ __forceinline__ bool page_new(const uint32_t* pnew, uint64_t pg, uint32_t tag) {
-  return pnew[ga_offset(pg) >> 10] == tag;
+__device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint32_t tag) {
+  return pnew[ga_offset(pg) >> 10] == new_mark(tag);
 }
 
 // One launch: every 1024-op tile counts its staged heads, publishes the
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  const uint64_t* n_dev, uint64_t* lbw,
                                                  uint32_t* seg_start, uint32_t* seg_end,
                                                  uint64_t* seg_page, uint32_t* num_seg,
-                                                 const uint32_t* pnew, uint32_t tag,
+                                                 const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err) {
   __shared__ uint32_t s_pre[kT / kWave];
   const uint32_t b = blockIdx.x;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
-                    uint32_t* num_seg, const uint32_t* pnew, uint32_t tag,
+                    uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev, lbw,

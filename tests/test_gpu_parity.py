@@ -151,6 +151,76 @@ def test_random_batches_vs_oracle(lib_ok, batch):
     t.close()
 
 
+def test_insert_order_apply_pipeline_vs_oracle(lib_ok):
+    """shm_insert_order / shm_insert_apply: batch i + 1 ordered on a second
+    stream while batch i applies (the ordering outputs alternate between two
+    buffer parities).  Upserts with in-batch duplicates, deletes and new keys
+    that split leaves; gets queued between the applies see exactly the
+    batches applied before them; contents and invariants equal the oracle's
+    after every batch; the API's refusals (third ticket, out-of-order apply,
+    other inserts while a ticket is outstanding, a chunk over max_batch) and
+    a kKeyMax chunk rejected at the next synchronising call."""
+    rng = np.random.default_rng(77)
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 14)
+    orc = OracleTree(256 << 20)
+    universe = hashed_keys(1, 40001)
+    pre = universe[:10000]
+    gpu_insert(t, pre, pre + U64(1))
+    orc.apply_batch(pre, pre + U64(1))
+    s_ord, s_main = torch.cuda.Stream(), torch.cuda.Stream()
+    s_ord.wait_stream(torch.cuda.current_stream())
+    s_main.wait_stream(torch.cuda.current_stream())
+    batches = []
+    for _ in range(8):
+        b = int(rng.integers(3000, 1 << 14))
+        ks = universe[rng.integers(0, universe.size, b)]  # updates, new keys, duplicates
+        vs = rng.integers(1, 1 << 62, b).astype(U64)
+        vs[rng.random(b) < 0.08] = 0  # deletes
+        batches.append((dev(ks), dev(vs), ks, vs))
+    probe = np.concatenate([universe, hashed_keys(50001, 51001)])
+    dprobe = dev(probe)
+    outs = []
+    tickets = [t.insert_order(batches[0][0], batches[0][1], stream=s_ord)]
+    for i in range(len(batches)):
+        if i + 1 < len(batches):
+            tickets.append(t.insert_order(batches[i + 1][0], batches[i + 1][1], stream=s_ord))
+            if i == 0:
+                # two tickets outstanding: a third is refused, and so is the
+                # newer one applied first, and any other insert
+                with pytest.raises(shm.ShermanError):
+                    t.insert_order(batches[0][0], batches[0][1], stream=s_ord)
+                with pytest.raises(shm.ShermanError):
+                    t.insert_apply(tickets[1], stream=s_main)
+                with pytest.raises(shm.ShermanError):
+                    t.insert_batch_async(batches[0][0], batches[0][1])
+        t.insert_apply(tickets[i], stream=s_main)
+        v = torch.empty_like(dprobe)
+        f = torch.empty(dprobe.numel(), dtype=torch.uint8, device="cuda")
+        t.search_batch(dprobe, v, f, stream=s_main)  # sees batches 0..i
+        outs.append((v, f))
+    t.synchronize()
+    for i, (_, _, ks, vs) in enumerate(batches):
+        orc.apply_batch(ks, vs)
+        ov, of = orc.search_batch(probe)
+        assert_same(probe, ov, of, host(outs[i][0]), outs[i][1].cpu().numpy())
+    compare_contents(t, orc)
+    assert orc.check()[0] == 0
+    # a chunk over max_batch is refused; a kKeyMax chunk is rejected whole
+    big = torch.ones((1 << 14) + 1, dtype=torch.int64, device="cuda")
+    with pytest.raises(shm.ShermanError):
+        t.insert_order(big, big)
+    bad = batches[0][2].copy()
+    bad[7] = U64((1 << 64) - 1)
+    dbad = dev(bad)
+    tk = t.insert_order(dbad, batches[0][1])
+    t.insert_apply(tk)
+    with pytest.raises(shm.ShermanError) as ei:
+        t.synchronize()
+    assert ei.value.rc == shm.SHM_EINVAL
+    compare_contents(t, orc)  # nothing of the rejected chunk applied
+    t.close()
+
+
 def test_bulk_sorted_and_reverse(lib_ok):
     """One huge batch into an empty tree (k-way splits up to a new root)."""
     t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 20)
@@ -341,9 +411,10 @@ def test_range_query_slots_vs_oracle(lib_ok):
     lo[2], hi[2] = U64(0), U64((1 << 64) - 1)  # whole key space
     cap = 200
     vals = torch.full((n, cap), 0x5A5A, dtype=torch.int64, device="cuda")
-    pend = t.range_query_slots(dev(lo), dev(hi), cap, vals=vals)
-    ovf, err = pend.check()
-    assert err == 0
+    status = torch.zeros(2, dtype=torch.int64, device="cuda")
+    pend = t.range_query_slots(dev(lo), dev(hi), cap, vals=vals, status=status)
+    ovf = pend.check()
+    assert int(status[1].item()) == 0 and int(status[0].item()) == ovf
     counts = pend.counts.cpu().numpy()
     hv = vals.cpu().numpy().view(np.uint64)
     img, root = t.dump_image()
@@ -369,10 +440,12 @@ def test_range_query_slots_vs_oracle(lib_ok):
     sc, sv = t.range_query_batch(dev(lo[sel]), dev(hi[sel]))
     assert np.array_equal(c2.cpu().numpy(), sc.cpu().numpy())
     assert np.array_equal(host(v2), host(sv))
-    # an empty batch still clears the status
+    # the status accumulates over calls; an empty batch adds nothing
     e = torch.empty(0, dtype=torch.int64, device="cuda")
-    c0, v0 = t.range_query_slots(e, e, cap).result()
+    c0, v0 = t.range_query_slots(e, e, cap, status=status).result()
     assert c0.numel() == 0
+    t.range_query_slots(dev(lo[:5]), dev(hi[:5]), cap, status=status).check()
+    assert int(status[0].item()) == ovf + int((counts[:5] > cap).sum())
     t.check()
     t.close()
 

@@ -19,20 +19,20 @@ INSERT_KERNELS = ("k_tile_dedup", "k_part_coarse", "k_bin_", "k_locate", "k_seg_
 ANCHOR = {"c3": "k_get", "c5": "k_range", "c2": "k_get"}
 
 
-def steps_of(rows, anchor, per):
-    n = sum(1 for r in rows if anchor in r["Kernel_Name"])
+def steps_of(rows, name, per):
+    n = sum(1 for r in rows if name in r["Kernel_Name"])
     return n / per if per else n
 
 
 def main(d, wl):
     anchor = ANCHOR[wl]
-    per = 2 if wl == "c5" else 1  # C5: count + fill range launches per step
     tr = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))))
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     i0 = next(i for i, r in enumerate(tr) if anchor in r["Kernel_Name"])
     # drop the trailing torch / readback-only tail after the last anchor step
     run = tr[i0:]
-    steps = steps_of(run, anchor, per)
+    # one insert chunk (one k_upper) per step in C3 and C5
+    steps = steps_of(run, "k_upper", 1)
     agg = collections.defaultdict(lambda: {"calls": 0, "ns": 0})
     for r in run:
         name = r["Kernel_Name"].split("(")[0]
