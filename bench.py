@@ -94,6 +94,10 @@ def parse():
                         "stream (shm_insert_order), so it runs beside the previous "
                         "batch's gets / scans and tree changes (shm_insert_apply); 0 = "
                         "shm_mixed_batch (c3) / shm_insert_batch_async (c5)")
+    p.add_argument("--order-first", type=int, default=0, choices=(0, 1),
+                   help="c5 slotted scans: 1 = each batch's insert ordering is queued "
+                        "(shm_insert_order) before its scans, its tree changes "
+                        "(shm_insert_apply) after them")
     p.add_argument("--slot-cap", type=int, default=256,
                    help="c5 slotted scans: values per scan buffer (every timed step is "
                         "checked to have no scan past it)")
@@ -387,12 +391,20 @@ def main():
             elif slots:
                 # one pass: each scan's values into its own buffer; every
                 # step's (scans past the slot, error bits) is checked after the run
+                tk = None
+                if args.order_first:
+                    # the batch's ordering queued before its scans (it reads
+                    # only the batch), its tree changes after them
+                    tk = tree.insert_order(pk, pv, stream=s_ins)
                 sv, sc = sbuf[applied[0] % 2]
                 pr = tree.range_query_slots(lo, hi, args.slot_cap, stream=s_scan, vals=sv,
                                             counts=sc, status=slot_status)
                 scan_out["r"] = SlotsResult(pr)
                 scan_out["slots"] = slot_status
-                tree.insert_batch_async(pk, pv, stream=s_ins)
+                if tk is None:
+                    tree.insert_batch_async(pk, pv, stream=s_ins)
+                else:
+                    tree.insert_apply(tk, stream=s_ins)
             elif route is None and args.async_scans:
                 # scans queued without a host wait; the batch's inserts queue
                 # behind them (their ordering beside them, on their own

@@ -203,6 +203,34 @@ __device__ __forceinline__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds&
   return lowest;
 }
 
+// An internal page written through to memory (8-B agent-scope relaxed
+// atomic stores = global_store ... sc1, two per lane): waves on other XCDs
+// read internal pages under the page's lock word (apply_run) or lock-free
+// (parent_of), so their stores must not wait in this XCD's L2 for a
+// release fence.  The writer drains them (s_waitcnt vmcnt(0)) before it
+// hands the word back (unlock_excl) -- MI355X_MICROARCH.md "visibility",
+// cdna_hip_programming.md §6 Guideline 16, R1 -- so unlocking needs no
+// buffer_wbl2 of the whole L2.
+__device__ __forceinline__ void store_page_wt(uint8_t* arena, uint64_t off, const uint32_t* lp) {
+  wave_lds_sync();
+  const int l = lane_id();
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(lp);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(arena + off);
+  const uint64_t w0 = src[l], w1 = src[kWave + l];
+  __hip_atomic_store(dst + l, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(dst + kWave + l, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The lane's 16 B of a page that other waves write through (store_page_wt)
+// under its lock word: agent-scope relaxed loads (global_load ... sc1), so
+// the locker needs no L1-invalidating acquire before reading the page
+__device__ __forceinline__ u32x4 load_page_slice_wt(const uint8_t* arena, uint64_t off) {
+  const uint64_t* p = reinterpret_cast<const uint64_t*>(arena + off + 16 * lane_id());
+  const uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+}
+
 // Internal page p of the split: q = T - (P - 1) records stay, one record per
 // extra page is pushed up (its ptr becomes that page's leftmost, its key the
 // separator, Tree.cpp:779-793).  Returns the page's lowest fence.
@@ -246,7 +274,7 @@ __device__ __forceinline__ uint64_t build_internal_page(const UpperArgs& a, Wave
     d[3] = (uint32_t)(val >> 32);
   }
   if (lane == 0) L.page[kOffInternalRear / 4] = fver;  // byte 1020
-  store_page(a.arena, ga_offset(s.dest), L.page);
+  store_page_wt(a.arena, ga_offset(s.dest), L.page);
   if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = kLeafHwFull;
   return lowest;
 }
@@ -260,7 +288,7 @@ __device__ __forceinline__ void write_new_root(const UpperArgs& a, WaveLds& L, u
   init_page_image(L.page, (old_fver + 1) & 0xFF, x, 0, level, -1, kKeyMin, kKeyMax);
   wave_lds_sync();
   if (lane_id() == 0) L.page[kOffInternalRear / 4] = (old_fver + 1) & 0xFF;
-  store_page(a.arena, ga_offset(a.root), L.page);
+  store_page_wt(a.arena, ga_offset(a.root), L.page);
   if (a.leaf_hw && lane_id() == 0) a.leaf_hw[ga_offset(a.root) >> 10] = kLeafHwFull;
   // the root page is internal now: its summary no longer describes a leaf
   if (lane_id() == 0) clear_leaf_sum(a.sum, ga_offset(a.root));
@@ -703,17 +731,18 @@ __device__ __forceinline__ bool lock_excl(const UpperArgs& a, uint64_t page) {
       __builtin_amdgcn_s_sleep(2);
     }
   }
+  // no acquire: the holder reads the page with sc1 loads (load_page_slice_wt)
+  // and its previous holders wrote it through (store_page_wt)
   got = rl32(got, 0);
-  if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return got != 0;
 }
 __device__ __forceinline__ void unlock_excl(const UpperArgs& a, uint64_t page) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the page's stores performed
-  if (lane_id() == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // the page's write-through stores (store_page_wt) performed: the next
+  // holder's acquire sees them, no L2 write-back needed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane_id() == 0)
     __hip_atomic_store(a.locks + lock_index(page, a.num_locks), a.tag, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // One internal page of `level` receives the ops o (sorted separators, their
@@ -759,6 +788,9 @@ __device__ __forceinline__ uint32_t apply_internal(const UpperArgs& a, WaveLds& 
     emit_sep(a, level + 1, low, sp.dest, par, err);
   }
   const uint64_t dest0 = grow ? ga_make(a.node, (first + P - 1) * kPageSize) : page;
+  // the new right siblings land before page 0 points at them (Tree.cpp:962:
+  // the sibling is written before the relink), for lock-free parent walks
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   (void)build_internal_page(a, L, h, na, o, SplitPage{0, (int)P, T2, first, dest0}, level);
   if (grow) {
     write_new_root(a, L, dest0, level + 1, h.fver);
@@ -795,7 +827,7 @@ __device__ __forceinline__ uint32_t apply_run(const UpperArgs& a, WaveLds& L, co
       err |= kErrLock;
       return nout;
     }
-    const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+    const u32x4 w = load_page_slice_wt(a.arena, ga_offset(page));
     const Hdr h = parse_hdr(w);
     const uint64_t k0 = keys[hs];
     if (h.leftmost == 0 || h.level != level || h.fver != h.rver_internal || k0 < h.lowest) {
