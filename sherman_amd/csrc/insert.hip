@@ -1064,6 +1064,14 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     __syncthreads();
   }
+  // nothing to split and nothing to delete (every op applied in place, C3's
+  // chunks): the superblock's batch count is the only change, so block 0
+  // writes it and no block waits for the others (no fan-in on `done`)
+  if (total == 0 && *a.n_del == 0 && !a.force_abort) {
+    if (b == 0 && t == 0) sb->batches = a.batch;
+    stamp();
+    return;
+  }
   bool ok = true;
   // every split small (C5's chunks): each wave takes its separators up
   // itself (propagate), no level list, no grid barrier
