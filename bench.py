@@ -813,7 +813,7 @@ def _request_roofline(batch, keys_log2, gets_per_s, page_walk):
             pmc.get("tcc_ea_rdreq_per_launch") and "k_get_sum" in pmc.get("kernel", "")):
         return {}
     rpg = pmc["tcc_ea_rdreq_per_launch"] / batch
-    ceil = cal.get("walk_mix_ceiling_G_per_s") or cal["random_request_ceiling_G_per_s"]
+    ceil = cal["random_request_ceiling_G_per_s"]  # the best calibration kernel's rate
     rate = rpg * gets_per_s / 1e9
     return {"requests_per_get": round(rpg, 3), "requests_G_per_s": round(rate, 2),
             "request_ceiling_G_per_s": ceil, "request_frac": round(rate / ceil, 4),

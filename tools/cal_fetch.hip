@@ -204,7 +204,7 @@ int main() {
   CK(hipDeviceSynchronize());
   timed("k_chain dir64M->sum128M(64B)->ent2G", (double)n * 3, 0, (2ull << 30) + (192ull << 20),
         [&](uint64_t salt) { k_chain<<<g, 256>>>(buf, n, salt, sink); });
-  timed("k_chain 1Mi lanes", (double)ns * 3, 0, (2ull << 30) + (192ull << 20),
+  timed("k_chain short 1Mi lanes", (double)ns * 3, 0, (2ull << 30) + (192ull << 20),
         [&](uint64_t salt) { k_chain<<<dim3((unsigned)((ns + 255) / 256)), 256>>>(buf, ns, salt, sink); });
   return 0;
 }
