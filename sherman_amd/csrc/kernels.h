@@ -98,9 +98,11 @@ void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
 // keys each
 // hint (nullable): 2 x n_ent u32, the level-1 and level-2 pages (page
 // indices, 0 = none) on the root-to-leaf path of each prefix's first key
+// from_hint: start each prefix at the level-1 page the previous build
+// recorded in hint (same entry count, same tree) instead of the root
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* hint, uint32_t* err, hipStream_t s);
+                     uint32_t* hint, int from_hint, uint32_t* err, hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.

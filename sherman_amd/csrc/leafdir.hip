@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
                                                   uint64_t root, uint64_t dir_lo,
                                                   uint32_t shift, uint64_t n_ent,
                                                   uint64_t* __restrict__ dir,
-                                                  uint32_t* __restrict__ hint, uint32_t* err) {
+                                                  uint32_t* __restrict__ hint, int from_hint,
+                                                  uint32_t* err) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_ent) return;
   const uint64_t lo = dir_lo + (p << shift);
@@ -63,6 +64,16 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
   uint64_t ptr = root, cover = root;
   uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t h1 = 0, h2 = 0;  // level-1 / level-2 pages on lo's path
+  // a rebuild starts at the level-1 page the previous build recorded on lo's
+  // path: a page keeps its lowest fence when it splits, so it is still a
+  // B-link start for lo (right moves past its new highest fence); the
+  // level-2 hint is kept as it was (a stale one is a valid start as well)
+  bool hinted = false;
+  if (from_hint && hint && hint[p]) {
+    ptr = dir_page_ga(hint[p], node);
+    h2 = hint[n_ent + p];
+    hinted = true;
+  }
   bool ok = false;
   for (int it = 0; it < 4096; ++it) {
     if (!ptr_ok(ptr, node, arena_bytes)) break;
@@ -70,6 +81,14 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
     const uint64_t leftmost = pg64_b1(pg, 2);
     const uint64_t sibling = pg64_b1(pg, 4);
     const uint64_t highest = pg64(pg, kOffHighest);
+    if (hinted && (leftmost == 0 || pg[kOffLevel] != 1 || lo < pg64(pg, kOffLowest))) {
+      // not a level-1 page on lo's path any more (the root page grew a
+      // level): descend from the root
+      hinted = false;
+      ptr = root;
+      h2 = 0;
+      continue;
+    }
     if (lo >= highest) {  // turn right (Tree.cpp:626-629)
       if (sibling == 0) break;
       ptr = sibling;
@@ -81,8 +100,11 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
       if (lv == 2) h2 = dir_page_index(ptr);
       const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
       const int c = keys_le(pg, cnt, lo);
-      if (hi < highest && keys_le(pg, cnt, hi) == c) cover = ptr;  // whole prefix below
+      // the deepest internal page whose fences hold the whole prefix (lo is
+      // past its lowest on the path): the start of a prefix of > 4 leaves
+      if (hi < highest) cover = ptr;
       ptr = c == 0 ? leftmost : pg64(pg, kOffRecords + kInternalEntry * (c - 1) + 8);
+      hinted = false;  // below the hinted level now
       continue;
     }
     // leaf containing lo; collect the leaves that cover [lo, hi]
@@ -132,10 +154,10 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
 
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* hint, uint32_t* err, hipStream_t s) {
+                     uint32_t* hint, int from_hint, uint32_t* err, hipStream_t s) {
   if (!n_ent) return;
   hipLaunchKernelGGL(k_leaf_dir, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s, arena,
-                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, err);
+                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, from_hint, err);
 }
 
 }  // namespace dev

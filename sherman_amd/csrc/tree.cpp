@@ -108,6 +108,7 @@ struct shm_tree {
   uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
   uint64_t dir_np = 0;
   bool dir_valid = false;
+  bool hint_ok = false;  // dir_hint holds the last build's pages of this tree
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
   uint64_t* top_keys = nullptr;
@@ -340,12 +341,14 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
     if (dalloc(&t->dir, 4ull << bits)) return SHM_ENOMEM;  // 32 B per entry
     if (dalloc(&t->dir_hint, 2ull << bits)) return SHM_ENOMEM;  // levels 1, 2
     t->dir_bits = bits;
+    t->hint_ok = false;
   }
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
-                       t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint, t->d_err,
-                       s);
+                       t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint,
+                       t->hint_ok ? 1 : 0, t->d_err, s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
+  t->hint_ok = true;
   return SHM_OK;
 }
 
@@ -1602,6 +1605,7 @@ int shm_load_image(shm_tree* t, const void* host_buf, uint64_t bytes,
   t->root_level = reinterpret_cast<const uint8_t*>(host_buf)[ro + kOffLevel];
   t->next_page = pages;
   t->dir_valid = false;  // contents changed: rebuild the leaf directory
+  t->hint_ok = false;    // ... from the root
   t->top_valid = false;
   Order ord(t, t->stream, true);
   return write_superblock(t, t->stream);
