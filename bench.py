@@ -94,8 +94,6 @@ def parse():
                         "stream (shm_insert_order), so it runs beside the previous "
                         "batch's gets / scans and tree changes (shm_insert_apply); 0 = "
                         "shm_mixed_batch (c3) / shm_insert_batch_async (c5)")
-    p.add_argument("--ins-priority", type=int, default=0, choices=(0, 1),
-                   help="c5, 2 streams: 1 = the inserts' stream at high priority")
     p.add_argument("--order-first", type=int, default=0, choices=(0, 1),
                    help="c5 slotted scans: 1 = each batch's insert ordering is queued "
                         "(shm_insert_order) before its scans, its tree changes "
@@ -353,10 +351,7 @@ def main():
         applied = [0]  # batches applied so far (all step loops)
         s_scan = s_ins = None
         if route is None and args.streams == 2:
-            # --ins-priority: the inserts' stream (their ordering runs beside
-            # the scans) at high priority, so its blocks dispatch first
-            s_scan = torch.cuda.Stream()
-            s_ins = torch.cuda.Stream(priority=-1 if args.ins_priority else 0)
+            s_scan, s_ins = torch.cuda.Stream(), torch.cuda.Stream()
             s_scan.wait_stream(torch.cuda.current_stream())
             s_ins.wait_stream(torch.cuda.current_stream())
 
