@@ -738,7 +738,7 @@ __device__ __forceinline__ bool lock_excl(const UpperArgs& a, uint64_t page) {
 }
 __device__ __forceinline__ void unlock_excl(const UpperArgs& a, uint64_t page) {
   // the page's write-through stores (store_page_wt) performed: the next
-  // holder's acquire sees them, no L2 write-back needed
+  // holder's sc1 loads (load_page_slice_wt) see them, no L2 write-back needed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane_id() == 0)
     __hip_atomic_store(a.locks + lock_index(page, a.num_locks), a.tag, __ATOMIC_RELAXED,
