@@ -94,6 +94,11 @@ def parse():
                         "stream (shm_insert_order), so it runs beside the previous "
                         "batch's gets / scans and tree changes (shm_insert_apply); 0 = "
                         "shm_mixed_batch (c3) / shm_insert_batch_async (c5)")
+    p.add_argument("--dir-fp", type=int, default=None, choices=(0, 1),
+                   help="leaf-directory entries of one-leaf prefixes carry the leaf's "
+                        "fingerprints (SHM_DIR_FP; library default 1; 0 = round-2 form)")
+    p.add_argument("--dir-extra-bits", type=int, default=None,
+                   help="leaf directory with 2^x entries per tree page (SHM_DIR_EXTRA_BITS)")
     p.add_argument("--order-first", type=int, default=0, choices=(0, 1),
                    help="c5 slotted scans: 1 = each batch's insert ordering is queued "
                         "(shm_insert_order) before its scans, its tree changes "
@@ -179,6 +184,10 @@ def build_shard(tree, n_keys, world, rank, dev):
 
 def main():
     args = parse()
+    if args.dir_fp is not None:  # read by the library when it loads
+        os.environ["SHM_DIR_FP"] = str(args.dir_fp)
+    if args.dir_extra_bits is not None:
+        os.environ["SHM_DIR_EXTRA_BITS"] = str(args.dir_extra_bits)
     import torch
 
     import sherman_amd as shm

@@ -203,11 +203,14 @@ __device__ __forceinline__ void store_page(uint8_t* arena, uint64_t off,
 }
 
 // leaf directory lookup (leafdir.hip): the start page for key k, `fallback`
-// when k is outside the directory.  Entry p is 32 B, u32[8] =
-// {pg0..pg3, t1..t3, count}: the leaves covering prefix p as page indices
-// (GlobalAddress offset / 1 KB) and their split points t_i, the top 32 bits
-// of (sep_i - lo_p) within the prefix (exact when the prefix spans <= 2^32
-// keys); count 0: pg0 is the deepest internal page covering the prefix.
+// when k is outside the directory.  Entry p is 64 B (kDirWords u64), its
+// first 32 B u32[8] = {pg0..pg3, t1..t3, count}: the leaves covering prefix
+// p as page indices (GlobalAddress offset / 1 KB) and their split points
+// t_i, the top 32 bits of (sep_i - lo_p) within the prefix (exact when the
+// prefix spans <= 2^32 keys); count 0: pg0 is the deepest internal page
+// covering the prefix.  count & kDirFp: ONE leaf covers the prefix and the
+// entry carries a copy of its summary fingerprints (dir_fp_cand below) in
+// place of pg1..pg3 / t1..t3 and in bytes 32..61.
 // Leaf i is taken only when t_i < t(k), which proves k > sep_i; on a tie the
 // walk starts one leaf to the left and moves right (B-link, Tree.cpp:626-629).
 // k lies inside the directory's key range (and is not kKeyMax)
@@ -220,17 +223,64 @@ __device__ __forceinline__ uint64_t dir_start(const uint64_t* dir, uint64_t dir_
                                               uint16_t node, uint64_t k, uint64_t fallback) {
   const uint64_t p = (k - dir_lo) >> dir_shift;
   if (k < dir_lo || p >= dir_n || k == kKeyMax) return fallback;
-  const u32x4* e = reinterpret_cast<const u32x4*>(dir + 4 * p);
+  const u32x4* e = reinterpret_cast<const u32x4*>(dir + kDirWords * p);
   const u32x4 e0 = e[0], e1 = e[1];
   const uint64_t off = (k - dir_lo) - (p << dir_shift);
   const bool exact = dir_shift <= 32;
   const uint32_t tk = exact ? (uint32_t)off : (uint32_t)(off >> (dir_shift - 32));
-  const uint32_t cnt = e1.w;
+  const uint32_t cnt = e1.w & 0xFFu;
   auto past = [&](uint32_t t) { return t < tk || (exact && t == tk); };
   const uint32_t i = (uint32_t)(cnt > 1 && past(e1.x)) + (uint32_t)(cnt > 2 && past(e1.y)) +
                      (uint32_t)(cnt > 3 && past(e1.z));
   const uint32_t pg = i == 0 ? e0.x : i == 1 ? e0.y : i == 2 ? e0.z : e0.w;
   return dir_page_ga(pg, node);
+}
+
+// dir_start reading the whole 64 B entry into e (one request): *fpform when
+// it is in fingerprint form (its one leaf returned, candidates by dir_fp_cand)
+__device__ __forceinline__ uint64_t dir_start_e(const uint64_t* dir, uint64_t dir_lo,
+                                                uint32_t dir_shift, uint64_t dir_n, uint16_t node,
+                                                uint64_t k, uint64_t fallback, u32x4 (&e)[4],
+                                                bool& fpform) {
+  fpform = false;
+  const uint64_t p = (k - dir_lo) >> dir_shift;
+  if (k < dir_lo || p >= dir_n || k == kKeyMax) return fallback;
+  const u32x4* ep = reinterpret_cast<const u32x4*>(dir + kDirWords * p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) e[j] = ep[j];
+  const uint64_t off = (k - dir_lo) - (p << dir_shift);
+  const bool exact = dir_shift <= 32;
+  const uint32_t tk = exact ? (uint32_t)off : (uint32_t)(off >> (dir_shift - 32));
+  const uint32_t cnt = e[1].w & 0xFFu;
+  fpform = (e[1].w & kDirFp) != 0;
+  auto past = [&](uint32_t t) { return t < tk || (exact && t == tk); };
+  const uint32_t i = fpform ? 0u
+                            : (uint32_t)(cnt > 1 && past(e[1].x)) +
+                                  (uint32_t)(cnt > 2 && past(e[1].y)) +
+                                  (uint32_t)(cnt > 3 && past(e[1].z));
+  const uint32_t pg = i == 0 ? e[0].x : i == 1 ? e[0].y : i == 2 ? e[0].z : e[0].w;
+  return dir_page_ga(pg, node);
+}
+
+// A directory entry in fingerprint form (count == 1 | kDirFp, layout.h):
+// the candidate slots of its one leaf for key k, from the copy of the leaf's
+// summary fingerprints taken when the directory was built: fp[s] at bytes
+// 4..27 (s < 24) and 32..61 (s >= 24) of the entry.  The copy may be stale
+// (the leaf got keys or split since): a candidate is only a slot to read,
+// and a get that finds no valid entry with its key there walks the summary
+// path (never a wrong answer, a stale copy only costs that fallback).
+__device__ __forceinline__ uint64_t dir_fp_cand(const u32x4 (&e)[4], uint64_t k) {
+  const uint32_t fq = key_fp(k);
+  uint64_t cand = 0;
+#pragma unroll
+  for (int s = 0; s < kLeafCardinality; ++s) {
+    const int b = s < 24 ? 4 + s : 8 + s;  // 24 fps at 4..27, 30 at 32..61
+    const u32x4 v = e[b >> 4];
+    const int d = (b >> 2) & 3;
+    const uint32_t x = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+    cand |= (uint64_t)(((x >> (8 * (b & 3))) & 0xFFu) == fq) << s;
+  }
+  return cand;
 }
 
 __device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,

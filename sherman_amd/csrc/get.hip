@@ -344,10 +344,33 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
   uint64_t val = 0;
   uint32_t err = 0;
   uint32_t c_int = 0, c_right = 0, c_hops = 0, c_ent = 0;
+  bool hit = false;
   if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
     uint64_t ptr = a.root;
     if (a.dir) {
-      ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
+      u32x4 e[4];
+      bool fpform;
+      ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform);
+      if (fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
+        // the prefix lies in one leaf and the entry holds its fingerprints:
+        // read the candidate slots straight away (Tree.cpp:687-697's first
+        // valid slot with the key); a key not found this way (absent, or
+        // the copy is stale) takes the summary walk below
+        const uint8_t* page = a.arena + ga_offset(ptr);
+        uint64_t cand = dir_fp_cand(e, k);
+        while (cand) {
+          uint64_t ek, ev;
+          uint32_t ef, er;
+          ++c_ent;
+          lane_entry(page, ctz64(cand), ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            hit = true;
+            break;
+          }
+          cand &= cand - 1;
+        }
+      }
     } else if (tn) {
       // the last page of the level whose lowest fence is <= k (tk[0] = kKeyMin)
       uint32_t lo = 0, hi = tn;
@@ -361,7 +384,7 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
       ptr = dir_page_ga(tpg[lo], a.node);
     }
     int retries = 0;
-    for (int hop = 0;; ++hop) {
+    for (int hop = 0; !hit; ++hop) {
       if (hop > kMaxRounds) {
         err |= kErrRounds;
         break;

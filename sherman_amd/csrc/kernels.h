@@ -100,9 +100,12 @@ void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
 // indices, 0 = none) on the root-to-leaf path of each prefix's first key
 // from_hint: start each prefix at the level-1 page the previous build
 // recorded in hint (same entry count, same tree) instead of the root
+// sum (nullable): the leaf summaries; an entry whose prefix lies inside one
+// leaf then carries that leaf's fingerprints (layout.h kDirFp)
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* hint, int from_hint, uint32_t* err, hipStream_t s);
+                     uint32_t* hint, int from_hint, const uint8_t* sum, uint32_t* err,
+                     hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.

@@ -81,6 +81,10 @@ constexpr uint32_t kSumOffTag = 8;
 constexpr uint32_t kSumOffFp = 9;
 constexpr uint8_t kSumLeaf = 0xA5;
 static_assert(kSumOffFp + kLeafCardinality <= kSumBytes, "summary line");
+// leaf directory entries (leafdir.hip): 64 B = kDirWords u64 each; count
+// word flag: the entry is in fingerprint form (device_common.h dir_fp_cand)
+constexpr uint64_t kDirWords = 8;
+constexpr uint32_t kDirFp = 0x100u;
 SHM_HD uint32_t key_fp(uint64_t k) {
   const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56);
   return f ? f : 1u;

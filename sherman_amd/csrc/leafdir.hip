@@ -55,6 +55,7 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
                                                   uint32_t shift, uint64_t n_ent,
                                                   uint64_t* __restrict__ dir,
                                                   uint32_t* __restrict__ hint, int from_hint,
+                                                  const uint8_t* __restrict__ sum,
                                                   uint32_t* err) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_ent) return;
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
     for (int i = 0; i < 8; ++i) out[i] = 0;
     out[0] = root;
   }
-  // out = {ptr0..3, sep1..3, n} -> the 32 B entry
+  // out = {ptr0..3, sep1..3, n} -> the 64 B entry
   const uint32_t sh = shift > 32 ? shift - 32 : 0;
   uint32_t t[3];
 #pragma unroll
@@ -146,18 +147,55 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
     hint[p] = ok ? h1 : 0u;
     hint[n_ent + p] = ok ? h2 : 0u;
   }
-  u32x4* e = reinterpret_cast<u32x4*>(dir + 4 * p);
-  e[0] = u32x4{dir_page_index(out[0]), dir_page_index(out[1]), dir_page_index(out[2]),
-               dir_page_index(out[3])};
+  u32x4* e = reinterpret_cast<u32x4*>(dir + kDirWords * p);
+  const uint32_t pg0 = dir_page_index(out[0]);
+  if (sum && out[7] == 1) {
+    // one leaf covers the whole prefix: the entry carries its summary's
+    // fingerprints (layout.h kDirFp), so a get of a key it holds reads the
+    // entry and then the key's slot, without the summary line
+    const u32x4* line = reinterpret_cast<const u32x4*>(sum + (ga_offset(out[0]) >> 10) * kSumBytes);
+    u32x4 l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = line[j];
+    if ((l[0].z & 0xFF) == kSumLeaf) {
+      uint8_t fp[kLeafCardinality];
+#pragma unroll
+      for (int sl = 0; sl < kLeafCardinality; ++sl) {
+        const int b = (int)kSumOffFp + sl;
+        const u32x4 v = l[b >> 4];
+        const int d = (b >> 2) & 3;
+        const uint32_t x = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+        fp[sl] = (uint8_t)(x >> (8 * (b & 3)));
+      }
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = 0;
+      w[0] = pg0;
+      w[7] = 1u | kDirFp;
+#pragma unroll
+      for (int sl = 0; sl < kLeafCardinality; ++sl) {
+        const int b = sl < 24 ? 4 + sl : 8 + sl;  // dir_fp_cand's placement
+        w[b >> 2] |= (uint32_t)fp[sl] << (8 * (b & 3));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = u32x4{w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]};
+      return;
+    }
+  }
+  e[0] = u32x4{pg0, dir_page_index(out[1]), dir_page_index(out[2]), dir_page_index(out[3])};
   e[1] = u32x4{t[0], t[1], t[2], (uint32_t)out[7]};
+  e[2] = u32x4{0u, 0u, 0u, 0u};
+  e[3] = u32x4{0u, 0u, 0u, 0u};
 }
 
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
-                     uint32_t* hint, int from_hint, uint32_t* err, hipStream_t s) {
+                     uint32_t* hint, int from_hint, const uint8_t* sum, uint32_t* err,
+                     hipStream_t s) {
   if (!n_ent) return;
   hipLaunchKernelGGL(k_leaf_dir, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s, arena,
-                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, from_hint, err);
+                     arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, from_hint, sum,
+                     err);
 }
 
 }  // namespace dev

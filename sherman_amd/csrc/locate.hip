@@ -54,13 +54,38 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   const bool match = a.out_slot != nullptr && a.target_level == 0;
   const uint64_t v = match ? a.vals[i] : 0;  // with the key: the update needs no later load
   uint64_t ptr = a.root;
-  if (a.dir && a.target_level == 0)
-    ptr = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr);
   uint32_t err = 0;
   int retries = 0;
   uint64_t out = 0;
   uint32_t slot = 0;
-  for (int hop = 0;; ++hop) {
+  if (a.dir && a.target_level == 0) {
+    u32x4 e[4];
+    bool fpform;
+    ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform);
+    if (match && fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
+      // the prefix lies in one leaf and the entry holds its fingerprints: an
+      // op whose key that leaf holds updates it without the summary line (a
+      // key has one valid slot, so a hit through a stale copy is the slot);
+      // any other op takes the summary walk below
+      const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.arena + ga_offset(ptr));
+      uint64_t cand = dir_fp_cand(e, k);
+      while (cand) {
+        const int sl = ctz64(cand);
+        uint64_t ek, ev;
+        uint32_t ef, er;
+        lane_entry(reinterpret_cast<const uint8_t*>(pg), sl, ek, ev, ef, er);
+        if (ek == k && ev != kValueNull) {
+          const uint32_t nf = ((ef & 0xF) + 1) & 0xF;
+          put_leaf_entry(const_cast<uint32_t*>(pg), sl, k, v, (ef & 0xF0) | nf, (er & 0xF0) | nf);
+          slot = 0x80000000u | (uint32_t)sl;
+          out = ptr;
+          break;
+        }
+        cand &= cand - 1;
+      }
+    }
+  }
+  for (int hop = 0; !slot; ++hop) {
     if (hop > kMaxRounds) {
       err |= kErrRounds;
       break;

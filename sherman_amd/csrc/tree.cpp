@@ -99,7 +99,7 @@ struct shm_tree {
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
   uint32_t* gcount = nullptr;       // insert ordering: survivors per 4096-op tile
   uint32_t* bins = nullptr;         // insert ordering: (start, count) per coarse bin
-  // leaf directory (leafdir.hip): 2^dir_bits entries of 32 B over the shard's
+  // leaf directory (leafdir.hip): 2^dir_bits entries of 64 B over the shard's
   // key range, rebuilt before a search once the tree grew by 1/32 since the
   // last build (stale entries only cost B-link right moves)
   bool err_pending = false;  // kernels ran since d_err was last read back
@@ -325,10 +325,34 @@ bool dir_stale(const shm_tree* t) {
   return !(t->dir_valid && t->next_page <= t->dir_np + t->dir_np / 32);
 }
 
+// directory entries in fingerprint form (SHM_DIR_FP=0: the round-2 form, A/B)
+bool dir_fp_on() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_DIR_FP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS,
+// default 1: two 64 B entries per page, so ~64 % of the prefixes lie inside
+// one leaf and carry its fingerprints; DESIGN §3 "Fingerprints in the
+// directory")
+uint32_t dir_extra_bits() {
+  static const uint32_t x = [] {
+    const char* e = getenv("SHM_DIR_EXTRA_BITS");
+    const int v = e ? atoi(e) : 1;
+    return (uint32_t)(v < 0 ? 0 : v > 3 ? 3 : v);
+  }();
+  return x;
+}
+
 int refresh_dir(shm_tree* t, hipStream_t s) {
   if (!dir_stale(t)) return SHM_OK;
   uint32_t bits = 10;
   while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
+  bits += dir_extra_bits();
+  if (bits > 25) bits = 25;  // 2 GB of entries at most
   if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
   if (!t->dir || bits != t->dir_bits) {
     if (t->dir) {
@@ -338,14 +362,14 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
       t->dir = nullptr;
       t->dir_hint = nullptr;
     }
-    if (dalloc(&t->dir, 4ull << bits)) return SHM_ENOMEM;  // 32 B per entry
+    if (dalloc(&t->dir, kDirWords << bits)) return SHM_ENOMEM;  // 64 B per entry
     if (dalloc(&t->dir_hint, 2ull << bits)) return SHM_ENOMEM;  // levels 1, 2
     t->dir_bits = bits;
     t->hint_ok = false;
   }
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
                        t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint,
-                       t->hint_ok ? 1 : 0, t->d_err, s);
+                       t->hint_ok ? 1 : 0, dir_fp_on() ? t->sum : nullptr, t->d_err, s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
   t->hint_ok = true;

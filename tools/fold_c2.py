@@ -138,6 +138,13 @@ def main():
     pw = json.load(open(os.path.join(P, "pmc_walk.json")))
     pw["tcc_ea_rdreq_per_launch"] = round(rdreq)
     pw["requests_source"] = "profiles/r%s_c2_timed.json (TCC_EA0_RDREQ_sum pass)" % rnd
+    # the walk's FETCH_SIZE from this pass (its writes, 8 B value + found
+    # byte per get, are unchanged: WRITE_SIZE kept from the earlier pass)
+    pw["fetch_size_kb"] = round(fetch_kb, 2)
+    pw["hbm_bytes_per_launch"] = fetch_kb * 1024 * 2 + pw["write_size_kb"] * 1024
+    pw.setdefault("write_source", pw.get("source", "earlier pass"))
+    pw["source"] = ("FETCH_SIZE: profiles/r%s_c2_timed.json (tools/measure_c2.sh %s); "
+                    "WRITE_SIZE: write_source" % (rnd, tag))
     open(os.path.join(P, "pmc_walk.json"), "w").write(json.dumps(pw, indent=1) + "\n")
     print(json.dumps(out, indent=1))
 
