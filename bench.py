@@ -585,16 +585,24 @@ def main():
     prof = tree.profile_read(reset=True)
     tree.profile(False)
     idx = None
-    if args.index_stats and args.workload == "c2":
+    if args.workload in ("c2", "c3") and args.sort != "on":
+        # the walk's index statistics over one more batch: how many gets the
+        # directory's fingerprints answered (two lines instead of three: the
+        # algorithmic bytes per get below)
         tree.profile(False, index_stats=True)
-        for i in range(max(args.profile_steps, 1)):
-            one(i)
+        for i in range(max(args.profile_steps, 1) if args.index_stats else 1):
+            if args.workload == "c2":
+                one(i)
+            else:
+                gk = mixed[i % N_BATCHES][0]
+                tree.search_batch(gk, vals[:gk.numel()], found[:gk.numel()])
         torch.cuda.synchronize()
         idx = tree.index_stats()
         tree.profile(False)
         g_ = max(idx["gets"], 1)
         idx.update({k + "_per_get": round(idx[k] / g_, 4)
-                    for k in ("start_internal", "right_moves", "page_hops", "entry_reads")})
+                    for k in ("start_internal", "right_moves", "page_hops", "entry_reads",
+                              "dir_fp_hits")})
     if c1 is not None:
         # C1 on the host cores, after every GPU measurement (the oracle's
         # build has run beside them)
@@ -608,6 +616,12 @@ def main():
     q_per_launch = prof["queries"] / max(prof["calls"], 1)
     page_walk = args.sort == "on"  # SHM_FLAG_SORT_GETS: ordered, whole pages (k_get)
     bpg = ALG_BYTES_PER_GET if page_walk else ALG_BYTES_PER_GET_SUM
+    fp_frac = None
+    if not page_walk and idx is not None and idx["gets"]:
+        # a get answered from the directory's fingerprints needs two random
+        # lines (directory entry, entry), any other three (+ summary line)
+        fp_frac = idx["dir_fp_hits"] / idx["gets"]
+        bpg = round(ALG_BYTES_PER_GET_SUM - 128 * fp_frac, 1)
     achieved = q_per_launch * bpg / (walk_ms * 1e-3) / 1e9 if walk_ms else 0.0
     traffic = None
     if args.workload == "c2" and args.start == "dir":
@@ -713,11 +727,19 @@ def main():
         if args.workload == "c2":
             step_s = elapsed / args.steps
             rf = out["roofline"]
-            rf["alg_bytes_note"] = (
-                "%d B/get: %s" % (bpg, "the summary walk's three random 128 B lines (directory "
-                                  "entry, leaf summary, entry) + 8 B key + 8 B value, DESIGN §3's "
-                                  "redefinition of SURVEY §8d's 1040 B whole-leaf read"
-                                  if not page_walk else "SURVEY §8d (1 KB leaf + key + value)"))
+            if page_walk:
+                note = "SURVEY §8d (1 KB leaf + key + value)"
+            elif fp_frac is not None:
+                note = ("the summary walk's random 128 B lines, two (directory entry, entry) "
+                        "for the gets the directory's fingerprints answered (dir_fp_frac of "
+                        "them) and three (+ leaf summary) for the rest, + 8 B key + 8 B value: "
+                        "DESIGN §3's redefinition of SURVEY §8d's 1040 B whole-leaf read")
+            else:
+                note = ("the summary walk's three random 128 B lines (directory entry, leaf "
+                        "summary, entry) + 8 B key + 8 B value, DESIGN §3's redefinition of "
+                        "SURVEY §8d's 1040 B whole-leaf read")
+            rf["alg_bytes_note"] = "%s B/get: %s" % (bpg, note)
+            rf["dir_fp_frac"] = round(fp_frac, 4) if fp_frac is not None else None
             rf["reference_bytes_frac"] = (round(rf["reference_bytes_GBps"] / HBM_PEAK_GBS, 4)
                                           if rf["reference_bytes_GBps"] else None)
             # the timed steps themselves (two walks in flight on two streams):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 6
+#define SHM_ABI_VERSION 7
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -266,6 +266,8 @@ typedef struct shm_index_stats_t {
   uint64_t page_hops;       /* pages walked from their own bytes */
   uint64_t entry_reads;     /* leaf entries read (fingerprint matches) */
   uint64_t hits;            /* queries found */
+  uint64_t dir_fp_hits;     /* found through the directory entry's copy of
+                               the leaf's fingerprints (no summary line) */
 } shm_index_stats_t;
 int shm_index_stats(shm_tree *t, shm_index_stats_t *out, int reset);
 

@@ -80,7 +80,7 @@ class ShermanError(RuntimeError):
 
 class ShmIndexStats(ctypes.Structure):
     _fields_ = [(f, u64) for f in ("gets", "start_internal", "right_moves", "page_hops",
-                                   "entry_reads", "hits")]
+                                   "entry_reads", "hits", "dir_fp_hits")]
 
 
 class ShmProfile(ctypes.Structure):
@@ -100,7 +100,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 6  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 7  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [

@@ -481,7 +481,8 @@ __global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
   if (a.stats) {  // wave-uniform; every lane of the wave is here
     const uint32_t v[kIdxStats] = {wave_sum32(act && k != kKeyMax ? 1u : 0u), wave_sum32(c_int),
                                    wave_sum32(c_right), wave_sum32(c_hops), wave_sum32(c_ent),
-                                   wave_sum32(act && val != kValueNull ? 1u : 0u)};
+                                   wave_sum32(act && val != kValueNull ? 1u : 0u),
+                                   wave_sum32(hit ? 1u : 0u)};
     if (lane_id() == 0)
       for (int j = 0; j < kIdxStats; ++j)
         if (v[j]) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + j), v[j]);

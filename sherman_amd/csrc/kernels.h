@@ -73,6 +73,7 @@ enum IdxStat {
   kIdxPageHops,        // pages walked from their own bytes (internal or unsummarised)
   kIdxEntryReads,      // leaf entries read (fingerprint matches)
   kIdxHits,            // queries found
+  kIdxDirFp,           // found through the directory entry's fingerprints
   kIdxStats
 };
 // top-of-tree table for the LDS replica: every page of the deepest level

@@ -1679,6 +1679,7 @@ int shm_index_stats(shm_tree* t, shm_index_stats_t* out, int reset) {
   out->page_hops = v[dev::kIdxPageHops];
   out->entry_reads = v[dev::kIdxEntryReads];
   out->hits = v[dev::kIdxHits];
+  out->dir_fp_hits = v[dev::kIdxDirFp];
   if (reset) HIP_OK(hipMemset(t->idx_stats, 0, sizeof(v)));
   return SHM_OK;
 }

@@ -1091,9 +1091,14 @@ def test_get_start_modes_and_index_stats(lib_ok, start):
         ov, of = orc.search_batch(probe)
         assert_same(probe, ov, of, gv, gf)
         assert st["gets"] == probe.size and st["hits"] == int(of.sum())
+        assert st["dir_fp_hits"] <= st["hits"], st
         if start == "dir":
             assert st["start_internal"] < probe.size // 100, st
+            # most prefixes lie inside one leaf: their gets are answered from
+            # the directory entry's fingerprints (the misses never are)
+            assert st["dir_fp_hits"] > st["hits"] // 4, st
         else:
+            assert st["dir_fp_hits"] == 0, st
             assert st["start_internal"] == probe.size, st
             assert st["page_hops"] >= probe.size * (1 if start == "lds" else 2), st
             # the replica's page is the one holding k (no walk along a level)
