@@ -325,8 +325,11 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   return v;
 }
 
+// 6 waves per SIMD (<= 80 VGPRs): with the directory's fingerprints a get's
+// chain is two requests, and more gets in flight pay (C2 +2 % against 5,
+// 8 no better; a same-box A/B)
 template <int TPB>
-__global__ __launch_bounds__(TPB) void k_get_sum(WalkArgs a) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k_get_sum(WalkArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_top[];  // top_n x (8 + 4) B
   const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
   const uint32_t tn = a.top_n;
