@@ -585,7 +585,8 @@ def main():
     prof = tree.profile_read(reset=True)
     tree.profile(False)
     idx = None
-    if args.workload in ("c2", "c3") and args.sort != "on":
+    if args.workload in ("c2", "c3") and args.sort != "on" and (args.profile_steps > 0 or
+                                                                args.index_stats):
         # the walk's index statistics over one more batch: how many gets the
         # directory's fingerprints answered (two lines instead of three: the
         # algorithmic bytes per get below)
