@@ -1016,6 +1016,9 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
   };
   stamp();
+  // per-block clocks (diagnostic): this block's start, and its end below
+  uint64_t* bclk = a.stamps && b < 256 && t == 0 ? a.stamps + kUpperStamps + 8 * 256 + b : nullptr;
+  if (bclk) bclk[0] = wall_clock64();
   Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
   const uint64_t cursor0 = sb->next_page;
   uint32_t root_level = (uint32_t)sb->root_level;
@@ -1070,6 +1073,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   if (total == 0 && *a.n_del == 0 && !a.force_abort) {
     if (b == 0 && t == 0) sb->batches = a.batch;
     stamp();
+    if (bclk) bclk[256] = wall_clock64();
     return;
   }
   bool ok = true;
@@ -1272,6 +1276,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     s_flag = d == nb - 1;
   }
   __syncthreads();
+  if (bclk) bclk[256] = wall_clock64();
   if (s_flag && t == 0) {
     // superblock (device-authoritative) and its host mirror
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

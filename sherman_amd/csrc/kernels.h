@@ -252,7 +252,9 @@ struct UpperArgs {
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins
-constexpr int kStampWords = kUpperStamps + 8 * 256;
+// + k_bin_unique's 7 x 256 phase words, then k_upper's per-block start (row 8)
+// and end (row 9) clocks
+constexpr int kStampWords = kUpperStamps + 10 * 256;
 uint32_t upper_blocks();
 // k_upper's blocks (one per CU, 512 threads) fit the device at all
 bool upper_resident();
@@ -423,6 +425,9 @@ struct RangeArgs {
   // slotted scans (shm_range_query_slots, nullable): += scans whose count
   // passed stage_cap, |= this launch's error bits (the caller zeroes them)
   uint64_t* status;
+  // 1: leaf reads issued ahead from the directory's list of the scan's
+  // leaves (range.hip range_plan); 0: along the sibling chain only
+  uint32_t plan;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // x[i] += c for i < n

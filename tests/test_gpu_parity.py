@@ -388,6 +388,62 @@ def test_range_query_vs_oracle(lib_ok, max_batch, cap, leaf_dir):
     t.close()
 
 
+def test_range_scan_plan_edges(lib_ok):
+    """Range scans whose directory plan (range.hip range_plan) meets each
+    entry form: spread keys (one-leaf fingerprint entries and entries of two
+    to four leaves) next to a dense run of consecutive keys (prefixes of more
+    than four leaves: the entry names an internal page, so the plan ends
+    there and the walk goes on along the sibling chain); scans that end at
+    the key space's top (past the directory's last prefix), scans inside one
+    leaf, scans of exactly one key, and scans from below the smallest key.
+    Counts and values against the oracle, exact leaf / slot order against
+    the reference scan over the GPU's own pages."""
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 17)
+    orc = OracleTree(256 << 20)
+    spread = hashed_keys(1, 60001)
+    c0 = U64(0x7123456789A00000)
+    dense = c0 + np.arange(20000, dtype=U64) * U64(3)
+    ks = np.unique(np.concatenate([spread, dense]))
+    vs = ks ^ U64(0x5A5A)
+    vs[vs == 0] = U64(1)
+    gpu_insert(t, ks, vs)
+    orc.apply_batch(ks, vs)
+    rng = np.random.default_rng(23)
+    probe = ks[rng.integers(0, ks.size, 4096)]
+    assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))  # builds the directory
+    pick = ks[rng.integers(0, ks.size, 300)]
+    lo = np.concatenate([
+        c0 - (U64(1) << U64(50)) * rng.integers(1, 8, 40).astype(U64),  # into the dense run
+        dense[rng.integers(0, dense.size, 40)],                          # inside it
+        pick,                                                            # anywhere
+        pick[:40],                                                       # one key
+        np.array([0, 5, int(ks[-1]), int(ks[0])], dtype=U64)])
+    hi = np.concatenate([
+        c0 + U64(3 * 500) * rng.integers(1, 8, 40).astype(U64),
+        lo[40:80] + U64(3 * 300),
+        pick + (U64(1) << U64(44)) * rng.integers(0, 512, 300).astype(U64),
+        pick[:40],
+        np.array([(1 << 64) - 1, 4, (1 << 64) - 1, int(ks[0])], dtype=U64)])
+    hi[hi < lo] = U64((1 << 64) - 1)
+    hi[-3] = U64(4)  # from > to: empty
+    counts, vals = t.range_query_batch(dev(lo), dev(hi))
+    counts = counts.cpu().numpy()
+    vals = host(vals)
+    img, root = t.dump_image()
+    same_pages = OracleTree(image=img, root_ptr=root)
+    off = 0
+    for i in range(lo.size):
+        ref, n = orc.range_query(int(lo[i]), int(hi[i]), cap=120000)
+        assert counts[i] == n, i
+        ref_img, n_img = same_pages.range_query(int(lo[i]), int(hi[i]), cap=120000)
+        assert n_img == n and np.array_equal(vals[off:off + n], ref_img), i
+        assert np.array_equal(np.sort(vals[off:off + n]), np.sort(ref)), i
+        off += n
+    same_pages.close()
+    orc.close()
+    t.close()
+
+
 def test_range_query_slots_vs_oracle(lib_ok):
     """shm_range_query_slots (a buffer per scan, Tree::range_query(from, to,
     buffer) batched): every scan's count and its values in the reference's
@@ -779,6 +835,24 @@ def test_leaf_dir_stale_after_splits(lib_ok):
         orc.apply_batch(add, av)
         probe = np.concatenate([add, add + U64(1 << 20), base[rng.integers(0, n0, 30000)]])
         assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))
+        # range scans over the split leaves: the directory's plan of a scan
+        # (range.hip range_plan) still names the pre-split leaves, so the
+        # walk must leave the plan where a sibling pointer names a new page
+        slo = np.concatenate([anchors - np.minimum(anchors, U64(5)),
+                              base[rng.integers(0, n0, 200)]])
+        span = np.concatenate([np.full(60, 200, dtype=U64),
+                               (U64(1) << U64(52)) * rng.integers(1, 8, 200).astype(U64)])
+        shi = slo + span
+        shi[shi < slo] = U64((1 << 64) - 1)
+        counts, vals = t.range_query_batch(dev(slo), dev(shi))
+        counts = counts.cpu().numpy()
+        vals = host(vals)
+        off = 0
+        for i in range(slo.size):
+            ref, n = orc.range_query(int(slo[i]), int(shi[i]), cap=60000)
+            assert counts[i] == n
+            assert np.array_equal(np.sort(vals[off:off + n]), np.sort(ref))
+            off += n
         if step == 0:
             assert pages0 < t.stats()["pages_used"] <= pages0 + pages0 // 32
     assert t.stats()["pages_used"] > pages0

@@ -32,7 +32,7 @@ def main():
     fn = lib.shm__upper_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     fn(t.h, 1, None)
-    out = (ctypes.c_uint64 * (32 + 8 * 256))()
+    out = (ctypes.c_uint64 * (32 + 10 * 256))()
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     for name, zn in (("c5", 2 * n), ("c3", n)):
@@ -57,6 +57,19 @@ def main():
                 v = [(x - t0) / 100.0 for x in bs[p] if x]
                 row.append("%.1f/%.1f" % (sum(v) / max(len(v), 1), max(v) if v else 0))
             print("   bin_unique phases (mean/max us):", " ".join(row), flush=True)
+            # k_upper per block: start and end clocks since block 0's first stamp
+            st = [int(out[32 + 8 * 256 + x]) for x in range(256)]
+            en = [int(out[32 + 9 * 256 + x]) for x in range(256)]
+            pairs = [(a_, b_) for a_, b_ in zip(st, en) if a_ and b_ >= a_]
+            if pairs:
+                s0 = ts[0]
+                ss = sorted((a_ - s0) / 100.0 for a_, _ in pairs)
+                ee = sorted((b_ - s0) / 100.0 for _, b_ in pairs)
+                q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))]  # noqa: E731
+                print("   k_upper blocks (us since block 0's start): start min/p50/max "
+                      "%.1f/%.1f/%.1f, end min/p50/p90/max %.1f/%.1f/%.1f/%.1f" %
+                      (ss[0], q(ss, 0.5), ss[-1], ee[0], q(ee, 0.5), q(ee, 0.9), ee[-1]),
+                      flush=True)
     fn(t.h, 0, None)
     t.close()
 
