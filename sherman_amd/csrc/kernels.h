@@ -425,9 +425,6 @@ struct RangeArgs {
   // slotted scans (shm_range_query_slots, nullable): += scans whose count
   // passed stage_cap, |= this launch's error bits (the caller zeroes them)
   uint64_t* status;
-  // 1: leaf reads issued ahead from the directory's list of the scan's
-  // leaves (range.hip range_plan); 0: along the sibling chain only
-  uint32_t plan;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // x[i] += c for i < n

@@ -905,16 +905,6 @@ int check_image(const uint8_t* img, uint64_t bytes, uint64_t root, uint16_t node
   return 0;
 }
 
-// range scans issue their leaf reads from the directory's plan
-// (SHM_RANGE_PLAN=0: along the sibling chain only, the A/B)
-bool range_plan_on() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_RANGE_PLAN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to, uint64_t n,
                           uint64_t* counts, const uint64_t* offsets, uint64_t* vals) {
   dev::RangeArgs a{};
@@ -931,7 +921,6 @@ dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to,
   a.err = t->d_err;
   a.vals_cap = ~0ull;
   a.leaf_hw = t->leaf_hw;
-  a.plan = range_plan_on() ? 1u : 0u;
   set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
   return a;
 }

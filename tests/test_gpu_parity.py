@@ -389,11 +389,11 @@ def test_range_query_vs_oracle(lib_ok, max_batch, cap, leaf_dir):
 
 
 def test_range_scan_plan_edges(lib_ok):
-    """Range scans whose directory plan (range.hip range_plan) meets each
-    entry form: spread keys (one-leaf fingerprint entries and entries of two
-    to four leaves) next to a dense run of consecutive keys (prefixes of more
-    than four leaves: the entry names an internal page, so the plan ends
-    there and the walk goes on along the sibling chain); scans that end at
+    """Range scans whose start meets each leaf-directory entry form: spread
+    keys (one-leaf fingerprint entries and entries of two to four leaves)
+    next to a dense run of consecutive keys (prefixes of more than four
+    leaves: the entry names an internal page, so the scan descends from it
+    before it walks the sibling chain); scans that end at
     the key space's top (past the directory's last prefix), scans inside one
     leaf, scans of exactly one key, and scans from below the smallest key.
     Counts and values against the oracle, exact leaf / slot order against
@@ -835,9 +835,9 @@ def test_leaf_dir_stale_after_splits(lib_ok):
         orc.apply_batch(add, av)
         probe = np.concatenate([add, add + U64(1 << 20), base[rng.integers(0, n0, 30000)]])
         assert_same(probe, *orc.search_batch(probe), *gpu_search(t, probe))
-        # range scans over the split leaves: the directory's plan of a scan
-        # (range.hip range_plan) still names the pre-split leaves, so the
-        # walk must leave the plan where a sibling pointer names a new page
+        # range scans over the split leaves: the stale directory still names
+        # the pre-split leaves, so a scan's start may lie left of its key and
+        # the walk must take the new pages from the sibling pointers
         slo = np.concatenate([anchors - np.minimum(anchors, U64(5)),
                               base[rng.integers(0, n0, 200)]])
         span = np.concatenate([np.full(60, 200, dtype=U64),
