@@ -208,9 +208,26 @@ int dalloc(T** p, uint64_t count) {
 // any HIP API; t->stream is used only for create / image transfers.
 hipStream_t pick(void* s) { return (hipStream_t)s; }
 
+// Cross-stream ordering events of one device: recording one needs no
+// system-scope release and waiting on one no system-scope acquire (the
+// streams share the device's memory; the host reads device results through
+// copies or the read-back kernel's own system-scope fence, never through
+// these events).  Default HIP events fence at system scope: a write-back of
+// the L2s at every record, measured as 12-22 us gaps around each C5 step's
+// cross-stream wait (tools/c5_trace.sh).  SHM_EVENT_SYSFENCE=1: the default
+// events (the A/B).
+unsigned event_flags() {
+  static const unsigned f = [] {
+    const char* e = getenv("SHM_EVENT_SYSFENCE");
+    return (e && e[0] == '1') ? (unsigned)hipEventDisableTiming
+                              : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+  }();
+  return f;
+}
+
 hipEvent_t new_event() {
   hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess) return nullptr;
   return e;
 }
 
