@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 7
+#define SHM_ABI_VERSION 8
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -130,9 +130,12 @@ int shm_search_batch(shm_tree *t, const uint64_t *keys, uint64_t n,
  * kKeyMax (the max_batch chunk holding it is rejected whole; the call's other
  * chunks, before and after it, are applied), SHM_ENOMEM if the arena ran out
  * (the splits that did not fit are left unapplied), SHM_EIO on a device fault
- * (a chunk whose split propagation stopped keeps its leaf splits linked by
- * sibling pointers, B-link reachable, and drops its parent updates and
- * deletes; later chunks run normally). */
+ * or a tree inconsistency the kernels detected (shm_last_error names the
+ * bits and the chunk that first saw them).  A chunk whose split propagation
+ * gave up waiting (a hand-off bound) is completed in the same launch by its
+ * last block alone, before any later call reads the tree (counted in
+ * shm_error_t.resumed; not an error), as the reference always completes a
+ * parent insert (src/Tree.cpp:973-988). */
 int shm_insert_batch(shm_tree *t, const uint64_t *keys, const uint64_t *vals,
                      uint64_t n, void *stream);
 /* The same batch queued on `stream` without any host wait (the reference's
@@ -223,6 +226,25 @@ int shm_load_image(shm_tree *t, const void *host_buf, uint64_t bytes,
 int shm_check(shm_tree *t, uint64_t *n_leaves, uint64_t *n_internal,
               uint64_t *n_keys);
 int shm_synchronize(shm_tree *t);
+/* The device error block as the last synchronising call that found bits in
+ * it read it (reset = 1 clears this record).  Errors of asynchronous calls
+ * surface at the next synchronising call, whichever it is: `chunk` names the
+ * insert chunk that first saw them, so a caller that noted shm_last_chunk()
+ * after each async insert knows which batch failed (the reference asserts at
+ * the failing operation instead, src/Tree.cpp:220-227, 332-337). */
+typedef struct shm_error_t {
+  uint32_t bits;     /* device error bits (0 = none was read) */
+  uint32_t chunk;    /* insert chunk that first saw them (0: none, e.g. a
+                        search's walk bound) */
+  int32_t status;    /* the status that call returned */
+  uint32_t resumed;  /* chunks whose split propagation gave up waiting and
+                        was completed by the launch's last block alone
+                        (cumulative) */
+} shm_error_t;
+int shm_last_error(shm_tree *t, shm_error_t *out, int reset);
+/* id of the last insert chunk queued on the handle (1, 2, ...; a batch of n
+ * ops is ceil(n / max_batch) chunks) */
+uint32_t shm_last_chunk(shm_tree *t);
 /* Copy `bytes` (a multiple of 4, <= 1024) of device memory at `src` to
  * host_out once the work queued on `stream` before it has produced them,
  * through the library's zero-copy read-back (one-wave kernel into mapped
@@ -304,11 +326,15 @@ int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *p
  * rank passes the same n).  Keys past their run's slot are answered by an
  * exact second round that end() runs after one read-back of the counts: no
  * lookup is dropped.  A routed insert: stable bucketing, each owner's run
- * in a slot of max_batch / P (kKeyMax padding the receiver skips), keys /
- * values / counts exchanged, queued as one insert on the owner with no host
- * wait (rank-major batch order across ranks); a run's tail past its slot is
- * sent and applied by the next call on the shard (or shm_shard_synchronize)
- * before anything else.  Device pointers; n <= the local tree's max_batch. */
+ * in a slot of max_batch / P (kKeyMax padding the receiver skips; a batch
+ * holding kKeyMax itself routes nothing and is reported as SHM_EINVAL by the
+ * next synchronising call), keys / values / counts exchanged, queued as one
+ * insert on the owner with no host wait.  Each rank's ops apply in its own
+ * batch order; across ranks the slots apply in rank order, and a run's tail
+ * past its slot is sent and applied by the next call on the shard (or
+ * shm_shard_synchronize) before anything else, after every rank's slots: one
+ * valid linearisation of the ranks' concurrent batches.  Device pointers;
+ * n <= the local tree's max_batch. */
 typedef struct shm_shard shm_shard;
 /* rank 0 makes the id (NCCL_UNIQUE_ID_BYTES = 128), the caller broadcasts it */
 int shm_nccl_unique_id(void *id_out, uint64_t bytes);

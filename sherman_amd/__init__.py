@@ -78,6 +78,10 @@ class ShermanError(RuntimeError):
         super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
 
 
+class ShmError(ctypes.Structure):
+    _fields_ = [("bits", u32), ("chunk", u32), ("status", ctypes.c_int32), ("resumed", u32)]
+
+
 class ShmIndexStats(ctypes.Structure):
     _fields_ = [(f, u64) for f in ("gets", "start_internal", "right_moves", "page_hops",
                                    "entry_reads", "hits", "dir_fp_hits")]
@@ -100,7 +104,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 7  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 8  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -128,6 +132,8 @@ _SIGNATURES = [
     ("shm_check", ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     ("shm_synchronize", ctypes.c_int, [vp]),
     ("shm_read_words", ctypes.c_int, [vp, vp, u64, vp, vp]),
+    ("shm_last_error", ctypes.c_int, [vp, ctypes.POINTER(ShmError), ctypes.c_int]),
+    ("shm_last_chunk", u32, [vp]),
     ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
     ("shm_index_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmIndexStats), ctypes.c_int]),
@@ -471,6 +477,18 @@ class Tree:
     def synchronize(self):
         _check(lib().shm_synchronize(self.h), "synchronize")
 
+    def last_error(self, reset=False):
+        """shm_last_error: the device error block as the last synchronising
+        call that found bits read it (bits, the chunk that first saw them, the
+        status returned, resumed chunks so far)."""
+        e = ShmError()
+        _check(lib().shm_last_error(self.h, ctypes.byref(e), 1 if reset else 0), "last_error")
+        return {f: getattr(e, f) for f, _ in ShmError._fields_}
+
+    def last_chunk(self):
+        """Id of the last insert chunk queued (shm_last_chunk)."""
+        return int(lib().shm_last_chunk(self.h))
+
     def stats(self):
         s = ShmStats()
         _check(lib().shm_stats(self.h, ctypes.byref(s)), "stats")
@@ -575,6 +593,8 @@ _HOOKS = [
     ("shm__local_group_create", ctypes.c_int, [u32, ctypes.POINTER(vp)]),
     ("shm__local_group_destroy", ctypes.c_int, [vp]),
     ("shm__shard_create_local", ctypes.c_int, [vp, vp, u32, ctypes.POINTER(vp)]),
+    ("shm__upper_force", ctypes.c_int, [vp, u32]),
+    ("shm__hog", ctypes.c_int, [u32, u64, vp]),
 ]
 
 
@@ -699,5 +719,5 @@ def header_symbols(path=HEADER_PATH):
     """Names of every function declared in include/sherman_amd.h."""
     import re
     txt = open(path).read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char \*)\s*(shm_\w+)\s*\(",
+    return sorted(set(re.findall(r"^\s*(?:int|uint32_t|uint64_t|const char \*)\s*(shm_\w+)\s*\(",
                                  txt, re.M)))

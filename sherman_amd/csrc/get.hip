@@ -104,7 +104,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_get(WalkArgs a) {
     const uint64_t pend = ballot(!done);
     if (pend == 0) break;
     if (++rounds > kMaxRounds) {
-      err |= kErrRounds;
+      err |= kErrGetHops;
       break;
     }
     // run heads: first lane of each run of equal page pointers
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
     int retries = 0;
     for (int hop = 0; !hit; ++hop) {
       if (hop > kMaxRounds) {
-        err |= kErrRounds;
+        err |= kErrGetHops;
         break;
       }
       if (!ptr_ok(ptr, a.node, a.arena_bytes)) {

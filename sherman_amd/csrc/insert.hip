@@ -8,32 +8,24 @@
 // set of flagged leaf segments (seg_P > 1: the page would reach 54 entries)
 // whose per-range new-page counts it accumulated in UpperCtl.
 //
-// k_upper is ONE persistent launch (one block per CU, all resident) that
-// finishes the batch.  Work is split by block range (the upsert kernel
-// assigns segment g to range g * nb / ns and counts its new pages there), so
-// a block finds its global page bases from the per-range counts alone and a
-// grid barrier is needed only where a level hands its separators to the
-// next one:
-//   leaf level     P2  per block: ordered scan of its range's new-page counts
-//                      -> its split segments and their first new page
-//                  P3  the block's waves: build new right siblings (k-way
-//                      split, ceil(T / 36) pages), each emitting its separator
-//                      and the parent it belongs to (a header walk from the
-//                      root); then page 0 of each split segment is rewritten
-//                      in place (set_consistent: front++ , rear = front) once
-//                      every sibling builder has read the old page (a per-
-//                      segment counter)
-//                  --- grid barrier ---
-//   level L >= 1   I1  per block: segment heads of its separator range, one
-//                      wave per head: lock the page (HBM lock table), plan T
-//                      and P (in place if T <= 60, else ceil((T + 1) / 41))
-//                  --- grid barrier ---
-//                  I2  per block: its dense segment list and page bases
-//                  I3  the block's waves: build / rewrite as for leaves
-//                  --- grid barrier, only if the level made separators ---
-//   deletes            every wave: Tree::del of the chunk's deletes
-// Lock words are epoch tagged (take_word below): nothing is released page by
-// page; the next chunk's larger tag releases them all.
+// k_upper is one launch per chunk that finishes the batch.  Work is split
+// into phases (the leaf level, then each internal level, then the deletes);
+// a phase whose results a later one reads hands its tasks out by ticket and
+// ends at a hand-off (see "phase tickets and hand-offs" below), so no phase
+// needs the launch's blocks to be resident together:
+//   leaf level     per block: ordered scan of the per-range new-page counts;
+//                  waves build new right siblings (k-way split, ceil(T / 36)
+//                  pages) and rewrite page 0 of each split in place
+//                  (set_consistent: front++, rear = front) once every sibling
+//                  builder has read the old page (a per-segment counter);
+//                  small splits take their separators up at once (propagate)
+//                  --- hand-off, when a later phase needs the leaves ---
+//   level L >= 1   block tasks: runs of separators with one parent, one wave
+//                  per run under the parent's exclusive lock word: merged in
+//                  place if T <= 60, else split into ceil((T + 1) / 41) pages
+//                  --- hand-off ---
+//   deletes        every wave: Tree::del of the chunk's deletes
+// Lock words are epoch tagged (lock_excl below).
 // Pages come from a device bump cursor (the superblock's next_page; the
 // reference's LocalAllocator bump, include/LocalAllocator.h:21-43), checked
 // against the arena capacity before each level.  The root page never moves:
@@ -54,7 +46,6 @@ namespace {
 
 constexpr int kUpT = 512;                  // threads per k_upper block
 constexpr int kUpWaves = kUpT / kWave;     // 8 waves
-constexpr uint32_t kBarrierSpins = 1u << 22;
 constexpr uint32_t kFanSpins = 1u << 22;
 
 struct WaveLds {
@@ -73,18 +64,12 @@ __device__ __forceinline__ uint32_t lock_index(uint64_t page, uint32_t n) {
 }
 
 // Lock words (the reference's lock table, Tree.cpp:205-264) are epoch
-// tagged: a chunk takes a word with atomic max of its tag (chunk number << 32;
-// a smaller value is an earlier chunk's hold, released when that chunk
-// retired) and never stores it back.  Every word a chunk holds is released at
-// once when the chunk retires, since the next chunk's tag is larger.  Only
-// the deletes need mutual exclusion inside a chunk: they hold tag | 1 and
-// hand the word back at the chunk's tag.
-__device__ __forceinline__ bool take_word(uint64_t* locks, uint32_t num, uint64_t page,
-                                          uint64_t tag) {
-  unsigned long long* w = reinterpret_cast<unsigned long long*>(locks) + lock_index(page, num);
-  return atomicMax(w, (unsigned long long)tag) <= (unsigned long long)tag;
-}
-
+// tagged: a word holding a value <= the chunk's tag (chunk number << 32) is
+// free for the chunk.  An exclusive hold is tag | 1 (lock_excl: one
+// atomicMax that returns a free value exactly when it took the word; the
+// deletes: a CAS of a free value), bounded by kMaxLockSpins (kErrLock), and
+// is handed back at the chunk's tag.  The next chunk's larger tag frees every
+// word of this one, including the upsert kernel's shared holds (upsert.hip).
 // the ops of one segment: keys [st, st + nb) of a sorted unique op array
 struct Ops {
   const uint64_t* key;
@@ -404,55 +389,79 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* red, uint32
   return base + incl - v;
 }
 
-// Grid barrier over all resident blocks, XCD-hierarchical
-// (MI355X_MICROARCH.md "barrier-xcd", ≈4 µs at 256 blocks against ≈7 for one
-// counter): every wave's stores performed, then one lane per block: release
-// fence, arrive on its XCD group's counter (blocks are dealt to the 8 XCDs
-// round-robin, b % 8; the grouping only affects speed); the group's last
-// arrival is its leader: it arrives on the top counter, polls it until all
-// groups are in, and publishes the generation to its group, whose other
-// blocks poll that word; acquire fence.  All counters are monotonic, so the
-// generation a barrier completes is derived from the value an arrival
-// returns.  Bounded: a spin past kBarrierSpins sets the abort word, which
-// releases every other block too; returns false then.
-__device__ __forceinline__ bool grid_sync(UpperCtl* ctl, uint32_t par, uint32_t nb, uint32_t* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// ---- phase tickets and hand-offs ----------------------------------------------
+// k_upper never needs its blocks to be resident together.  A phase whose
+// results a later phase reads hands its tasks out by ticket: a running wave
+// (or block) takes the next task of the phase with one atomic add, in
+// dispatch order, and counts it finished when its stores are done.  A block
+// that has run out of tickets waits at the hand-off until the phase's
+// finished count reaches its task count.  Every task it waits for was taken
+// by a wave that is running (tickets are only taken by running waves) and
+// that finishes it without waiting on anything but lock words held by other
+// running waves and, for a large split's page 0, the sibling builders of the
+// previous phase (all of whose tasks were taken before any task of this phase
+// was).  So the launch drains with any number of resident blocks, one
+// included: beside another process's persistent kernels, RCCL kernels or a
+// kernel holding most CUs (tests/test_gpu_parity.py::
+// test_split_insert_beside_cu_hog) -- the reference's parent insert likewise
+// waits only on a page lock (Tree.cpp:205-242, 973-988).  Phases nobody waits
+// on (C5's direct propagation) keep the static wave-per-task assignment.
+
+// the wave's next task: lane 0 takes `step` tickets of the phase at once
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* tk, uint32_t step) {
+  uint32_t v = 0;
+  if (lane_id() == 0) v = atomicAdd(tk, step);
+  return rl32(v, 0);
+}
+
+// the block's next task (thread 0 takes the ticket; slot: LDS broadcast)
+__device__ __forceinline__ uint32_t block_claim(uint32_t* tk, uint32_t* slot) {
+  __syncthreads();  // every thread has read the previous ticket
+  if (threadIdx.x == 0) *slot = atomicAdd(tk, 1u);
   __syncthreads();
+  return *slot;
+}
+
+constexpr uint32_t kHandoffSpins = 1u << 22;
+
+// the block's stores performed and released, then acquired by every thread
+// (the solo pass of the last block, which waits for nobody)
+__device__ __forceinline__ bool block_fence() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// Phase hand-off: the block adds the tasks it finished (`mine`, summed over
+// its threads' values) to the phase's count after its stores are performed
+// and released, then waits until `want` tasks are finished; acquire.  False
+// (every thread) when a wait gave up (kHandoffSpins, or another block gave
+// up, or force): the abort word tells every block to leave at its next
+// hand-off, and the launch's last block completes the chunk alone.
+__device__ __forceinline__ bool handoff(UpperCtl* ctl, uint32_t par, uint32_t ph, uint32_t mine,
+                                        uint32_t want, bool force, uint32_t* red,
+                                        uint32_t* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t sum = block_sum(mine, red);
   if (threadIdx.x == 0) {
-    const uint32_t nx = nb < 8u ? nb : 8u;
-    const uint32_t x = blockIdx.x % nx;
-    const uint64_t m = nb / nx + (x < nb % nx ? 1u : 0u);  // blocks of group x
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     uint32_t* abort = &ctl->abort[par][0];
-    const uint64_t old = __hip_atomic_fetch_add(&ctl->xbar[par][x][0], 1ull, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t e = old / m + 1;  // the generation this barrier completes
-    uint32_t ok = 1;
-    auto spin_until = [&](uint64_t* w, uint64_t want) {
-      for (uint32_t spin = 0;; ++spin) {
-        if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return;
-        if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-            spin > kBarrierSpins) {
-          __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          return;
-        }
+    uint32_t* d = &ctl->dn[par][ph][0];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (sum) __hip_atomic_fetch_add(d, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t ok = force ? 0u : 1u;
+    for (uint32_t spin = 0; ok; ++spin) {
+      if (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+      if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+          spin > kHandoffSpins)
+        ok = 0;
+      else
         __builtin_amdgcn_s_sleep(1);
-      }
-    };
-    if (old % m == m - 1) {
-      // leader: the group's releases happened before its arrivals
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      const uint64_t ot = __hip_atomic_fetch_add(&ctl->top[par][0], 1ull, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      spin_until(&ctl->top[par][0], (ot / nx + 1) * nx);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      __hip_atomic_store(&ctl->gen[par][x][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      spin_until(&ctl->gen[par][x][0], e);
     }
+    if (ok && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ok = 0;
+    if (!ok) __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *flag = ok;
   }
   __syncthreads();
@@ -530,7 +539,8 @@ __device__ __forceinline__ void fan_arrive(uint64_t* w, uint32_t tag) {
     old = prev;
   }
 }
-// wait until the word reads (tag, want)
+// wait until the word reads (tag, want); the builders it waits for took
+// their tasks (phase 0 tickets) before this wave took its phase-1 one
 __device__ __forceinline__ bool fan_in(uint64_t* cnt, uint32_t want, uint32_t tag) {
   const uint64_t target = ((uint64_t)tag << 32) | want;
   uint32_t ok = 1;
@@ -581,6 +591,8 @@ __device__ __forceinline__ void delete_key(const UpperArgs& a, uint64_t k, uint3
         err |= kErrInconsistent;
         break;
       }
+      // an internal page another wave rewrote: drop this XCD's stale lines
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       continue;
     }
     if (k >= h0.highest && h0.sibling != 0) {
@@ -891,10 +903,10 @@ __device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32
   }
 }
 
-// The block's share of level `level`'s separators (emitted unordered by
-// the level below), sorted by key in LDS, cut into runs of one parent hint,
-// one wave per run.  Shares of ceil(n / nb) (at most kLvlSort a round):
-// the few separators of C5's upper levels spread over as many blocks.
+// Chunk r of level `level`'s separators (emitted unordered by the level
+// below; chunks of `per` <= kLvlSort), sorted by key in LDS, cut into runs
+// of one parent hint, one wave per run.  With per = ceil(n / nb) the few
+// separators of C5's upper levels spread over as many blocks.
 constexpr uint32_t kLvlSort = 1024;
 struct LvlLds {
   uint64_t key[kLvlSort];
@@ -902,18 +914,20 @@ struct LvlLds {
   uint64_t hint[kLvlSort];
   uint32_t head[kLvlSort];
 };
-__device__ __forceinline__ void upper_level(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t* red,
-                            uint32_t n, uint32_t level, uint64_t base, uint64_t cap,
-                            uint32_t& err) {
-  const int t = threadIdx.x, wv = t >> 6;
-  const uint32_t b = blockIdx.x, nb = gridDim.x;
+__device__ __forceinline__ uint32_t level_per(uint32_t n, uint32_t nb) {
   const uint32_t share = (n + nb - 1) / nb;
-  const uint32_t per = share < kLvlSort ? share : kLvlSort;
+  return share < kLvlSort ? share : kLvlSort;
+}
+__device__ __forceinline__ void upper_chunk(const UpperArgs& a, WaveLds& L, LvlLds& S, uint32_t* red,
+                            uint32_t n, uint32_t per, uint32_t r, uint32_t level, uint64_t base,
+                            uint64_t cap, uint32_t& err) {
+  const int t = threadIdx.x, wv = t >> 6;
   const bool odd = (level & 1) != 0;
   const uint64_t* gk = odd ? a.sep_key[1] : a.sep_key[0];
   const uint64_t* gp = odd ? a.sep_ptr[1] : a.sep_ptr[0];
   const uint64_t* gh = odd ? a.ipage[1] : a.ipage[0];
-  for (uint32_t c0 = b * per; c0 < n; c0 += nb * per) {
+  {
+    const uint32_t c0 = r * per;
     const uint32_t cnt = n - c0 < per ? n - c0 : per;
     uint32_t m2 = 1;
     while (m2 < cnt) m2 <<= 1;
@@ -966,41 +980,45 @@ __device__ __forceinline__ void upper_level(const UpperArgs& a, WaveLds& L, LvlL
 }
 
 // ---------------------------------------------------------------------------
-// k_upper: one persistent launch per insert chunk, one 512-thread block per
-// CU (all resident: grid barriers).
+// k_upper: one launch per insert chunk, one 512-thread block per CU at most;
+// no phase needs the blocks to be resident together (tickets and hand-offs
+// above).
 //   prologue  per-range prefix sums of the upsert kernel's new-page counts
-//   leaf      splits into <= kSmallSplit pages: one wave builds all of a
-//             split's pages, siblings first and page 0 last (it holds the old
-//             page's survivors, so no fan-in); larger splits: their sibling
-//             pages spread over every wave of the grid, page 0 after the
-//             fan-in of its builders.
+//   leaf      phase 0 (large splits only): their sibling pages, four per
+//             ticket; phase 1, every split: a small one (<= kSmallSplit
+//             pages) built whole by one wave, siblings first and page 0 last
+//             (it holds the old page's survivors, so no fan-in); a large
+//             one's page 0 after the fan-in of its sibling builders
 //   direct    (every split small, C5's chunks) the wave then takes its
 //             split's separators up itself (propagate): parents under their
 //             exclusive words, a parent's split going one level further, the
-//             root growing in place -- no list, no grid barrier
+//             root growing in place -- no list and, unless deletes follow,
+//             no hand-off: splits are then dealt statically (wave w takes
+//             w, w + W, ...)
 //   otherwise each new leaf's separator goes to position (its global
 //             new-page index) of level 1's list: key order
-//   --- grid barrier ---
-//   level 1   runs of separators with one parent, one wave per run: the
-//             parent's epoch lock word, its survivors and the run merged,
-//             rewritten in place or split (pages by an atomic bump past the
-//             leaf level's), new separators to level 2's list
-//   --- grid barrier ---
-//   level >=2 each block's share of the separators (emitted unordered),
-//             sorted in LDS, runs of one parent under its exclusive word
-//   (--- grid barrier --- after every level: the next level's count)
-//   deletes   Tree::del of the chunk's deletes (after every split: a grid
-//             barrier in the direct case too)
-//   last      the last block to finish: the superblock and its host mirror
-// 4 waves per SIMD (<= 128 VGPRs): two blocks fit a CU, so the persistent
-// launches of two processes sharing a GPU can be resident together
+//   --- hand-off (phases 0 and 1) ---
+//   level 1   block tasks: separator range r of nb, runs of one parent, one
+//             wave per run: the parent's epoch lock word, its survivors and
+//             the run merged, rewritten in place or split (pages by an
+//             atomic bump past the leaf level's), new separators to level 2
+//   --- hand-off ---
+//   level >=2 block tasks: chunks of the level's separators (emitted
+//             unordered), sorted in LDS, runs of one parent under its
+//             exclusive word; a hand-off after every level
+//   deletes   Tree::del of the chunk's deletes, after every split
+//   last      the last block to finish: if a hand-off gave up, it runs the
+//             levels and the deletes again alone (idempotent); then the
+//             superblock and its host mirror
+// 4 waves per SIMD (<= 128 VGPRs): two blocks fit a CU.
 __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void k_upper(
     UpperArgs a) {
   __shared__ __attribute__((aligned(16))) WaveLds s_l[kUpWaves];
   __shared__ uint32_t s_red[kUpWaves];
   __shared__ uint32_t s_flag;
+  __shared__ uint32_t s_tk;  // the block's ticket
   __shared__ uint32_t s_list[kUpT];  // segment heads of one separator chunk
-  __shared__ __attribute__((aligned(16))) LvlLds s_lvl;  // levels >= 2: the block's share
+  __shared__ __attribute__((aligned(16))) LvlLds s_lvl;  // levels >= 2: one chunk
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t b = blockIdx.x, nb = gridDim.x;
   const uint64_t W = (uint64_t)nb * kUpWaves;
@@ -1020,26 +1038,26 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   uint64_t* bclk = a.stamps && b < 256 && t == 0 ? a.stamps + kUpperStamps + 8 * 256 + b : nullptr;
   if (bclk) bclk[0] = wall_clock64();
   Superblock* sb = reinterpret_cast<Superblock*>(a.arena);
+  const uint32_t par = a.par;
+  // the superblock as the chunk found it (the last block derives the new one
+  // from it and the chunk's counters)
   const uint64_t cursor0 = sb->next_page;
+  const uint64_t splits0 = sb->splits;
   uint32_t root_level = (uint32_t)sb->root_level;
   const uint64_t cap = sb->capacity_pages;
   uint32_t err = 0;
   const uint32_t ns = *a.ns_dev;
-  const uint32_t par = a.par;
-  // the other parity's counters and barrier words start the next chunk at 0
+  // the other parity's counters and hand-off words start the next chunk at 0
   for (uint64_t j = tid; j < (uint64_t)kMaxUpper; j += T) {
     ctl->leaf_np[par ^ 1][j] = 0;
     ctl->leaf_ns[par ^ 1][j] = 0;
     ctl->leaf_nb[par ^ 1][j] = 0;
   }
-  for (uint64_t j = tid; j < 8 * 16; j += T) {
-    (&ctl->xbar[par ^ 1][0][0])[j] = 0;
-    (&ctl->gen[par ^ 1][0][0])[j] = 0;
+  for (uint64_t j = tid; j < (uint64_t)kUpPhases * 32; j += T) {
+    (&ctl->tk[par ^ 1][0][0])[j] = 0;
+    (&ctl->dn[par ^ 1][0][0])[j] = 0;
   }
-  if (tid < 16) {
-    ctl->top[par ^ 1][tid] = 0;
-    ctl->lvl_sep[par ^ 1][tid] = 0;
-  }
+  if (tid < 16) ctl->lvl_sep[par ^ 1][tid] = 0;
   if (tid == 0) {
     ctl->abort[par ^ 1][0] = 0;
     ctl->alloc[par ^ 1][0] = 0;
@@ -1067,23 +1085,34 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     __syncthreads();
   }
+  const uint64_t n_del = *a.n_del;
   // nothing to split and nothing to delete (every op applied in place, C3's
   // chunks): the superblock's batch count is the only change, so block 0
   // writes it and no block waits for the others (no fan-in on `done`)
-  if (total == 0 && *a.n_del == 0 && !a.force_abort) {
-    if (b == 0 && t == 0) sb->batches = a.batch;
+  if (total == 0 && n_del == 0 && !a.force_abort) {
+    if (b == 0 && t == 0) {
+      sb->batches = a.batch;
+      // the chunk's kernels before this one have finished: attribute their
+      // error bits (tree.cpp check_err)
+      if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kErrKeyMax)
+        atomicCAS(a.err + 1, 0u, (uint32_t)a.batch);
+    }
     stamp();
     if (bclk) bclk[256] = wall_clock64();
     return;
   }
   bool ok = true;
   // every split small (C5's chunks): each wave takes its separators up
-  // itself (propagate), no level list, no grid barrier
+  // itself (propagate), no level list
   const bool direct = nbig == 0 && !a.no_direct;
   const bool grow0 = root_level == 0;  // the root is a leaf: its split grows the tree
   const bool fits = cursor0 + total + (grow0 ? 1u : 0u) <= cap;
   // pages past the leaf level's: the internal levels' bump allocator
   const uint64_t base = cursor0 + total + (grow0 ? 1u : 0u);
+  // a later phase reads the leaf level's results (level 1's list, or the
+  // deletes its pages): its tasks go by ticket and end at a hand-off
+  const bool wait_leaf = !direct || n_del != 0 || a.force_abort != 0;
+  uint32_t mine = 0;  // lane 0: the wave's finished tasks of the current phase
   if (total && !fits) {
     // arena exhausted: the flagged segments stay unapplied (reported)
     err |= kErrNoMem;
@@ -1092,42 +1121,50 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const uint64_t first = cursor0;          // arena page of global new page 0
     const uint64_t xroot = cursor0 + total;  // the root's left half (grow0)
     const uint32_t ftag = fan_tag(a.batch, 0);
-    // (a) sibling pages of the large splits, over every wave (none in C5)
-    for (uint32_t gp = (uint32_t)wid; nbig && gp < total; gp += (uint32_t)W) {
-      const uint32_t r = last_le(s_pnp, nb, gp);
-      uint32_t r0, r1, g, before;
-      block_range(ns, r, nb, r0, r1);
-      find_seg(a.seg_np, r0, r1, gp - s_pnp[r], false, g, before);
-      if (g >= r1) {
-        err |= kErrPlan;
-        continue;
-      }
-      if (a.seg_P[g] <= kSmallSplit) continue;  // built whole by (b)
-      const uint32_t pb = s_pnp[r] + before;
-      const int p = (int)(gp - pb) + 1;
-      const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
-      const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
-      const Hdr h = parse_hdr(w);
-      stage_page(L.page, w);
-      wave_lds_sync();
-      const Ops o = stage_ops(L, o0);
-      const int na = leaf_survivors(L, o);
-      // the old page 0 has been read: its rewrite may go ahead
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) fan_arrive(a.leaf_rd + g, ftag);
-      const SplitPage sp{p, (int)a.seg_P[g], a.seg_T[g], first + pb,
-                         new_ga(a.node, first + pb, p)};
-      const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
-      const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
-      if (lane == 0) {
-        a.sep_key[1][gp] = low;
-        a.sep_ptr[1][gp] = sp.dest;
-        a.ipage[1][gp] = par_pg;
+    // phase 0: sibling pages of the large splits (none in C5), four per
+    // ticket (nbig > 0 implies wait_leaf: always by ticket)
+    constexpr uint32_t kStepA = 4;
+    for (uint32_t g0 = nbig ? wave_claim(&ctl->tk[par][0][0], kStepA) : total; g0 < total;
+         g0 = wave_claim(&ctl->tk[par][0][0], kStepA)) {
+      for (uint32_t gp = g0; gp < g0 + kStepA && gp < total; ++gp) {
+        if (lane == 0) ++mine;
+        const uint32_t r = last_le(s_pnp, nb, gp);
+        uint32_t r0, r1, g, before;
+        block_range(ns, r, nb, r0, r1);
+        find_seg(a.seg_np, r0, r1, gp - s_pnp[r], false, g, before);
+        if (g >= r1) {
+          err |= kErrPlan;
+          continue;
+        }
+        if (a.seg_P[g] <= kSmallSplit) continue;  // built whole in phase 1
+        const uint32_t pb = s_pnp[r] + before;
+        const int p = (int)(gp - pb) + 1;
+        const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
+        const u32x4 w = load_page_slice(a.arena, ga_offset(a.seg_page[g]));
+        const Hdr h = parse_hdr(w);
+        stage_page(L.page, w);
+        wave_lds_sync();
+        const Ops o = stage_ops(L, o0);
+        const int na = leaf_survivors(L, o);
+        // the old page 0 has been read: its rewrite may go ahead
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) fan_arrive(a.leaf_rd + g, ftag);
+        const SplitPage sp{p, (int)a.seg_P[g], a.seg_T[g], first + pb,
+                           new_ga(a.node, first + pb, p)};
+        const uint64_t low = build_leaf_page(a, L, h, na, o, sp);
+        const uint64_t par_pg = grow0 ? a.root : parent_of(a, low, 1, &err);
+        if (lane == 0) {
+          a.sep_key[1][gp] = low;
+          a.sep_ptr[1][gp] = sp.dest;
+          a.ipage[1][gp] = par_pg;
+        }
       }
     }
-    // (b) every split: a small one whole (siblings, then page 0), a large
-    // one's page 0 once its sibling builders have read the old page
-    for (uint32_t k = (uint32_t)wid; k < nsplit; k += (uint32_t)W) {
+    // phase 1: every split -- a small one whole (siblings, then page 0), a
+    // large one's page 0 once its sibling builders have read the old page
+    uint32_t k = wait_leaf ? wave_claim(&ctl->tk[par][1][0], 1u) : (uint32_t)wid;
+    for (; k < nsplit; k = wait_leaf ? wave_claim(&ctl->tk[par][1][0], 1u) : k + (uint32_t)W) {
+      if (lane == 0) ++mine;
       const uint32_t r = last_le(s_pns, nb, k);
       uint32_t r0, r1, g, before;
       block_range(ns, r, nb, r0, r1);
@@ -1140,7 +1177,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       const int P = (int)a.seg_P[g];
       const uint64_t page = a.seg_page[g];
       const bool small = (uint32_t)P <= kSmallSplit;
-      if (!small && !fan_in(a.leaf_rd + g, (uint32_t)(P - 1), ftag)) err |= kErrLock;
+      if (!small && !fan_in(a.leaf_rd + g, (uint32_t)(P - 1), ftag)) err |= kErrFanIn;
       const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
       const u32x4 w = load_page_slice(a.arena, ga_offset(page));
       const Hdr h = parse_hdr(w);
@@ -1176,95 +1213,109 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
       if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err, grow0 ? 0ull : hint1);
     }
-    if (grow0) root_level = 1;
     stamp();
-    if (a.force_abort && b == 0 && t == 0)  // diagnostics: this launch stops here
-      __hip_atomic_store(&ctl->abort[par][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // level 1 reads every block's separators; with direct propagation only
-    // the deletes wait for the splits
-    if (!direct || *a.n_del || a.force_abort) ok = grid_sync(ctl, par, nb, &s_flag);
+    if (wait_leaf)
+      ok = handoff(ctl, par, 0, mine, (nbig ? total : 0u) + nsplit, a.force_abort != 0, s_red,
+                   &s_flag);
     stamp();
   }
 
-  // ---- level 1: runs of separators with one parent -----------------------------
-  if (ok && total && fits && !direct) {
+  // ---- internal levels: block tasks ------------------------------------------
+  // solo: the launch's last block alone, every task in order, no tickets or
+  // hand-offs (it completes what the hand-offs of the others abandoned)
+  auto run_levels = [&](bool solo) -> bool {
+    bool okl = true;
+    // level 1: runs of separators with one parent (range rr of nb)
     const uint64_t* skey = a.sep_key[1];
     const uint64_t* sptr = a.sep_ptr[1];
     const uint64_t* spg = a.ipage[1];
     const uint32_t nsep = total;
-    uint32_t r0, r1;
-    block_range(nsep, b, nb, r0, r1);
-    for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
-      const uint32_t i = c0 + (uint32_t)t;
-      const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
-      uint32_t th;
-      const uint32_t x = block_scan(head ? 1u : 0u, s_red, &th);
-      __syncthreads();
-      if (head) s_list[x] = i;
-      __syncthreads();
-      for (uint32_t hx = (uint32_t)wv; hx < th; hx += kUpWaves) {
-        const uint32_t hi = s_list[hx];
-        const uint64_t page = spg[hi];
-        // the run's end: first index past hi whose page differs
-        uint32_t e = hi + 1;
-        for (;;) {
-          const uint32_t j = e + (uint32_t)lane;
-          const uint64_t m = ballot(j >= nsep || spg[j] != page);
-          if (m) {
-            e += (uint32_t)ctz64(m);
-            break;
+    uint32_t done1 = 0, seq = 0;  // thread 0: the block's finished tasks
+    for (uint32_t rr = solo ? seq++ : block_claim(&ctl->tk[par][2][0], &s_tk); rr < nb;
+         rr = solo ? seq++ : block_claim(&ctl->tk[par][2][0], &s_tk)) {
+      if (t == 0) ++done1;
+      uint32_t r0, r1;
+      block_range(nsep, rr, nb, r0, r1);
+      for (uint32_t c0 = r0; c0 < r1; c0 += kUpT) {
+        const uint32_t i = c0 + (uint32_t)t;
+        const bool head = i < r1 && (i == 0 || spg[i] != spg[i - 1]);
+        uint32_t th;
+        const uint32_t x = block_scan(head ? 1u : 0u, s_red, &th);
+        __syncthreads();
+        if (head) s_list[x] = i;
+        __syncthreads();
+        for (uint32_t hx = (uint32_t)wv; hx < th; hx += kUpWaves) {
+          const uint32_t hi = s_list[hx];
+          const uint64_t page = spg[hi];
+          // the run's end: first index past hi whose page differs
+          uint32_t e = hi + 1;
+          for (;;) {
+            const uint32_t j = e + (uint32_t)lane;
+            const uint64_t m = ballot(j >= nsep || spg[j] != page);
+            if (m) {
+              e += (uint32_t)ctz64(m);
+              break;
+            }
+            e += kWave;
           }
-          e += kWave;
+          if (!ptr_ok(page, a.node, a.arena_bytes)) {
+            err |= kErrBadPtr;
+            continue;
+          }
+          // the run under the parent's exclusive word, B-link right moves as
+          // at the upper levels (a solo pass finds parents that split since
+          // the hint was taken); a short run staged in the wave's LDS
+          const uint32_t nr = e - hi;
+          if (nr <= (uint32_t)kWave) {
+            if ((uint32_t)lane < nr) {
+              L.o_key[lane] = skey[hi + lane];
+              L.o_val[lane] = sptr[hi + lane];
+            }
+            wave_lds_sync();
+            apply_run(a, L, L.o_key, L.o_val, 0, nr, page, 1, base, cap, err);
+          } else {
+            apply_run(a, L, skey, sptr, hi, e, page, 1, base, cap, err);
+          }
         }
-        if (!ptr_ok(page, a.node, a.arena_bytes)) {
-          err |= kErrBadPtr;
-          continue;
-        }
-        // the parent's word, held until the chunk retires (epoch tags)
-        uint32_t lk = 0;
-        if (lane == 0) lk = take_word(a.locks, a.num_locks, page, a.tag) ? 1u : 0u;
-        if (!rl32(lk, 0)) {
-          err |= kErrLock;
-          continue;
-        }
-        const u32x4 w = load_page_slice(a.arena, ga_offset(page));
-        const Hdr h = parse_hdr(w);
-        if (h.fver != h.rver_internal || h.leftmost == 0 || h.level != 1) {
-          err |= kErrInconsistent;  // left untouched
-          continue;
-        }
-        const Ops o = stage_ops(L, Ops{skey, sptr, hi, e - hi});
-        const int na = internal_survivors(L, w, h.last_index + 1, o);
-        apply_internal(a, L, h, na, o, page, 1, base, cap, err);
+        __syncthreads();
       }
-      __syncthreads();
     }
     stamp();
-    ok = grid_sync(ctl, par, nb, &s_flag);
+    okl = solo ? block_fence() : handoff(ctl, par, 2, done1, nb, false, s_red, &s_flag);
     stamp();
-    // ---- levels >= 2: the block's share, sorted, runs under exclusive words --
-    for (uint32_t level = 2; ok; ++level) {
-      const uint32_t n = __hip_atomic_load(&ctl->lvl_sep[par][level], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      if (n == 0) break;
+    // levels >= 2: chunks of the level's separators
+    for (uint32_t level = 2; okl; ++level) {
+      const uint32_t n0 = __hip_atomic_load(&ctl->lvl_sep[par][level], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (n0 == 0) break;
       if (level > (uint32_t)kMaxLevelOfTree) {
         err |= kErrRounds;
         break;
       }
-      upper_level(a, L, s_lvl, s_red, n < a.sep_cap ? n : (uint32_t)a.sep_cap, level, base, cap,
-                  err);
+      const uint32_t n = n0 < a.sep_cap ? n0 : (uint32_t)a.sep_cap;
+      const uint32_t per = level_per(n, nb);
+      const uint32_t nchunks = (n + per - 1) / per;
+      uint32_t dl = 0, sq = 0;
+      for (uint32_t rr = solo ? sq++ : block_claim(&ctl->tk[par][1 + level][0], &s_tk);
+           rr < nchunks; rr = solo ? sq++ : block_claim(&ctl->tk[par][1 + level][0], &s_tk)) {
+        if (t == 0) ++dl;
+        upper_chunk(a, L, s_lvl, s_red, n, per, rr, level, base, cap, err);
+      }
       stamp();
-      ok = grid_sync(ctl, par, nb, &s_flag);
+      okl = solo ? block_fence() : handoff(ctl, par, 1 + level, dl, nchunks, false, s_red, &s_flag);
       stamp();
     }
-  }
-  if (!ok) err |= kErrRounds;
+    return okl;
+  };
+  if (ok && total && fits && !direct) ok = run_levels(false);
+  if (!ok) err |= kErrHandoff;
   // the chunk's deletes, after every split (Tree::del, Tree.cpp:542-591):
   // the keys are located afresh, so pages that moved right are followed; the
-  // last level ended with a grid barrier, so no page is still being written
-  const uint64_t n_del = *a.n_del;
+  // leaf level ended with a hand-off, so no leaf is still being written.
+  // Nothing waits for them: dealt statically
   for (uint64_t i = wid; ok && i < n_del; i += W) delete_key(a, a.dk[i], L.page, err);
   if (err && lane == 0) atomicOr(a.err, err);
+  err = 0;
   stamp();
   // the last block to finish writes the superblock: every block's
   // allocations and root growth are in the counters by then
@@ -1273,11 +1324,33 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t d = __hip_atomic_fetch_add(&ctl->done[par][0], 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
-    s_flag = d == nb - 1;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_flag = (d == nb - 1 ? 1u : 0u) |
+             (d == nb - 1 && __hip_atomic_load(&ctl->abort[par][0], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                  ? 2u
+                  : 0u);
   }
   __syncthreads();
+  const uint32_t last = s_flag;
+  __syncthreads();
+  if (last & 2u) {
+    // A hand-off gave up (its wait bound, or force_abort).  Every block has
+    // finished, so every task any block took is done: this block alone runs
+    // the internal levels again from level 1 (re-inserting a separator a page
+    // already holds rewrites it unchanged) and the deletes (deleting an absent
+    // key changes nothing), so the chunk completes in this launch, before any
+    // later call reads the tree -- nothing is dropped (the reference always
+    // completes a parent insert, Tree.cpp:973-988).
+    block_fence();
+    if (total && fits && !direct) (void)run_levels(true);
+    for (uint64_t i = (uint64_t)wv; i < n_del; i += kUpWaves) delete_key(a, a.dk[i], L.page, err);
+    if (err && lane == 0) atomicOr(a.err, err);
+    block_fence();
+    if (t == 0) atomicAdd(a.err + 2, 1u);  // chunks completed this way (shm_last_error)
+  }
   if (bclk) bclk[256] = wall_clock64();
-  if (s_flag && t == 0) {
+  if ((last & 1u) && t == 0) {
     // superblock (device-authoritative) and its host mirror
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const uint64_t extra = total && fits ? __hip_atomic_load(&ctl->alloc[par][0], __ATOMIC_RELAXED,
@@ -1295,15 +1368,19 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
                       : 0ull;
     sb->next_page = cursor;
     sb->root_level = root_level;
-    sb->splits += made;
+    sb->splits = splits0 + made;
     sb->batches = a.batch;
     if (a.pub && cursor != cursor0) {  // the host mirror changes only with new pages
       __hip_atomic_store(a.pub + 1, cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.pub + 2, (uint64_t)root_level, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(a.pub + 3, sb->splits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.pub + 3, splits0 + made, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    // every block's error bits are in (released before its `done` arrival):
+    // the first chunk to see a bit other than kErrKeyMax names itself
+    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kErrKeyMax)
+      atomicCAS(a.err + 1, 0u, (uint32_t)a.batch);
   }
 }
 
@@ -1333,6 +1410,8 @@ uint32_t upper_blocks() {
   return nb;
 }
 
+// a block of k_upper fits a CU at all (nothing more is needed: no phase
+// waits for blocks that are not running)
 bool upper_resident() {
   int nb = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_upper, kUpT, 0) == hipSuccess &&
@@ -1340,8 +1419,8 @@ bool upper_resident() {
 }
 
 void launch_upper(const UpperArgs& a, hipStream_t s) {
-  // one block per CU: every block resident (grid barriers); 512 threads,
-  // ~20 KB of LDS
+  // one block per CU (fewer may be resident: tickets and hand-offs, above);
+  // 512 threads, ~66 KB of LDS
   hipLaunchKernelGGL(k_upper, dim3(upper_blocks()), dim3(kUpT), 0, s, a);
 }
 

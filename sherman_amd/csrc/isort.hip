@@ -131,6 +131,7 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
   if (bad) {
     // the chunk is rejected whole (k_bin_unique emits nothing) and reported
     atomicOr(err, kErrKeyMax);
+    atomicCAS(err + 1, 0u, tag);  // the first chunk with an error names itself
     *gate = tag;
   }
   __syncthreads();
@@ -328,7 +329,7 @@ __device__ void bin_prefix(uint64_t* lbw, uint32_t b, uint32_t tag, uint32_t ups
         w = __hip_atomic_load(lbw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((w >> 48) == tg) break;
         if (spin > (1u << 24)) {
-          atomicOr(err, kErrRounds);
+          atomicOr(err, kErrBinSpin);
           w = 0;
           break;
         }

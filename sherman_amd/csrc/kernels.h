@@ -111,17 +111,19 @@ void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.
 constexpr int kMaxUpper = 512;
+// k_upper's phases (insert.hip): tickets / completion counts per phase.
+// 0 = sibling pages of large leaf splits, 1 = leaf splits (dn[.][0] counts
+// both), 1 + L = internal level L (L = 1 .. kMaxLevelOfTree)
+constexpr int kUpPhases = 16;
 struct UpperCtl {
-  // XCD-hierarchical grid barrier (insert.hip grid_sync), each word on a
-  // 128 B line of its own: arrivals per XCD group, the XCD leaders' count,
-  // the generation each leader publishes to its group (monotonic within a
-  // launch) and the abort word (a barrier timed out: every block leaves).
-  // Double buffered by chunk parity: a launch uses set par and zeroes set
-  // par ^ 1 for the next one, so every launch starts from clean words even
-  // after one that aborted.
-  uint64_t xbar[2][8][16];
-  uint64_t top[2][16];
-  uint64_t gen[2][8][16];
+  // Phase hand-offs (insert.hip handoff), each word on a 128 B line of its
+  // own: tk = the next unclaimed task of a phase (tickets, taken in dispatch
+  // order by running waves / blocks), dn = its finished tasks, abort = a
+  // hand-off gave up (every block leaves at its next hand-off; the launch's
+  // last block completes the chunk alone).  Double buffered by chunk parity:
+  // a launch uses set par and zeroes set par ^ 1 for the next one.
+  uint32_t tk[2][kUpPhases][32];
+  uint32_t dn[2][kUpPhases][32];
   uint32_t abort[2][32];
   uint32_t gate;    // tag of the last chunk rejected by its ordering (kKeyMax)
   // leaf split counts of the upsert kernel per k_upper block range, double
@@ -243,8 +245,9 @@ struct UpperArgs {
   // nullable: block 0 records the wall clock (100 MHz) at each phase end,
   // stamps[0] = count (tools/upper_stamps.py)
   uint64_t* stamps;
-  // diagnostics (shm__upper_force_abort): block 0 raises the abort word
-  // before the first grid barrier of this launch
+  // diagnostics (shm__upper_force): every block gives up at the first phase
+  // hand-off of this launch, as if its wait had timed out (the last block
+  // then completes the chunk alone)
   uint32_t force_abort;
   // diagnostics (SHM_UPPER_LISTS=1 in the environment): never propagate
   // directly, every chunk through the level lists and grid barriers
@@ -256,9 +259,12 @@ constexpr int kUpperStamps = 32;
 // and end (row 9) clocks
 constexpr int kStampWords = kUpperStamps + 10 * 256;
 uint32_t upper_blocks();
-// k_upper's blocks (one per CU, 512 threads) fit the device at all
+// k_upper's blocks (512 threads) fit a CU at all
 bool upper_resident();
 void launch_upper(const UpperArgs& a, hipStream_t s);
+// diagnostics (shm__hog): n blocks that each hold a whole CU's LDS and spin
+// until `ticks` of the 100 MHz wall clock have passed since they started
+void launch_hog(uint32_t n, uint64_t ticks, hipStream_t s);
 
 void launch_empty_leaf(uint8_t* arena, uint64_t page_off, uint8_t* sum, hipStream_t s);
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s);
@@ -344,9 +350,11 @@ void launch_hash_ids(const uint64_t* ids, uint64_t n, uint64_t keyspace, uint64_
                      hipStream_t s);
 // stable bucketing by owning shard; cm = route_scratch_words(n) words
 uint64_t route_scratch_words(uint64_t n_max);
+// keymax / err (nullable): a routed insert's batch holding kKeyMax is
+// rejected whole (every count 0, kErrKeyMax in *err; keymax: a zeroed word)
 void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
                          uint64_t* counts, uint64_t* keys_out, uint32_t* perm,
-                         uint32_t* cm, hipStream_t s);
+                         uint32_t* cm, uint32_t* keymax, uint32_t* err, hipStream_t s);
 // out[i] = in[perm[i]]
 void launch_permute(const uint64_t* in, const uint32_t* perm, uint64_t n, uint64_t* out,
                     hipStream_t s);
@@ -432,9 +440,10 @@ void launch_add_u64(uint64_t* x, uint64_t n, uint64_t c, hipStream_t s);
 
 // ---- host read-backs (range.hip) ------------------------------------------------
 // dst[i] = src[i] for i < nw (<= 256, dst in mapped host memory), then a
-// system-scope release store of seq to *flag
+// system-scope release store of seq to *flag; clear: src[i] is exchanged
+// with 0 (atomically) as it is read
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
-                     uint32_t seq, hipStream_t s);
+                     uint32_t seq, int clear, hipStream_t s);
 
 }  // namespace dev
 }  // namespace shm

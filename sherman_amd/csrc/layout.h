@@ -119,15 +119,26 @@ struct Superblock {
 };
 constexpr uint64_t kSuperMagic = 0x5348524d414d4431ull;  // "SHRMAMD1"
 
-// device error bits
+// device error bits (word 0 of the tree's error block; word 1 = the tag of
+// the first insert chunk that saw a bit other than kErrKeyMax, tree.cpp
+// check_err).  Every bound that can stop a kernel has a bit of its own, so a
+// record names the kernel that hit it.
 constexpr uint32_t kErrBadPtr = 1u << 0;       // pointer outside arena / node
 constexpr uint32_t kErrInconsistent = 1u << 1; // version mismatch persisted
-constexpr uint32_t kErrRounds = 1u << 2;       // walk did not converge
+constexpr uint32_t kErrRounds = 1u << 2;       // k_upper: a parent / delete walk did not converge
 constexpr uint32_t kErrFence = 1u << 3;        // k < lowest on a walk
 constexpr uint32_t kErrLock = 1u << 4;         // lock spin bound exceeded
 constexpr uint32_t kErrPlan = 1u << 5;         // page changed between plan/apply
 constexpr uint32_t kErrOverflow = 1u << 6;     // page overfull at apply
 constexpr uint32_t kErrNoMem = 1u << 7;        // page arena exhausted (splits left unapplied)
+constexpr uint32_t kErrHandoff = 1u << 8;      // k_upper: a phase hand-off wait timed out
+                                               // (the chunk's levels / deletes resume later)
+constexpr uint32_t kErrSegSpin = 1u << 9;      // k_seg_fill: look-back spin bound
+constexpr uint32_t kErrScanSpin = 1u << 10;    // k_scan_u64: look-back spin bound
+constexpr uint32_t kErrBinSpin = 1u << 11;     // k_bin_unique: look-back spin bound
+constexpr uint32_t kErrGetHops = 1u << 12;     // a get walk (k_get / k_get_sum) hop bound
+constexpr uint32_t kErrLocateHops = 1u << 13;  // k_locate: walk hop bound
+constexpr uint32_t kErrFanIn = 1u << 14;       // k_upper: a large split's fan-in wait bound
 
 // CityHash64 v1.1 (google/cityhash, city.cc HashLen0to16 for len == 8).
 // Third-party dependency of the reference (script/installLibs.sh:16-20, HEAD,

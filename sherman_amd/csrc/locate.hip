@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   }
   for (int hop = 0; !slot; ++hop) {
     if (hop > kMaxRounds) {
-      err |= kErrRounds;
+      err |= kErrLocateHops;
       break;
     }
     if (!ptr_ok(ptr, a.node, a.arena_bytes)) {

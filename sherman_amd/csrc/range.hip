@@ -302,10 +302,13 @@ void launch_range(const RangeArgs& a, hipStream_t s) {
 
 // zero-copy read-back (tree.cpp readback): one wave copies the words into
 // mapped host memory with vector stores, fences at system scope, then lane 0
-// publishes the sequence number the host spins on
-__global__ void k_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
-                           uint32_t seq) {
-  for (uint32_t l = threadIdx.x; l < nw; l += blockDim.x) dst[l] = src[l];
+// publishes the sequence number the host spins on.  clear: each word is
+// taken by an atomic exchange with 0 (the error block: a bit another stream
+// sets after the exchange stays for the next read)
+__global__ void k_readback(uint32_t* dst, uint32_t* src, uint32_t nw, uint32_t* flag,
+                           uint32_t seq, int clear) {
+  for (uint32_t l = threadIdx.x; l < nw; l += blockDim.x)
+    dst[l] = clear ? atomicExch(src + l, 0u) : src[l];
   const uint32_t l = threadIdx.x;
   __threadfence_system();
   __syncthreads();
@@ -313,8 +316,9 @@ __global__ void k_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint
 }
 
 void launch_readback(uint32_t* dst, const uint32_t* src, uint32_t nw, uint32_t* flag,
-                     uint32_t seq, hipStream_t s) {
-  hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, dst, src, nw, flag, seq);
+                     uint32_t seq, int clear, hipStream_t s) {
+  hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, dst, const_cast<uint32_t*>(src), nw,
+                     flag, seq, clear);
 }
 
 __global__ void k_add_u64(uint64_t* x, uint64_t n, uint64_t c) {

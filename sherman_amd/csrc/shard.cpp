@@ -27,14 +27,17 @@
 //            owner's run packed into a slot of max_batch / P (kKeyMax
 //            padding), keys / values / counts exchanged, then the received
 //            slots queued as one local insert that skips the padding: no
-//            host wait.  Received slots arrive in source-rank order and the
-//            bucketing is stable, so a shard applies the union of the ranks'
-//            batches in rank-major batch order (last writer wins), one valid
-//            linearisation of Sherman's concurrent inserts.  A run longer
+//            host wait (a batch holding kKeyMax routes nothing and reports
+//            SHM_EINVAL, as a local insert rejects its chunk).  Received
+//            slots arrive in source-rank order and the bucketing is stable,
+//            so the slots apply in rank-major batch order.  A run longer
 //            than its slot keeps its tail, which the next call on the shard
 //            (or shm_shard_synchronize) sends in an exact second round and
-//            applies before anything else: each rank's ops stay in its own
-//            order.
+//            applies before anything else; each rank's ops stay in its own
+//            order, but a tail applies after every rank's slots, so across
+//            ranks the result is one valid linearisation of the ranks'
+//            concurrent batches (Sherman's clients are not ordered either),
+//            not strict rank-major order.
 //   range  : scan j's overlap with shard p is piece (p, j) of a P x n_cap
 //            matrix (empty where it misses the shard); row p goes to rank p
 //            (ncclAllToAll, no count exchange), the owner scans the pieces
@@ -72,6 +75,9 @@
 extern "C" uint32_t* shm__error_word(shm_tree* t);
 extern "C" int shm__insert_batch_padded(shm_tree* t, const uint64_t* keys, const uint64_t* vals,
                                         uint64_t n, void* stream);
+extern "C" int shm__route_bucket_insert(shm_tree* t, const uint64_t* keys, uint64_t n,
+                                        uint32_t num_shards, uint64_t* counts_out,
+                                        uint64_t* keys_out, uint32_t* perm_out, void* stream);
 extern "C" int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n,
                              uint64_t* tot_dev, void* stream);
 
@@ -689,7 +695,9 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   ExclCtx& e = h->ex;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t P = h->world;
-  RC_OK(shm_route_bucket(h->local, keys, n, P, e.icnt, e.kb, e.perm, s));
+  // a batch holding kKeyMax routes nothing (SHM_EINVAL at the next
+  // synchronising call), as a local insert rejects its chunk
+  RC_OK(shm__route_bucket_insert(h->local, keys, n, P, e.icnt, e.kb, e.perm, s));
   RC_OK(shm_route_permute(h->local, vals, e.perm, n, e.vb, s));
   shm::dev::launch_route_pack(e.kb, e.vb, e.icnt, P, e.icap, e.pk, e.pv, s);
   HIP_OK2(hipGetLastError());

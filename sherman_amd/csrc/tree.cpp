@@ -88,7 +88,11 @@ struct shm_tree {
   // k_upper state (insert.hip)
   dev::UpperCtl* ctl = nullptr;
   uint64_t* leaf_rd = nullptr;
-  bool force_abort = false;  // shm__upper_force_abort: the next chunk's k_upper stops
+  // shm__upper_force: bit 0 = the next chunk's k_upper gives up at its first
+  // hand-off, bit 1 = it propagates through the level lists (no direct path)
+  uint32_t force_flags = 0;
+  // shm_last_error: the last synchronising call that saw device error bits
+  shm_error_t last_error{};
   uint64_t *sep_key[2] = {nullptr, nullptr}, *sep_ptr[2] = {nullptr, nullptr};
   uint64_t* ipage[2] = {nullptr, nullptr};
   uint32_t *h_end = nullptr, *h_T = nullptr, *h_P = nullptr, *h_ver = nullptr, *h_lk = nullptr;
@@ -226,6 +230,14 @@ unsigned event_flags() {
   return f;
 }
 
+// INVARIANT: events from new_event() order streams of this device and
+// nothing else.  They are only ever passed to hipEventRecord and
+// hipStreamWaitEvent; never host-queried (hipEventSynchronize /
+// hipEventQuery) and never relied on to make device writes visible to the
+// host or to another device: with hipEventDisableSystemFence their record
+// does not write back the L2s.  Host-facing completion goes through
+// take_event() (HIP's default events: the profiler's timing) or the
+// read-back kernel's system-scope release (readback below).
 hipEvent_t new_event() {
   hipEvent_t e = nullptr;
   if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess) return nullptr;
@@ -394,7 +406,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   return SHM_OK;
 }
 
-int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes);
+int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes, int clear = 0);
 
 // the LDS replica's table (rebuilt like the directory, once the tree grew
 // by 1/32); one read-back of its size per rebuild
@@ -457,10 +469,10 @@ int dbg(hipStream_t s, const char* what) {
 // synchronisation.  While spinning it polls the stream, so a fault in an
 // earlier kernel (which would keep the word from ever arriving) still returns
 // SHM_EIO.
-int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes) {
+int readback(shm_tree* t, hipStream_t s, const void* src, size_t bytes, int clear) {
   const uint32_t seq = ++t->rb_seq;
   dev::launch_readback(t->h_pin_dev, static_cast<const uint32_t*>(src),
-                       (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, s);
+                       (uint32_t)((bytes + 3) / 4), t->h_pin_dev + kFlagWord, seq, clear, s);
   HIP_OK(hipGetLastError());
   const uint32_t* flag = reinterpret_cast<const uint32_t*>(t->h_pin) + kFlagWord;
   for (uint32_t spin = 1;; ++spin) {
@@ -492,23 +504,31 @@ int write_superblock(shm_tree* t, hipStream_t s) {
   return SHM_OK;
 }
 
-// sticky device error bits -> status (kErrKeyMax: a chunk with kKeyMax was
-// rejected whole; kErrNoMem: the arena ran out, splits left unapplied)
+// device error block -> status.  Word 0 holds the bits (kErrKeyMax: a chunk
+// with kKeyMax was rejected whole; kErrNoMem: the arena ran out, splits left
+// unapplied; kErrHandoff: a chunk's k_upper gave up at a hand-off and its
+// last block completed the chunk alone -- word 2 counts those chunks; the
+// rest: a tree inconsistency or a kernel bound, SHM_EIO), word 1 the first
+// insert chunk that saw a bit (0: none did).  The words are taken by atomic
+// exchange (readback clear), so a bit set by another stream after the read
+// stays for the next call.  shm_last_error reports what was read.
 int check_err(shm_tree* t, hipStream_t s) {
   t->err_pending = false;
-  int rc = readback(t, s, t->d_err, sizeof(uint32_t));
+  int rc = readback(t, s, t->d_err, 3 * sizeof(uint32_t), 1);
   if (rc) return rc;
-  const uint32_t e = (uint32_t)t->h_pin[0];
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(t->h_pin);
+  const uint32_t e = w[0], chunk = w[1], resumed = w[2];
   mirror(t);  // the stream is idle up to here: the mirror is exact
+  t->last_error.resumed += resumed;
   if (!e) return SHM_OK;
-  HIP_OK(hipMemsetAsync(t->d_err, 0, sizeof(uint32_t), s));
-  const uint32_t other = e & ~(dev::kErrKeyMax | kErrNoMem);
   t->sticky_err |= e;
-  if (other) {
-    fprintf(stderr, "sherman_amd: device error bits 0x%x\n", e);
-    return SHM_EIO;
-  }
-  return (e & kErrNoMem) ? SHM_ENOMEM : SHM_EINVAL;
+  const uint32_t other = e & ~(dev::kErrKeyMax | kErrNoMem | kErrHandoff);
+  rc = other ? SHM_EIO : (e & kErrNoMem) ? SHM_ENOMEM : (e & dev::kErrKeyMax) ? SHM_EINVAL : SHM_OK;
+  t->last_error.bits = e;
+  t->last_error.chunk = chunk;
+  t->last_error.status = rc;
+  if (other) fprintf(stderr, "sherman_amd: device error bits 0x%x (first seen by chunk %u)\n", e, chunk);
+  return rc;
 }
 
 hipEvent_t take_event(shm_tree* t) {
@@ -717,13 +737,13 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
-  u.force_abort = t->force_abort ? 1u : 0u;
+  u.force_abort = (t->force_flags & 1u) ? 1u : 0u;
   static const bool lists_only = [] {
     const char* e = getenv("SHM_UPPER_LISTS");
     return e && e[0] == '1';
   }();
-  u.no_direct = lists_only ? 1u : 0u;
-  t->force_abort = false;
+  u.no_direct = lists_only || (t->force_flags & 2u) ? 1u : 0u;
+  t->force_flags = 0;
   dev::launch_upper(u, s);
   DBG(s, "upper");
   HIP_OK(hipGetLastError());
@@ -1543,13 +1563,26 @@ int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n, ui
 // synchronising call on the tree returns their errors)
 uint32_t* shm__error_word(shm_tree* t) { return t ? t->d_err : nullptr; }
 
-// Diagnostics, not part of include/sherman_amd.h: the next insert chunk's
-// k_upper raises its abort word before its first grid barrier (the test of a
-// barrier timeout: the chunk reports SHM_EIO, later chunks run normally)
-int shm__upper_force_abort(shm_tree* t) {
+// Diagnostics, not part of include/sherman_amd.h: flags for the next insert
+// chunk's k_upper.  Bit 0: every block gives up at its first phase hand-off
+// (as a timed-out wait would; the launch's last block then completes the
+// chunk alone); bit 1: the chunk propagates its splits through the level
+// lists instead of the direct path.
+int shm__upper_force(shm_tree* t, uint32_t flags) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
-  t->force_abort = true;
+  t->force_flags = flags;
+  return SHM_OK;
+}
+int shm__upper_force_abort(shm_tree* t) { return shm__upper_force(t, 1u); }
+
+// Diagnostics, not part of include/sherman_amd.h: `blocks` blocks that each
+// hold a whole CU (all of its LDS) for `ticks` of the 100 MHz wall clock, on
+// `stream`: other streams' kernels meanwhile get the remaining CUs only
+int shm__hog(uint32_t blocks, uint64_t ticks, void* stream) {
+  if (blocks > 4096 || ticks > 1000000000ull) return SHM_EINVAL;  // <= 10 s
+  dev::launch_hog(blocks, ticks, pick(stream));
+  HIP_OK(hipGetLastError());
   return SHM_OK;
 }
 
@@ -1603,6 +1636,24 @@ int shm_read_words(shm_tree* t, const void* src, uint64_t bytes, void* host_out,
   if (rc) return rc;
   memcpy(host_out, t->h_pin, bytes);
   return SHM_OK;
+}
+
+int shm_last_error(shm_tree* t, shm_error_t* out, int reset) {
+  if (!t || !out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  *out = t->last_error;
+  if (reset) {
+    const uint32_t resumed = t->last_error.resumed;
+    t->last_error = shm_error_t{};
+    t->last_error.resumed = resumed;
+  }
+  return SHM_OK;
+}
+
+uint32_t shm_last_chunk(shm_tree* t) {
+  if (!t) return 0;
+  std::lock_guard<std::mutex> g(t->mu);
+  return t->chunks;
 }
 
 int shm_synchronize(shm_tree* t) {
@@ -1712,9 +1763,35 @@ int shm_profile_read(shm_tree* t, shm_profile_t* out, int reset) {
   return SHM_OK;
 }
 
+namespace {
+int route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t num_shards,
+                 uint64_t* counts_out, uint64_t* keys_out, uint32_t* perm_out, void* stream,
+                 bool reject_keymax);
+}
+
 int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
                      uint32_t num_shards, uint64_t* counts_out,
                      uint64_t* keys_out, uint32_t* perm_out, void* stream) {
+  return route_bucket(t, keys, n, num_shards, counts_out, keys_out, perm_out, stream, false);
+}
+
+// Library-internal (shard.cpp shm_shard_insert): the bucketing of a routed
+// insert; a batch holding kKeyMax is rejected whole on the sending rank
+// (nothing routed, SHM_EINVAL at the next synchronising call), as a local
+// insert rejects its chunk (the receivers skip kKeyMax as slot
+// padding, so it must be caught before packing)
+int shm__route_bucket_insert(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t num_shards,
+                             uint64_t* counts_out, uint64_t* keys_out, uint32_t* perm_out,
+                             void* stream) {
+  return route_bucket(t, keys, n, num_shards, counts_out, keys_out, perm_out, stream, true);
+}
+
+}  // extern "C"
+
+namespace {
+int route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t num_shards,
+                 uint64_t* counts_out, uint64_t* keys_out, uint32_t* perm_out, void* stream,
+                 bool reject_keymax) {
   if (!t || num_shards == 0 || num_shards > 64 || !counts_out) return SHM_EINVAL;
   if (n && (!keys || !keys_out || !perm_out)) return SHM_EINVAL;
   if (n > t->nmax) return SHM_E2BIG;
@@ -1733,10 +1810,15 @@ int shm_route_bucket(shm_tree* t, const uint64_t* keys, uint64_t n,
     }
     t->route_ws.push_back({s, scratch});
   }
-  dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out, scratch, s);
+  // d_err[3]: the kKeyMax flag of a routed insert (zero between calls)
+  dev::launch_route_bucket(keys, n, num_shards, counts_out, keys_out, perm_out, scratch,
+                           reject_keymax ? t->d_err + 3 : nullptr, t->d_err, s);
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int shm_route_permute(shm_tree* t, const uint64_t* in, const uint32_t* perm,
                       uint64_t n, uint64_t* out, void* stream) {

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
       w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((w & ~0xFFFFFFFFull) == tg) break;
       if (spin > (1u << 24)) {
-        atomicOr(err, kErrRounds);
+        atomicOr(err, kErrSegSpin);
         w = tg;
         break;
       }
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kT) void k_scan_u64(const uint64_t* in, uint64_t n,
       w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((w & ~kMask) == tg) break;
       if (spin > (1u << 24)) {
-        atomicOr(err_out, kErrRounds);
+        atomicOr(err_out, kErrScanSpin);
         w = tg;
         break;
       }
@@ -253,25 +253,36 @@ constexpr int kRouteTile = kT * kRoutePer;
 //   count   : per-tile shard counts            -> cm[tile][shard]
 //   scan    : per shard, exclusive over tiles  -> cm = tile bases, counts_out
 //   scatter : per tile, ranks in index order from wave ballots
+//   (keymax, nullable: a routed insert's batch -- a kKeyMax key sets the
+//   flag, and the scan then rejects the batch whole: every count 0, the
+//   error bit kErrKeyMax, as a local insert rejects its chunk)
 __global__ __launch_bounds__(kT) void k_route_count(const uint64_t* __restrict__ keys,
                                                     uint64_t n, uint32_t shards,
-                                                    uint32_t* __restrict__ cm) {
+                                                    uint32_t* __restrict__ cm,
+                                                    uint32_t* keymax) {
   __shared__ uint32_t c[kRouteMaxShards];
   if (threadIdx.x < kRouteMaxShards) c[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+  bool bad = false;
 #pragma unroll
   for (int r = 0; r < kRoutePer; ++r) {
     const uint64_t i = base + (uint64_t)r * kT + threadIdx.x;
-    if (i < n) atomicAdd(&c[owner_of(keys[i], shards)], 1u);
+    if (i < n) {
+      const uint64_t k = keys[i];
+      bad |= k == kKeyMax;
+      atomicAdd(&c[owner_of(k, shards)], 1u);
+    }
   }
+  if (keymax && ballot(bad) && lane_id() == 0) atomicOr(keymax, 1u);
   __syncthreads();
   if (threadIdx.x < shards) cm[(uint64_t)blockIdx.x * shards + threadIdx.x] = c[threadIdx.x];
 }
 
 __global__ __launch_bounds__(1024) void k_route_scan(uint32_t* __restrict__ cm, uint32_t tiles,
                                                      uint32_t shards,
-                                                     uint64_t* __restrict__ counts_out) {
+                                                     uint64_t* __restrict__ counts_out,
+                                                     uint32_t* keymax, uint32_t* err) {
   __shared__ uint32_t part[1024];
   __shared__ uint32_t off[kRouteMaxShards];
   const uint32_t t = threadIdx.x;
@@ -295,10 +306,15 @@ __global__ __launch_bounds__(1024) void k_route_scan(uint32_t* __restrict__ cm, 
   if (live && q == Q - 1) off[sh] = incl;  // shard total for now
   __syncthreads();
   if (t == 0) {
+    const bool reject = keymax && *keymax;
+    if (reject) {
+      *keymax = 0;
+      atomicOr(err, kErrKeyMax);
+    }
     uint32_t acc = 0;
     for (uint32_t x = 0; x < shards; ++x) {
       const uint32_t v = off[x];
-      counts_out[x] = v;
+      counts_out[x] = reject ? 0u : v;
       off[x] = acc;
       acc += v;
     }
@@ -370,10 +386,12 @@ uint64_t route_scratch_words(uint64_t n_max) {
 
 void launch_route_bucket(const uint64_t* keys, uint64_t n, uint32_t shards,
                          uint64_t* counts, uint64_t* keys_out, uint32_t* perm,
-                         uint32_t* cm, hipStream_t s) {
+                         uint32_t* cm, uint32_t* keymax, uint32_t* err, hipStream_t s) {
   const uint32_t tiles = (uint32_t)((n + kRouteTile - 1) / kRouteTile);
-  if (n) hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kT), 0, s, keys, n, shards, cm);
-  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, s, cm, tiles, shards, counts);
+  if (n)
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kT), 0, s, keys, n, shards, cm, keymax);
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, s, cm, tiles, shards, counts, keymax,
+                     err);
   if (n)
     hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kT), 0, s, keys, n, shards,
                        (const uint32_t*)cm, keys_out, perm);
@@ -706,6 +724,29 @@ __global__ __launch_bounds__(kT) void k_lock_bench(const uint64_t* keys, uint64_
 void launch_lock_bench(const uint64_t* keys, uint64_t n, uint64_t* locks, uint32_t num_locks,
                        uint64_t tag, uint32_t* err, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lock_bench, grid1(n), dim3(kT), 0, s, keys, n, locks, num_locks, tag, err);
+}
+
+// ---- diagnostics: a kernel that holds CUs (shm__hog) -----------------------------
+// Each block declares a whole CU's LDS (160 KiB), so no other block that uses
+// LDS fits its CU while it runs, and spins on the 100 MHz wall clock until
+// `ticks` have passed since it started (bounded: every wave leaves).  n
+// blocks therefore take n CUs away from the kernels of other streams for that
+// long (tests/test_gpu_parity.py::test_split_insert_beside_cu_hog).
+constexpr uint32_t kHogLdsWords = 160 * 1024 / 4;
+__global__ __launch_bounds__(kWave) void k_hog(uint64_t ticks, uint32_t* sink) {
+  __shared__ uint32_t s_pad[kHogLdsWords];
+  s_pad[threadIdx.x] = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  uint32_t spins = 0;
+  while (wall_clock64() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(8);
+    ++spins;
+  }
+  // keep the LDS array alive; never true for a real run (spins > 0)
+  if (spins == 0xFFFFFFFFu) sink[0] = s_pad[(threadIdx.x * 7) % kHogLdsWords];
+}
+void launch_hog(uint32_t n, uint64_t ticks, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_hog, dim3(n), dim3(kWave), 0, s, ticks, nullptr);
 }
 
 }  // namespace dev

@@ -1055,20 +1055,182 @@ def test_async_inserts_grow_from_empty_tree(lib_ok):
 
 def test_async_batch_with_kkeymax_is_rejected_and_reported(lib_ok):
     """A queued batch holding kKeyMax is dropped whole on the device and the
-    error surfaces at the next synchronising call; batches after it apply."""
+    error surfaces at the next synchronising call -- here a range scan, not
+    an insert -- naming the chunk that failed (shm_last_error), not the call
+    that read it; batches after it apply."""
     t = shm.Tree(arena_bytes=32 << 20, max_batch=4096)
     bad_k = dev(np.array([5, (1 << 64) - 1, 6], dtype=U64))
     bad_v = dev(np.array([1, 2, 3], dtype=U64))
     ok_k, ok_v = dev(np.array([7], dtype=U64)), dev(np.array([70], dtype=U64))
-    t.insert_batch_async(bad_k, bad_v)
     t.insert_batch_async(ok_k, ok_v)
+    t.insert_batch_async(bad_k, bad_v)
+    bad_chunk = t.last_chunk()
+    t.insert_batch_async(ok_k, ok_v)
+    assert t.last_chunk() == bad_chunk + 1
     with pytest.raises(shm.ShermanError) as ei:
-        t.synchronize()
+        t.range_query_batch(dev(np.array([0], dtype=U64)), dev(np.array([100], dtype=U64)))
     assert ei.value.rc == shm.SHM_EINVAL
+    e = t.last_error()
+    assert e["chunk"] == bad_chunk and e["bits"] & (1 << 31) and e["status"] == shm.SHM_EINVAL, e
     assert t.search(5) == (False, 0) and t.search(6) == (False, 0)
     assert t.search(7) == (True, 70)
     t.synchronize()  # reported once
     t.check()
+    t.close()
+
+
+def test_kkeymax_on_two_streams_both_reported(lib_ok):
+    """the error word is cleared by the atomic exchange that reads
+    it, not by a memset on the reading call's stream, so a rejected chunk on
+    a second stream right after a synchronised one is still reported."""
+    t = shm.Tree(arena_bytes=32 << 20, max_batch=4096)
+    bad_k = dev(np.array([5, (1 << 64) - 1], dtype=U64))
+    bad_v = dev(np.array([1, 2], dtype=U64))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for s in (s1, s2, s1):
+        with torch.cuda.stream(s):
+            with pytest.raises(shm.ShermanError) as ei:
+                t.insert_batch(bad_k, bad_v, stream=s)
+            assert ei.value.rc == shm.SHM_EINVAL
+            assert t.last_error()["chunk"] == t.last_chunk()
+    t.synchronize()
+    assert t.search(5) == (False, 0)
+    t.close()
+
+
+def _right_moves(t, probe):
+    t.profile(False, index_stats=True)
+    gpu_search(t, probe)
+    st = t.index_stats()
+    t.profile(False)
+    return st["right_moves"]
+
+
+@pytest.mark.parametrize("lists", [False, True])
+def test_forced_handoff_abort_resumes(lib_ok, lists):
+    """k_upper's blocks giving up at their first phase hand-off (forced by the
+    diagnostic shm__upper_force; in a real run a timed-out wait).  The
+    chunk's leaf splits are linked by sibling pointers when they stop; the
+    launch's last block then runs the parent levels and the deletes again
+    alone (Tree.cpp:973-988 always completes the parent insert), so nothing
+    is dropped: the call returns SHM_OK, shm_last_error shows the hand-off
+    bit, the chunk id and one completed chunk, the contents (deletes
+    included) equal the oracle, and the right moves per get equal those of
+    a tree that never gave up.  lists: the chunk propagates through the
+    level lists (the bulk-load path) instead of the direct path."""
+    H = shm._hooks()
+    rng = np.random.default_rng(77)
+    trees = [shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16) for _ in range(2)]
+    orc = OracleTree(256 << 20)
+    ks = hashed_keys(1, 60001)
+    for t in trees:
+        gpu_insert(t, ks, ks ^ U64(0x33))
+    orc.apply_batch(ks, ks ^ U64(0x33))
+    new = hashed_keys(100001, 130001)
+    dels = rng.choice(ks, 3000, replace=False)
+    k = np.concatenate([new, dels])
+    v = np.concatenate([np.arange(1, new.size + 1, dtype=U64) * U64(7),
+                        np.zeros(dels.size, dtype=U64)])
+    for i, t in enumerate(trees):
+        flags = (1 if i == 0 else 0) | (2 if lists else 0)
+        assert H.shm__upper_force(t.h, flags) == 0
+        gpu_insert(t, k, v)  # SHM_OK: completed inside the launch
+    orc.apply_batch(k, v)
+    e = trees[0].last_error()
+    assert e["bits"] & 0x100 and e["chunk"] == trees[0].last_chunk(), e
+    assert e["resumed"] == 1 and e["status"] == shm.SHM_OK, e
+    assert trees[1].last_error()["resumed"] == 0
+    for t in trees:
+        compare_contents(t, orc)
+    probe = np.concatenate([ks, new, hashed_keys(900001, 901001)])
+    rm = [_right_moves(t, probe) for t in trees]
+    assert rm[0] <= rm[1] + probe.size // 100 + 16, rm
+    # later chunks (splits, root growth, deletes) run normally
+    for r in range(2):
+        add = hashed_keys(200001 + 20000 * r, 220001 + 20000 * r)
+        d2 = rng.choice(ks, 2000, replace=False)
+        kk = np.concatenate([add, d2])
+        vv = np.concatenate([add ^ U64(r + 1), np.zeros(d2.size, dtype=U64)])
+        gpu_insert(trees[0], kk, vv)
+        orc.apply_batch(kk, vv)
+    compare_contents(trees[0], orc)
+    ov, of = orc.search_batch(probe)
+    gv, gf = gpu_search(trees[0], probe)
+    assert_same(probe, ov, of, gv, gf)
+    orc.close()
+    for t in trees:
+        t.close()
+
+
+def test_async_forced_abort_completed_before_next_call(lib_ok):
+    """An async chunk whose blocks give up at their hand-off is completed by
+    the launch's last block, before the next call on the handle (a range scan
+    here) reads the tree: the scan sees the chunk's inserts and deletes, and
+    shm_last_error, read by that scan, names the chunk."""
+    H = shm._hooks()
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16)
+    orc = OracleTree(256 << 20)
+    ks = hashed_keys(1, 40001)
+    gpu_insert(t, ks, ks + U64(1))
+    orc.apply_batch(ks, ks + U64(1))
+    new = hashed_keys(50001, 70001)
+    dels = ks[::7].copy()
+    k = np.concatenate([new, dels])
+    v = np.concatenate([new + U64(5), np.zeros(dels.size, dtype=U64)])
+    assert H.shm__upper_force(t.h, 1) == 0
+    dk, dv = dev(k), dev(v)
+    t.insert_batch_async(dk, dv)
+    chunk = t.last_chunk()
+    orc.apply_batch(k, v)
+    lo = np.array([0], dtype=U64)
+    hi = np.array([(1 << 64) - 2], dtype=U64)
+    counts, vals = t.range_query_batch(dev(lo), dev(hi))
+    ok, ov = orc.dump()
+    assert int(counts.cpu().numpy()[0]) == ok.size
+    e = t.last_error()
+    assert e["chunk"] == chunk and e["bits"] & 0x100 and e["resumed"] == 1, e
+    compare_contents(t, orc)
+    orc.close()
+    t.close()
+
+
+@pytest.mark.parametrize("lists", [False, True])
+def test_split_insert_beside_cu_hog(lib_ok, lists):
+    """Forward progress of the split propagation: a kernel on
+    another stream holds 240 of the 256 CUs (each block takes a whole CU's
+    LDS) for 3 s while a split-heavy insert with deletes runs on the rest.
+    k_upper's phases hand work out by ticket and never wait for a block that
+    is not running, so the insert returns SHM_OK with oracle-equal contents
+    while the hog still holds its CUs (a grid barrier over 256 blocks would
+    have waited for the hog, or timed out)."""
+    H = shm._hooks()
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 17)
+    orc = OracleTree(256 << 20)
+    ks = hashed_keys(1, 50001)
+    gpu_insert(t, ks, ks + U64(3))
+    orc.apply_batch(ks, ks + U64(3))
+    new = hashed_keys(60001, 160001)  # 2x the tree: splits everywhere
+    dels = ks[::5].copy()
+    k = np.concatenate([new, dels])
+    v = np.concatenate([new ^ U64(9), np.zeros(dels.size, dtype=U64)])
+    dk, dv = dev(k), dev(v)
+    gpu_search(t, ks[:1000])  # the leaf directory is current: no reallocation
+    torch.cuda.synchronize()
+    # both on non-blocking streams (the null stream would wait for the hog)
+    hog, ins = torch.cuda.Stream(), torch.cuda.Stream()
+    done = torch.cuda.Event()
+    if lists:
+        assert H.shm__upper_force(t.h, 2) == 0
+    assert H.shm__hog(240, 300_000_000, ctypes.c_void_p(hog.cuda_stream)) == 0
+    done.record(hog)
+    with torch.cuda.stream(ins):
+        t.insert_batch(dk, dv, stream=ins)
+    assert not done.query(), "the insert waited for the CU hog"
+    done.synchronize()
+    orc.apply_batch(k, v)
+    assert t.last_error()["bits"] == 0
+    compare_contents(t, orc)
+    orc.close()
     t.close()
 
 
@@ -1090,50 +1252,6 @@ def test_arena_exhaustion_reports_enomem_and_stays_consistent(lib_ok):
     want = dict(zip(ks.tolist(), vs.tolist()))
     assert k.size == st["keys"] and k.size > 0
     assert all(want[a] == b for a, b in zip(k.tolist(), v.tolist()))
-    orc.close()
-    t.close()
-
-
-def test_forced_barrier_abort_reports_eio_and_recovers(lib_ok):
-    """k_upper's grid barrier timing out (forced by the diagnostic
-    shm__upper_force_abort: block 0 raises the abort word before the first
-    barrier).  The chunk reports SHM_EIO; its upserts and leaf splits are
-    applied and linked by sibling pointers, so the tree is a valid B-link
-    tree (shm_check) holding exactly the batch's contents; its parent
-    updates are dropped.  The next chunks start from clean barrier words
-    (double-buffered by chunk parity) and propagate splits, root growth and
-    deletes normally: one timeout no longer damages the handle."""
-    L = shm.lib()
-    L.shm__upper_force_abort.restype = ctypes.c_int
-    L.shm__upper_force_abort.argtypes = [ctypes.c_void_p]
-    rng = np.random.default_rng(77)
-    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16)
-    orc = OracleTree(256 << 20)
-    ks = hashed_keys(1, 60001)
-    gpu_insert(t, ks, ks ^ U64(0x33))
-    orc.apply_batch(ks, ks ^ U64(0x33))
-    splits0 = t.stats()["splits"]
-    new = hashed_keys(100001, 130001)
-    nv = np.arange(1, new.size + 1, dtype=U64) * U64(7)
-    assert L.shm__upper_force_abort(t.h) == 0
-    with pytest.raises(shm.ShermanError) as ei:
-        gpu_insert(t, new, nv)
-    assert ei.value.rc == shm.SHM_EIO
-    orc.apply_batch(new, nv)
-    assert t.stats()["splits"] > splits0  # the leaf level ran before the barrier
-    compare_contents(t, orc)
-    for r in range(3):
-        add = hashed_keys(200001 + 20000 * r, 220001 + 20000 * r)
-        dels = rng.choice(ks, 2000, replace=False)
-        k = np.concatenate([add, dels])
-        v = np.concatenate([add ^ U64(r + 1), np.zeros(dels.size, dtype=U64)])
-        gpu_insert(t, k, v)
-        orc.apply_batch(k, v)
-        compare_contents(t, orc)
-    probe = np.concatenate([ks, new, hashed_keys(900001, 901001)])
-    ov, of = orc.search_batch(probe)
-    gv, gf = gpu_search(t, probe)
-    assert_same(probe, ov, of, gv, gf)
     orc.close()
     t.close()
 

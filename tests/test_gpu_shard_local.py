@@ -17,6 +17,10 @@ Checked against ONE unsharded CPU oracle tree (test infrastructure):
     second round, applied before anything else; a rank re-writes some of its
     keys inside the batch, head and tail): contents = the rank-major
     application of every rank's batches;
+  * a round in which rank 3's batch holds kKeyMax: that batch is rejected
+    whole on the sending rank (nothing of it reaches any shard, SHM_EINVAL at
+    rank 3's next synchronising call) while the other ranks' batches apply,
+    as a local insert rejects the chunk holding kKeyMax;
   * routed gets of a uniform batch, of a zipf(0.99) batch (the hot key's
     shard passes its slot of 1.25 n / P + 256) and of a batch whose every key
     belongs to shard 0 (7/8 of it overflows): every value returned, no key
@@ -46,6 +50,20 @@ def skew_batch(rank, n=2000):
     k = np.arange(n, dtype=U64) + U64(1 + 100000 * rank)
     k[n - 300:] = k[:300]
     v = np.arange(n, dtype=U64) + U64(5 * 10 ** 8 + 10 ** 6 * rank)
+    return k, v
+
+
+KM_RANK = 3
+
+
+def keymax_batch(rank):
+    """Five keys per rank spread over the shards; rank KM_RANK's batch also
+    holds kKeyMax (rejected whole)."""
+    k = (np.arange(5, dtype=U64) * U64(0x3333333333333333)) + U64(777 + rank)
+    v = np.arange(5, dtype=U64) + U64(9 * 10 ** 8 + 10 ** 3 * rank)
+    if rank == KM_RANK:
+        k = np.concatenate([k[:2], np.array([(1 << 64) - 1], dtype=U64), k[2:]])
+        v = np.concatenate([v[:2], np.array([1], dtype=U64), v[2:]])
     return k, v
 
 
@@ -86,6 +104,14 @@ def run_rank(r, trees, group, stream, out, errs):
                 cs.insert(d(k), d(v), stream=stream)
             k, v = skew_batch(r)
             cs.insert(d(k), d(v), stream=stream)
+            k, v = keymax_batch(r)
+            cs.insert(d(k), d(v), stream=stream)
+            km = None
+            if r == KM_RANK:
+                try:
+                    cs.synchronize()
+                except shm.ShermanError as e:
+                    km = e.rc
             res = {}
             for name, q in rank_queries(r).items():
                 vals = torch.empty(q.size, dtype=torch.int64, device=dev)
@@ -108,7 +134,8 @@ def run_rank(r, trees, group, stream, out, errs):
             cs.synchronize()
             stream.synchronize()
             out[r] = ({k: (a.cpu().numpy().view(U64), b.cpu().numpy()) for k, (a, b) in res.items()},
-                      {k: (a.cpu().numpy(), b.cpu().numpy().view(U64)) for k, (a, b) in scans.items()})
+                      {k: (a.cpu().numpy(), b.cpu().numpy().view(U64)) for k, (a, b) in scans.items()},
+                      km)
             cs.close()
     except BaseException as e:  # noqa: BLE001 - reported by the main thread
         errs.append((r, repr(e)))
@@ -148,6 +175,10 @@ def test_local_group_p8_routed_paths():
             ref.apply_batch(*rank_batches(r)[rnd])
     for r in range(P):
         ref.apply_batch(*skew_batch(r))
+    for r in range(P):
+        if r != KM_RANK:
+            ref.apply_batch(*keymax_batch(r))
+    assert out[KM_RANK][2] == shm.SHM_EINVAL, out[KM_RANK][2]
     rk, rv = ref.dump()
     o = np.argsort(rk)
     rk, rv = rk[o], rv[o]
@@ -165,7 +196,7 @@ def test_local_group_p8_routed_paths():
     assert np.array_equal(uv[o], rv)
     key_of = dict(zip(rv.tolist(), rk.tolist()))
     for r in range(P):
-        res, scans = out[r]
+        res, scans, _ = out[r]
         qs = rank_queries(r)
         for name, q in list(qs.items()) + [("inflight_zipf", qs["zipf"]),
                                             ("inflight_shard0", qs["shard0"])]:
