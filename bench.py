@@ -486,7 +486,7 @@ def main():
     cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
-            parity = parity_get(qs[0], qi[0], vals, found, step)
+            parity = parity_get(qs[0], qi[0], vals, found, step, tree, keys_local, n_keys, g)
         elif args.workload == "c5":
             cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step, n_keys)
         else:
@@ -1079,17 +1079,40 @@ class C1Build:
         }
 
 
-def parity_get(q, qi, vals, found, step):
+def parity_get(q, qi, vals, found, step, tree, keys_local, n_keys, g, miss_frac=0.09):
     """One full C2 batch through the GPU path (step 0) against the values the
     build wrote: query j is key(qi[j] + 1), stored with value 2 (qi[j] + 1),
     so every get must be found with exactly that value (what Tree::search
     returns over the same key stream; the expectation is the key stream's,
-    not the tree's own image)."""
+    not the tree's own image).  Then the same batch with ~9 % of its queries
+    replaced by keys that were never stored -- key(i) for ids past the key
+    count, as the reference benchmark's C1 read phase misses ~9 % of its
+    gets (kKeySpace with the modulus, test/benchmark.cpp:43-46) -- each of
+    which must come back not found with value 0 (Tree.cpp:445-448), the rest
+    as above."""
     import torch
     step(0)
     torch.cuda.synchronize()
     want = (qi + 1) * 2
-    return bool(torch.equal(vals, want) and bool(found.all()))
+    ok = bool(torch.equal(vals, want) and bool(found.all()))
+    n = q.numel()
+    miss = torch.rand(n, device=q.device, generator=g) < miss_frac
+    m = int(miss.sum().item())
+    mk = torch.empty(m, dtype=torch.int64, device=q.device)
+    tree.gen_keys(n_keys + 1, m, mk)  # ids n_keys + 1 .. : never stored
+    # the expectation is the key stream's: none of these keys equals a stored
+    # one (CityHash64 collisions would show here)
+    ok = ok and not bool(torch.isin(mk, keys_local).any())
+    q2 = q.clone()
+    q2[miss] = mk
+    v2 = torch.empty_like(q2)
+    f2 = torch.empty(n, dtype=torch.uint8, device=q.device)
+    tree.search_batch(q2, v2, f2)
+    tree.synchronize()
+    want2 = torch.where(miss, torch.zeros_like(want), want)
+    ok = ok and bool(torch.equal(v2, want2)) and bool(torch.equal(f2.bool(), ~miss))
+    log(f"C2 parity: {n} hits + a batch with {m} misses ({m / n:.3f}): {ok}")
+    return ok
 
 
 def c5_model(tree, n_keys, dev):

@@ -820,22 +820,26 @@ __device__ __forceinline__ uint32_t apply_internal(const UpperArgs& a, WaveLds& 
 // (B-link); a page no longer at `level` (the root grew, or a page another
 // wave has just created is not visible yet) is found again from the root.
 // direct: as apply_internal; returns the separators made (direct only).
+// held: the caller already holds `page`'s exclusive word (a valid page)
 __device__ __forceinline__ uint32_t apply_run(const UpperArgs& a, WaveLds& L, const uint64_t* keys,
                               const uint64_t* ptrs, uint32_t hs, uint32_t he, uint64_t page,
                               uint32_t level, uint64_t base, uint64_t cap, uint32_t& err,
-                              bool direct = false) {
+                              bool direct = false, bool held = false) {
   uint32_t nout = 0;
   for (int hop = 0; hs < he; ++hop) {
     if (hop >= kMaxRounds) {
       err |= kErrRounds;
+      if (held) unlock_excl(a, page);
       return nout;
     }
-    if (!ptr_ok(page, a.node, a.arena_bytes)) {
+    if (!held && !ptr_ok(page, a.node, a.arena_bytes)) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       page = parent_of(a, keys[hs], level, &err, true);
       continue;
     }
-    if (!lock_excl(a, page)) {
+    if (held) {
+      held = false;  // taken by the caller for this first page
+    } else if (!lock_excl(a, page)) {
       err |= kErrLock;
       return nout;
     }
@@ -879,8 +883,11 @@ __device__ __forceinline__ uint32_t apply_run(const UpperArgs& a, WaveLds& L, co
 // No list and no grid barrier: waves meet only on a shared parent's word.
 // A run of <= kSmallSplit - 1 separators splits each page it touches at most
 // once, so every level's run stays that short (the 64-entry LDS bound).
+// held1: the caller holds hint1's exclusive word (taken while it built the
+// leaf pages, so the word's round trip is off the chain)
 __device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32_t n, uint32_t level,
-                          uint64_t base, uint64_t cap, uint32_t& err, uint64_t hint1 = 0) {
+                          uint64_t base, uint64_t cap, uint32_t& err, uint64_t hint1 = 0,
+                          bool held1 = false) {
   for (; n; ++level) {
     if (level > (uint32_t)kMaxLevelOfTree) {
       err |= kErrRounds;
@@ -899,7 +906,8 @@ __device__ __forceinline__ void propagate(const UpperArgs& a, WaveLds& L, uint32
     // moves right or relocates
     const uint64_t hint =
         level == 1 && hint1 ? hint1 : parent_of(a, L.o_key[0], level, &err, true);
-    n = apply_run(a, L, L.o_key, L.o_val, 0, n, hint, level, base, cap, err, true);
+    n = apply_run(a, L, L.o_key, L.o_val, 0, n, hint, level, base, cap, err, true,
+                  level == 1 && held1);
   }
 }
 
@@ -1179,14 +1187,34 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       const bool small = (uint32_t)P <= kSmallSplit;
       if (!small && !fan_in(a.leaf_rd + g, (uint32_t)(P - 1), ftag)) err |= kErrFanIn;
       const Ops o0{a.op_key, a.op_val, a.seg_start[g], a.seg_end[g] - a.seg_start[g]};
+      // the page and the segment's ops (<= 64 of them) requested together
+      const bool few = o0.nb <= (uint32_t)kWave;
+      uint64_t ok0 = 0, ov0 = 0;
+      if (few && (uint32_t)lane < o0.nb) {
+        ok0 = o0.key[o0.st + lane];
+        ov0 = o0.val[o0.st + lane];
+      }
       const u32x4 w = load_page_slice(a.arena, ga_offset(page));
+      const uint64_t first_key = few ? rl64(ok0, 0) : o0.key[o0.st];
+      // the level-1 parent (the directory's hint for the first op key), and
+      // in the direct path its exclusive word, taken while the leaf pages are
+      // built: one atomic whose result is looked at after the builds
+      const uint64_t hint1 = direct ? dir_hint_page(a, first_key, 1) : 0ull;
+      const bool pre = direct && !grow0 && hint1 != 0 && ptr_ok(hint1, a.node, a.arena_bytes);
+      unsigned long long lk_old = ~0ull;
+      if (pre && lane == 0)
+        lk_old = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +
+                               lock_index(hint1, a.num_locks),
+                           (unsigned long long)(a.tag | 1ull));
       const Hdr h = parse_hdr(w);
       if (h.fver != a.seg_ver[g] || h.fver != h.rver_leaf) err |= kErrPlan;
       stage_page(L.page, w);
+      if (few && (uint32_t)lane < o0.nb) {
+        L.o_key[lane] = ok0;
+        L.o_val[lane] = ov0;
+      }
       wave_lds_sync();
-      const Ops o = stage_ops(L, o0);
-      // the level-1 parent's directory hint, in flight during the builds
-      const uint64_t hint1 = direct ? dir_hint_page(a, o.key[o.st], 1) : 0ull;
+      const Ops o = few ? Ops{L.o_key, L.o_val, 0, o0.nb} : o0;
       const int na = leaf_survivors(L, o);
       if (small) {
         for (int p = 1; p < P; ++p) {
@@ -1211,7 +1239,10 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       const uint64_t dest = grow0 ? ga_make(a.node, xroot * kPageSize) : page;
       (void)build_leaf_page(a, L, h, na, o, SplitPage{0, P, a.seg_T[g], first + pb, dest});
       if (grow0) write_new_root(a, L, dest, 1, h.fver);
-      if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err, grow0 ? 0ull : hint1);
+      // the word taken above: a free value came back exactly when it was taken
+      // (lock_excl's rule); otherwise apply_run spins for it as usual
+      const bool held = pre && rl64((uint64_t)lk_old, 0) <= a.tag;
+      if (direct) propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err, grow0 ? 0ull : hint1, held);
     }
     stamp();
     if (wait_leaf)

