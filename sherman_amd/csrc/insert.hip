@@ -1200,7 +1200,8 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       // in the direct path its exclusive word, taken while the leaf pages are
       // built: one atomic whose result is looked at after the builds
       const uint64_t hint1 = direct ? dir_hint_page(a, first_key, 1) : 0ull;
-      const bool pre = direct && !grow0 && hint1 != 0 && ptr_ok(hint1, a.node, a.arena_bytes);
+      const bool pre = direct && !grow0 && !a.no_prelock && hint1 != 0 &&
+                       ptr_ok(hint1, a.node, a.arena_bytes);
       unsigned long long lk_old = ~0ull;
       if (pre && lane == 0)
         lk_old = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +

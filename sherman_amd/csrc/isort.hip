@@ -87,7 +87,8 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
                                                    uint32_t* __restrict__ gcount,
                                                    uint32_t* err, uint32_t* gate, uint32_t tag,
                                                    KeyRange kr, uint32_t* __restrict__ M,
-                                                   uint32_t* __restrict__ S, int skip_pad) {
+                                                   uint32_t* __restrict__ S,
+                                                   uint32_t* __restrict__ Mx, int skip_pad) {
   // LDS hash table of the tile's distinct keys: slot -> (key, 1 + last index)
   constexpr int kSlots = 2 * kIsortTile;
   constexpr int PER = kIsortTile / kIT;
@@ -135,6 +136,47 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
     *gate = tag;
   }
   __syncthreads();
+  if (Mx) {
+    // Tile mode: the survivors sorted by coarse bin (a counting sort in LDS),
+    // bin b's run of this tile at keys_out[tile base + Mx[tile][b] ...] with
+    // M[tile][b] keys.  k_bin_unique gathers its bin's runs from every tile,
+    // so no coarse scatter pass moves the survivors once more.
+    __shared__ uint32_t lex[kCoarse];
+    uint64_t kk[SPT];
+    uint32_t ii[SPT], bn[SPT], rk[SPT];
+#pragma unroll
+    for (int r = 0; r < SPT; ++r) {
+      kk[r] = hkey[SPT * t + r];
+      ii[r] = hidx[SPT * t + r] - 1u;
+      bn[r] = kk[r] != kKeyMax ? coarse_of(kk[r], kr) : 0u;
+      rk[r] = kk[r] != kKeyMax ? atomicAdd(&hist[bn[r]], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t c = t < kCoarse ? hist[t] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_scan(c, wsum, &total);  // ends with a barrier
+    if (t < kCoarse) {
+      lex[t] = ex;
+      M[(uint64_t)blockIdx.x * kCoarse + t] = c;
+      Mx[(uint64_t)blockIdx.x * kCoarse + t] = ex;
+      if (c) atomicAdd(&S[(blockIdx.x / 16) * kCoarse + t], c);
+    }
+    __syncthreads();  // lex set; every slot read into registers
+#pragma unroll
+    for (int r = 0; r < SPT; ++r)
+      if (kk[r] != kKeyMax) {
+        const uint32_t p = lex[bn[r]] + rk[r];
+        hkey[p] = kk[r];
+        hidx[p] = ii[r];
+      }
+    __syncthreads();
+    for (uint32_t j = (uint32_t)t; j < total; j += kIT) {  // contiguous stores
+      keys_out[base + j] = hkey[j];
+      idx_out[base + j] = hidx[j];
+    }
+    if (t == 0) gcount[blockIdx.x] = total;
+    return;
+  }
   uint32_t keep = 0;
 #pragma unroll
   for (int r = 0; r < SPT; ++r) keep += hkey[SPT * t + r] != kKeyMax ? 1u : 0u;
@@ -381,7 +423,8 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
                                                    uint32_t* __restrict__ err,
                                                    uint32_t* __restrict__ S,
                                                    const uint32_t* gate, uint32_t tag,
-                                                   uint64_t* __restrict__ stamps) {
+                                                   uint64_t* __restrict__ stamps,
+                                                   TileRuns tr) {
   constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
   __shared__ unsigned long long hkey[kUniqSlots];  // hash, then the sorted keys
   __shared__ uint32_t hidx[kUniqSlots];            // 1 + op index, then op index
@@ -390,13 +433,21 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   __shared__ uint32_t wsum[kIT / kWave];
   __shared__ uint32_t s_big;
   __shared__ uint32_t s_cnt2[2];
+  // tile mode: this bin's run in every tile (prefix of the run lengths over
+  // the tiles, and where each run starts in the tiles' output)
+  __shared__ uint32_t s_tpre[kMaxTiles + 1];
+  __shared__ uint32_t s_tbase[kMaxTiles];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
+  const uint32_t tiles = tr.tiles;
   // the coarse pass is complete: clear its group sums for the next batch
-  if (b == 0)
+  // (tile mode: the last bin, once every bin has read them, bin_prefix)
+  if (b == 0 && !tiles)
     for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
   if (*gate == tag) {  // rejected chunk (kKeyMax): nothing to apply
     if (b == 0 && t == 0) counts[0] = counts[1] = 0;
+    if (tiles && b == (uint32_t)kCoarse - 1)
+      for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
     return;
   }
   // diagnostic phase clock (shm__upper_stamps): stamps[p * kCoarse + b]
@@ -404,12 +455,58 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     if (stamps && t == 0) stamps[p * kCoarse + b] = wall_clock64();
   };
   bstamp(0);
-  const uint32_t start = bins[2 * b], cnt = bins[2 * b + 1];
+  uint32_t start = 0, cnt = 0;
+  if (tiles) {
+    const uint32_t c = (uint32_t)t < tiles ? tr.M[(uint64_t)t * kCoarse + b] : 0u;
+    const uint32_t bx = (uint32_t)t < tiles ? tr.Mx[(uint64_t)t * kCoarse + b] : 0u;
+    const uint32_t ex = block_scan(c, wsum, &cnt);  // ends with a barrier
+    if ((uint32_t)t < tiles) {
+      s_tpre[t] = ex;
+      s_tbase[t] = (uint32_t)t * (uint32_t)kIsortTile + bx;
+    }
+    if (t == 0) s_tpre[tiles] = cnt;
+    __syncthreads();
+  } else {
+    start = bins[2 * b];
+    cnt = bins[2 * b + 1];
+  }
+  // tile mode: where bin element o lies in the tiles' output (the tile whose
+  // run holds it: the last tile with prefix <= o, a binary search in LDS)
+  auto src_of = [&](uint32_t o) -> uint32_t {
+    uint32_t lo = 0, hi = tiles;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_tpre[mid] <= o)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    return s_tbase[lo] + (o - s_tpre[lo]);
+  };
   if (cnt > (uint32_t)kUniqCap) {  // block-uniform
+    if (tiles) {
+      // the bin's own contiguous range of keys1 / pay1: its start is the sum
+      // of the bins before it (the tiles' group sums S), then a copy
+      uint32_t v = 0;
+      if ((uint32_t)t < b)
+        for (int g = 0; g < kPartGroupWords / kCoarse; ++g) v += S[g * kCoarse + t];
+      uint32_t bt;
+      (void)block_scan(v, wsum, &bt);
+      start = bt;
+      for (uint32_t o = (uint32_t)t; o < cnt; o += kIT) {
+        const uint32_t q = src_of(o);
+        keys1[start + o] = tr.keys[q];
+        pay1[start + o] = tr.idx[q];
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
     big_bin_unique(keys1, pay1, kscr, iscr, start, cnt, vals, lrank, s_cnt2,
                    reinterpret_cast<uint32_t*>(hkey));
     uint32_t bu, bd;
     bin_prefix(lbw, b, tag, s_cnt2[0], s_cnt2[1], wsum, bu, bd, counts, err);
+    if (tiles && b == (uint32_t)kCoarse - 1)  // every bin has read S (bin_prefix)
+      for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
     const uint32_t u = s_cnt2[0] + s_cnt2[1];
     for (uint32_t o = (uint32_t)t; o < u; o += kIT) {
       const uint32_t r = lrank[start + o];
@@ -443,8 +540,16 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     cr[r] = 0;
     const uint32_t o = (uint32_t)(r * kIT + t);
     if (o >= cnt) continue;
-    const uint64_t k = keys1[start + o];
-    const uint32_t ix = pay1[start + o];
+    uint64_t k;
+    uint32_t ix;
+    if (tiles) {
+      const uint32_t q = src_of(o);
+      k = tr.keys[q];
+      ix = tr.idx[q];
+    } else {
+      k = keys1[start + o];
+      ix = pay1[start + o];
+    }
     uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 51) & (kUniqSlots - 1);
     for (int probe = 0; probe < kUniqSlots; ++probe) {
       const unsigned long long old = atomicCAS(&hkey[h], (unsigned long long)kKeyMax,
@@ -558,6 +663,8 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   bstamp(4);
   uint32_t bu, bd;
   bin_prefix(lbw, b, tag, tot >> 16, tot & 0xFFFF, wsum, bu, bd, counts, err);
+  if (tiles && b == (uint32_t)kCoarse - 1)  // every bin has read S (bin_prefix)
+    for (int j = t; j < kPartGroupWords; j += kIT) S[j] = 0;
   bstamp(5);
   uint32_t ru = bu + (ex >> 16), rd = bd + (ex & 0xFFFF);
 #pragma unroll
@@ -578,12 +685,13 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
                        uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
-                       int skip_pad, hipStream_t s) {
+                       uint32_t* Mx, int skip_pad, hipStream_t s) {
   if (!n) return;
   const uint64_t tiles = (n + kIsortTile - 1) / kIsortTile;
-  if (tiles > (uint64_t)kMaxTiles) M = S = nullptr;  // the coarse pass counts for itself
+  if (tiles > (uint64_t)kMaxTiles) M = S = Mx = nullptr;  // the coarse pass counts for itself
+  if (!M || !S) Mx = nullptr;
   hipLaunchKernelGGL(k_tile_dedup, dim3((unsigned)tiles), dim3(kIT), 0, s, keys, n, keys_out,
-                     idx_out, gcount, err, gate, tag, KeyRange{key_lo, key_bits}, M, S,
+                     idx_out, gcount, err, gate, tag, KeyRange{key_lo, key_bits}, M, S, Mx,
                      skip_pad);
 }
 
@@ -591,10 +699,10 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, uint64_t* stamps, hipStream_t s) {
+                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, hipStream_t s) {
   const KeyRange kr{key_lo, key_bits};
   hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
-                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag, stamps);
+                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag, stamps, tr);
 }
 
 }  // namespace dev

@@ -252,6 +252,9 @@ struct UpperArgs {
   // diagnostics (SHM_UPPER_LISTS=1 in the environment): never propagate
   // directly, every chunk through the level lists and grid barriers
   uint32_t no_direct;
+  // A/B (SHM_UPPER_PRELOCK=0): take the level-1 parent's word only after
+  // the leaf pages are built (round 3's chain) instead of during the builds
+  uint32_t no_prelock;
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins
@@ -303,10 +306,22 @@ constexpr int kIsortTile = 2048;
 constexpr uint32_t kErrKeyMax = 1u << 31;
 // For batches of <= kMaxTiles tiles it also writes the coarse pass's tile
 // histograms M and group sums S (launch_partition_coarse then skips its own).
+// Tile mode (Mx non-null, <= kMaxTiles tiles): each tile's survivors are
+// written sorted by coarse bin, bin b's run at tile base + Mx[tile][b] with
+// M[tile][b] keys, and k_bin_unique gathers them (TileRuns) -- no coarse
+// scatter pass.
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
                        uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,
-                       int skip_pad, hipStream_t s);
+                       uint32_t* Mx, int skip_pad, hipStream_t s);
+// the tile mode's runs for k_bin_unique (tiles = 0: the coarse pass's bins)
+struct TileRuns {
+  const uint64_t* keys;  // tile_dedup's keys_out
+  const uint32_t* idx;   // tile_dedup's idx_out
+  const uint32_t* M;
+  const uint32_t* Mx;
+  uint32_t tiles;
+};
 // steps 3-4: per-bin last-writer dedup + sort (bins of <= 6144 ops in LDS,
 // larger ones by an LSD radix sort through global scratch kscr / iscr, n
 // words each), then uk / uv / dk at the bins' prefixes and (upserts, deletes)
@@ -316,7 +331,7 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, uint64_t* stamps, hipStream_t s);
+                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);

@@ -70,6 +70,8 @@ struct shm_tree {
   uint64_t nmax = 0, sep_cap = 0;
   uint64_t *ka = nullptr, *kb = nullptr;
   uint32_t *ia = nullptr, *ib = nullptr, *ic = nullptr;
+  uint64_t* kc = nullptr;  // tile-mode ordering scratch (insert_order)
+  uint32_t* id = nullptr;
   uint64_t *uk = nullptr, *uv = nullptr, *dk = nullptr;
   uint64_t* pages = nullptr;
   uint64_t* seg_lb = nullptr;  // tagged per-tile staged-head counts (launch_segment)
@@ -100,6 +102,7 @@ struct shm_tree {
   uint64_t* int_rd = nullptr;
   uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
   uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
+  uint32_t* part_mx = nullptr;    // [kMaxTiles][kCoarse] tile mode: each bin's run offset in a tile
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
   uint32_t* gcount = nullptr;       // insert ordering: survivors per 4096-op tile
   uint32_t* bins = nullptr;         // insert ordering: (start, count) per coarse bin
@@ -357,10 +360,18 @@ void publish_host(shm_tree* t) {
 // (C2) then runs on an exact directory, with no B-link right moves left
 // from the pages the last 1/32 of growth split (0.039 per get at C2 before
 // this rule: each one a header and a summary read)
+// (SHM_DIR_READ_PHASE=0: only the growth rule, the A/B)
 constexpr uint32_t kReadPhase = 4;
+bool dir_read_phase_on() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_DIR_READ_PHASE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
-  return t->reads_since_write >= kReadPhase && t->next_page != t->dir_np;
+  return dir_read_phase_on() && t->reads_since_write >= kReadPhase && t->next_page != t->dir_np;
 }
 
 // directory entries in fingerprint form (SHM_DIR_FP=0: the round-2 form, A/B)
@@ -628,16 +639,32 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   if (t->ord_valid && t->ord_s != s) HIP_OK(hipStreamWaitEvent(s, t->ord_ev, 0));
   const uint32_t p = tag & 1u;
   if (t->app_valid[p] && t->app_s[p] != s) HIP_OK(hipStreamWaitEvent(s, t->app_ev[p], 0));
+  // Tile mode (chunks of <= kMaxTiles tiles, i.e. <= 1 Mi ops): the tiles
+  // write their survivors sorted by coarse bin and k_bin_unique gathers its
+  // bin's runs from every tile, so there is no coarse scatter pass (round 4;
+  // SHM_TILE_MODE=0 restores the coarse pass, the A/B).  The tiles' output
+  // (kb / ia) stays live through k_bin_unique, so a bin over kUniqCap ops
+  // sorts in ka / ib with kc / id as scratch and ic for its ranks.
+  static const bool tile_mode_on = [] {
+    const char* e = getenv("SHM_TILE_MODE");
+    return !(e && e[0] == '0');
+  }();
+  const uint64_t tiles = (n + dev::kIsortTile - 1) / dev::kIsortTile;
+  const bool tile_mode = tile_mode_on && tiles <= (uint64_t)dev::kMaxTiles;
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
                          t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S,
-                         skip_pad ? 1 : 0, s);
-  dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
-                               t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
-  dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals, t->ia,
-                         reinterpret_cast<uint64_t*>(t->bins + 2 * dev::kCoarse), t->kb, t->ic,
+                         tile_mode ? t->part_mx : nullptr, skip_pad ? 1 : 0, s);
+  dev::TileRuns tr{t->kb, t->ia, t->part_hist, t->part_mx, tile_mode ? (uint32_t)tiles : 0u};
+  if (!tile_mode)
+    dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
+                                 t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
+  dev::launch_bin_unique(t->ka, t->ib, t->bins, t->cfg.key_lo, t->cfg.key_bits, vals,
+                         tile_mode ? t->ic : t->ia,
+                         reinterpret_cast<uint64_t*>(t->bins + 2 * dev::kCoarse),
+                         tile_mode ? t->kc : t->kb, tile_mode ? t->id : t->ic,
                          op_keys(t, tag), op_vals(t, tag), op_dels(t, tag), op_counts(t, tag),
                          t->d_err, t->part_S, &t->ctl->gate,
-                         tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, s);
+                         tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, tr, s);
   DBG(s, "ordering");
   return record(t, &t->ord_ev, &t->ord_s, &t->ord_valid, s);
 }
@@ -752,6 +779,11 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
     return e && e[0] == '1';
   }();
   u.no_direct = lists_only || (t->force_flags & 2u) ? 1u : 0u;
+  static const bool no_prelock = [] {
+    const char* e = getenv("SHM_UPPER_PRELOCK");
+    return e && e[0] == '0';
+  }();
+  u.no_prelock = no_prelock ? 1u : 0u;
   t->force_flags = 0;
   dev::launch_upper(u, s);
   DBG(s, "upper");
@@ -842,7 +874,7 @@ void free_all(shm_tree* t) {
   F(t->arena); F(t->locks); F(t->stamps); F(t->d_err); F(t->d_counts); F(t->route_scratch);
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
-  F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic);
+  F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic); F(t->kc); F(t->id); F(t->part_mx);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->seg_lb); F(t->bsum64);
   F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
@@ -1107,6 +1139,8 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->ia, n);
   rc |= dalloc(&t->ib, n);
   rc |= dalloc(&t->ic, n);
+  rc |= dalloc(&t->kc, n);
+  rc |= dalloc(&t->id, n);
   rc |= dalloc(&t->uk, 2 * n);  // two parities (op_keys)
   rc |= dalloc(&t->uv, 2 * n);
   rc |= dalloc(&t->dk, 2 * n);
@@ -1141,6 +1175,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->int_rd, t->sep_cap);
   rc |= dalloc(&t->part_hist, dev::kPartHistWords);
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
+  rc |= dalloc(&t->part_mx, dev::kPartHistWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
   rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count) per bin, then the bins' tagged counts
