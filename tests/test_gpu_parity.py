@@ -956,6 +956,60 @@ def test_searches_on_two_streams_with_an_insert_between(lib_ok):
     orc.close()
 
 
+def test_async_interleaved_searches_and_split_inserts(lib_ok):
+    """The ordering that replaces the get fast path's page-level
+    check_consistent (Tree.h:241-261; the summary walk checks only entry
+    versions): nothing but the library's cross-stream events (device-scope,
+    hipEventDisableSystemFence) orders these calls.  Twelve rounds, no host
+    wait anywhere: a search batch on stream A or B, then an async insert on
+    stream C that splits leaves (new keys next to stored ones), updates and
+    deletes.  Every search must equal the oracle's state at its point in
+    host call order: a search that overlapped an insert on the device would
+    read torn pages or a half-applied batch."""
+    n = 1 << 16
+    keys = hashed_keys(1, n + 1)
+    t = shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16)
+    orc = OracleTree(256 << 20)
+    gpu_insert(t, keys, keys + U64(1))
+    orc.apply_batch(keys, keys + U64(1))
+    t.synchronize()
+    rng = np.random.default_rng(2024)
+    sa, sb, sc = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    nxt = n + 1
+    outs, want, keep = [], [], []
+    for r in range(12):
+        st = sa if r % 2 else sb
+        q = np.concatenate([keys[rng.integers(0, keys.size, 20000)],
+                            hashed_keys(nxt - 3000, nxt + 1000)])
+        with torch.cuda.stream(st):
+            k = dev(q)
+            v = torch.empty_like(k)
+            f = torch.empty(k.numel(), dtype=torch.uint8, device=k.device)
+        t.search_batch(k, v, f, stream=st)
+        outs.append((q, v, f))
+        want.append(orc.search_batch(q))
+        keep.append(k)
+        add = hashed_keys(nxt, nxt + 6000)
+        nxt += 6000
+        upd = keys[rng.integers(0, keys.size, 3000)]
+        dels = keys[rng.integers(0, keys.size, 500)]
+        ik = np.concatenate([add, upd, dels])
+        iv = np.concatenate([add ^ U64(r + 5), upd + U64(r + 9), np.zeros(dels.size, dtype=U64)])
+        with torch.cuda.stream(sc):
+            dk, dv = dev(ik), dev(iv)
+        t.insert_batch_async(dk, dv, stream=sc)
+        orc.apply_batch(ik, iv)
+        keep += [dk, dv]
+    t.synchronize()
+    torch.cuda.synchronize()
+    for (q, v, f), (ov, of) in zip(outs, want):
+        assert_same(q, ov, of, host(v), f.cpu().numpy())
+    assert t.stats()["splits"] > 0
+    compare_contents(t, orc)
+    t.close()
+    orc.close()
+
+
 def test_insert_bin_overflow_reorders(lib_ok):
     """Clustered keys put > 6144 ops into one ordering bin: k_bin_unique sorts
     that bin on the device with its global-scratch LSD radix path

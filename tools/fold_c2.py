@@ -97,6 +97,9 @@ def main():
     # the highest request rate any calibration kernel sustained (the walk-shaped
     # mix, MALL-resident and HBM-resident random reads, more reads in flight)
     ceil = cal["random_request_ceiling_G_per_s"]
+    # the bench line's own accounting: 128 B per random line the walk must
+    # touch (two or three, by the measured directory-fingerprint share) + 16 B
+    bpg = bench["roofline"].get("alg_bytes_per_get") or 400
     out = {
         "what": "C2 timed steps (bench.py default: two HIP streams, two k_get_sum walks in "
                 "flight) under rocprofv3 --kernel-trace; PMC passes of the same command",
@@ -113,12 +116,11 @@ def main():
             "l2_hits_per_get": round(hit / batch, 3),
         },
         "byte_roofline": {
-            "alg_bytes_per_get": 400,
-            "note": "400 B/get = three random 128 B lines (directory entry, leaf summary, "
-                    "entry) + 8 B key + 8 B value: DESIGN §3's redefinition of SURVEY §8d's "
-                    "1040 B (the reference's whole-leaf read)",
-            "alg_GBps_over_step": round(batch * 400 / step_s / 1e9, 1),
-            "frac": round(batch * 400 / step_s / 1e9 / 8000.0, 4),
+            "alg_bytes_per_get": bpg,
+            "note": bench["roofline"].get("alg_bytes_note",
+                                          "%s B/get (bench.py roofline.alg_bytes_per_get)" % bpg),
+            "alg_GBps_over_step": round(batch * bpg / step_s / 1e9, 1),
+            "frac": round(batch * bpg / step_s / 1e9 / 8000.0, 4),
             "reference_1040B_frac": round(batch * 1040 / step_s / 1e9 / 8000.0, 4),
         },
         "request_roofline": {
