@@ -1055,6 +1055,12 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   const uint64_t cap = sb->capacity_pages;
   uint32_t err = 0;
   const uint32_t ns = *a.ns_dev;
+  // the counts the earlier kernels left, requested before the stores below
+  // (which the compiler cannot move them past): one round trip at the start
+  const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
+  const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
+  const uint32_t v_nb = (uint32_t)t < nb ? ctl->leaf_nb[par][t] : 0u;
+  const uint64_t n_del = *a.n_del;
   // the other parity's counters and hand-off words start the next chunk at 0
   for (uint64_t j = tid; j < (uint64_t)kMaxUpper; j += T) {
     ctl->leaf_np[par ^ 1][j] = 0;
@@ -1074,9 +1080,6 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     ctl->done[par ^ 1][0] = 0;
   }
   // leaf level: the upsert kernel left per-range new-page / split counts
-  const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
-  const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
-  const uint32_t v_nb = (uint32_t)t < nb ? ctl->leaf_nb[par][t] : 0u;
   __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
   uint32_t total, nsplit, nbig;
   {
@@ -1093,7 +1096,6 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     __syncthreads();
   }
-  const uint64_t n_del = *a.n_del;
   // nothing to split and nothing to delete (every op applied in place, C3's
   // chunks): the superblock's batch count is the only change, so block 0
   // writes it and no block waits for the others (no fan-in on `done`)

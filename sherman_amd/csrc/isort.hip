@@ -156,9 +156,10 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
     uint32_t total;
     const uint32_t ex = block_scan(c, wsum, &total);  // ends with a barrier
     if (t < kCoarse) {
+      // bin-major ([bin][tile]): k_bin_unique reads its bin's row whole
       lex[t] = ex;
-      M[(uint64_t)blockIdx.x * kCoarse + t] = c;
-      Mx[(uint64_t)blockIdx.x * kCoarse + t] = ex;
+      M[(uint64_t)t * kMaxTiles + blockIdx.x] = c;
+      Mx[(uint64_t)t * kMaxTiles + blockIdx.x] = ex;
       if (c) atomicAdd(&S[(blockIdx.x / 16) * kCoarse + t], c);
     }
     __syncthreads();  // lex set; every slot read into registers
@@ -457,8 +458,8 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   bstamp(0);
   uint32_t start = 0, cnt = 0;
   if (tiles) {
-    const uint32_t c = (uint32_t)t < tiles ? tr.M[(uint64_t)t * kCoarse + b] : 0u;
-    const uint32_t bx = (uint32_t)t < tiles ? tr.Mx[(uint64_t)t * kCoarse + b] : 0u;
+    const uint32_t c = (uint32_t)t < tiles ? tr.M[(uint64_t)b * kMaxTiles + t] : 0u;
+    const uint32_t bx = (uint32_t)t < tiles ? tr.Mx[(uint64_t)b * kMaxTiles + t] : 0u;
     const uint32_t ex = block_scan(c, wsum, &cnt);  // ends with a barrier
     if ((uint32_t)t < tiles) {
       s_tpre[t] = ex;

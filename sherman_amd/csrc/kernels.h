@@ -307,9 +307,10 @@ constexpr uint32_t kErrKeyMax = 1u << 31;
 // For batches of <= kMaxTiles tiles it also writes the coarse pass's tile
 // histograms M and group sums S (launch_partition_coarse then skips its own).
 // Tile mode (Mx non-null, <= kMaxTiles tiles): each tile's survivors are
-// written sorted by coarse bin, bin b's run at tile base + Mx[tile][b] with
-// M[tile][b] keys, and k_bin_unique gathers them (TileRuns) -- no coarse
-// scatter pass.
+// written sorted by coarse bin, bin b's run at tile base + Mx[b][tile] with
+// M[b][tile] keys (bin-major, [kCoarse][kMaxTiles]: a bin's row is read
+// whole), and k_bin_unique gathers them (TileRuns) -- no coarse scatter
+// pass.  S still gets the group sums.
 void launch_tile_dedup(const uint64_t* keys, uint64_t n, uint64_t* keys_out, uint32_t* idx_out,
                        uint32_t* gcount, uint32_t* err, uint32_t* gate, uint32_t tag,
                        uint64_t key_lo, uint32_t key_bits, uint32_t* M, uint32_t* S,

@@ -102,7 +102,8 @@ struct shm_tree {
   uint64_t* int_rd = nullptr;
   uint32_t* part_hist = nullptr;  // [kMaxTiles][kCoarse] coarse tile counts
   uint32_t* part_S = nullptr;     // coarse group sums (zero between batches)
-  uint32_t* part_mx = nullptr;    // [kMaxTiles][kCoarse] tile mode: each bin's run offset in a tile
+  uint32_t* part_mx = nullptr;    // [kCoarse][kMaxTiles] tile mode: each bin's run offset in a tile
+  uint32_t* part_mt = nullptr;    // [kCoarse][kMaxTiles] tile mode: each bin's run length in a tile
   uint32_t* part_chunks = nullptr;  // fine-pass chunk table
   uint32_t* gcount = nullptr;       // insert ordering: survivors per 4096-op tile
   uint32_t* bins = nullptr;         // insert ordering: (start, count) per coarse bin
@@ -651,10 +652,12 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   }();
   const uint64_t tiles = (n + dev::kIsortTile - 1) / dev::kIsortTile;
   const bool tile_mode = tile_mode_on && tiles <= (uint64_t)dev::kMaxTiles;
+  // tile mode: M and Mx bin-major in part_mt / part_mx (part_hist keeps the
+  // coarse pass's tile-major layout for the other path and ordered gets)
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
-                         t->cfg.key_lo, t->cfg.key_bits, t->part_hist, t->part_S,
-                         tile_mode ? t->part_mx : nullptr, skip_pad ? 1 : 0, s);
-  dev::TileRuns tr{t->kb, t->ia, t->part_hist, t->part_mx, tile_mode ? (uint32_t)tiles : 0u};
+                         t->cfg.key_lo, t->cfg.key_bits, tile_mode ? t->part_mt : t->part_hist,
+                         t->part_S, tile_mode ? t->part_mx : nullptr, skip_pad ? 1 : 0, s);
+  dev::TileRuns tr{t->kb, t->ia, t->part_mt, t->part_mx, tile_mode ? (uint32_t)tiles : 0u};
   if (!tile_mode)
     dev::launch_partition_coarse(t->kb, n, t->gcount, t->ia, t->cfg.key_lo, t->cfg.key_bits,
                                  t->part_hist, t->part_S, t->ka, t->ib, t->bins, s);
@@ -874,7 +877,7 @@ void free_all(shm_tree* t) {
   F(t->arena); F(t->locks); F(t->stamps); F(t->d_err); F(t->d_counts); F(t->route_scratch);
   for (auto& r : t->route_ws)
     if (r.second != t->route_scratch) F(r.second);
-  F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic); F(t->kc); F(t->id); F(t->part_mx);
+  F(t->ka); F(t->kb); F(t->ia); F(t->ib); F(t->ic); F(t->kc); F(t->id); F(t->part_mx); F(t->part_mt);
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->seg_lb); F(t->bsum64);
   F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
@@ -1176,6 +1179,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->part_hist, dev::kPartHistWords);
   rc |= dalloc(&t->part_S, dev::kPartGroupWords);
   rc |= dalloc(&t->part_mx, dev::kPartHistWords);
+  rc |= dalloc(&t->part_mt, dev::kPartHistWords);
   rc |= dalloc(&t->part_chunks, 2 * (uint64_t)dev::partition_chunk_slots(n));
   rc |= dalloc(&t->gcount, n / dev::kIsortTile + 1);
   rc |= dalloc(&t->bins, 4 * dev::kCoarse);  // (start, count) per bin, then the bins' tagged counts
