@@ -107,11 +107,17 @@ __global__ __launch_bounds__(kIT) void k_tile_dedup(const uint64_t* __restrict__
   }
   __syncthreads();
   bool bad = false;
+  uint64_t kin[PER];  // both keys requested before the first probe
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint64_t i = base + (uint64_t)(r * kIT + t);
+    kin[r] = i < n ? keys[i] : kKeyMax;
+  }
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
     const uint64_t i = base + (uint64_t)(r * kIT + t);
     if (i >= n) continue;
-    const uint64_t k = keys[i];
+    const uint64_t k = kin[r];
     if (k == kKeyMax) {
       // kKeyMax cannot be stored (root highest is exclusive, Tree.h:150);
       // a routed insert's slot padding (skip_pad) is no op at all
@@ -534,6 +540,22 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   // sub-bucket, so b. touches only the claimed slots
   uint64_t ck[kUniqPer];
   uint32_t ch[kUniqPer], cr[kUniqPer];
+  // every element's (key, op index) requested before the first hash probe:
+  // one memory round trip, not one per element (the LDS atomics below keep
+  // the compiler from moving later loads above them)
+  uint64_t lk[kUniqPer];
+  uint32_t li[kUniqPer];
+#pragma unroll
+  for (int r = 0; r < kUniqPer; ++r) {
+    const uint32_t o = (uint32_t)(r * kIT + t);
+    lk[r] = kKeyMax;
+    li[r] = 0;
+    if (o < cnt) {
+      const uint32_t q = tiles ? src_of(o) : start + o;
+      lk[r] = tiles ? tr.keys[q] : keys1[q];
+      li[r] = tiles ? tr.idx[q] : pay1[q];
+    }
+  }
 #pragma unroll
   for (int r = 0; r < kUniqPer; ++r) {
     ch[r] = ~0u;
@@ -541,16 +563,8 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
     cr[r] = 0;
     const uint32_t o = (uint32_t)(r * kIT + t);
     if (o >= cnt) continue;
-    uint64_t k;
-    uint32_t ix;
-    if (tiles) {
-      const uint32_t q = src_of(o);
-      k = tr.keys[q];
-      ix = tr.idx[q];
-    } else {
-      k = keys1[start + o];
-      ix = pay1[start + o];
-    }
+    const uint64_t k = lk[r];
+    const uint32_t ix = li[r];
     uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 51) & (kUniqSlots - 1);
     for (int probe = 0; probe < kUniqSlots; ++probe) {
       const unsigned long long old = atomicCAS(&hkey[h], (unsigned long long)kKeyMax,
