@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
     a.out_slot[i] = slot;
     // a new key (or a leaf without a summary): its page is staged whole
     // (out = 0 after an error marks page 0: staged, rejected as a bad pointer)
-    if (!slot) a.out_new[ga_offset(out) >> 10] = new_mark(a.out_new_tag);
+    if (!slot && a.out_new) a.out_new[ga_offset(out) >> 10] = new_mark(a.out_new_tag);
   }
   if (match && a.any_new) {
     const uint64_t m = ballot(!slot);

@@ -673,13 +673,26 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
 }
 
 // steps 2-5 on the ordered chunk of tag (the leaf directory is current)
+// segmentation from the ops' own verdicts (k_seg_fill_slot) instead of the
+// page marks: SHM_SEG_SLOTS=1.  Measured slower (one gpurun call, C5 4517
+// against 4678 Mops/s with the marks, whose random byte reads hit L2), so
+// the marks stay the default
+bool seg_from_slots() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_SEG_SLOTS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
   t->reads_since_write = 0;
   // the byte marks repeat every 255 chunks: clear them when they wrap, so
   // no page still carries this chunk's mark from 255 chunks ago
-  if (dev::new_mark(tag) == 1) HIP_OK(hipMemsetAsync(t->pnew, 0, t->cap_pages, s));
+  if (!seg_from_slots() && dev::new_mark(tag) == 1)
+    HIP_OK(hipMemsetAsync(t->pnew, 0, t->cap_pages, s));
   dev::WalkArgs w = walk_args(t);
   uint64_t* const cnt = op_counts(t, tag);
   w.keys = op_keys(t, tag);
@@ -688,7 +701,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.out_page = t->pages;
   w.target_level = 0;
   w.out_slot = t->oslot;
-  w.out_new = t->pnew;
+  w.out_new = seg_from_slots() ? nullptr : t->pnew;  // the page marks: the old segmentation only
   w.out_new_tag = tag;
   w.any_new = reinterpret_cast<uint32_t*>(t->d_counts + 10);
   w.vals = op_vals(t, tag);
@@ -700,7 +713,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
-                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s);
+                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
+                      seg_from_slots() ? t->oslot : nullptr);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
