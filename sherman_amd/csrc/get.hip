@@ -350,10 +350,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
   bool hit = false;
   if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
     uint64_t ptr = a.root;
+    uint64_t alt = 0;  // a tie's safe start (dir_start_e)
     if (a.dir) {
       u32x4 e[4];
       bool fpform;
-      ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform);
+      ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform, &alt);
       if (fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
         // the prefix lies in one leaf and the entry holds its fingerprints:
         // read the candidate slots straight away (Tree.cpp:687-697's first
@@ -422,6 +423,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
           }
           cand &= cand - 1;
         }
+        if (val == kValueNull && alt) {
+          // a tie's optimistic leaf does not hold k: k may lie below its
+          // lowest fence, so walk again from the safe start
+          ptr = alt;
+          alt = 0;
+          continue;
+        }
         break;
       }
       // no summary: the page's own bytes
@@ -451,6 +459,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
         ++c_right;
         continue;
       }
+      if (k < lowest && alt) {  // a tie's optimistic leaf: k lies to its left
+        ptr = alt;
+        alt = 0;
+        continue;
+      }
       if (k < lowest || k >= highest) {
         err |= kErrFence;
         break;
@@ -465,7 +478,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
             break;
           }
         }
-        break;
+        break;  // k >= lowest: this leaf is k's, found or not
       }
       // internal_page_search (Tree.cpp:665-685): child = #keys <= k
       int lo = 0, hi = cnt < kInternalCardinality ? cnt : kInternalCardinality;

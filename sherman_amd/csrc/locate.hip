@@ -58,10 +58,12 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   int retries = 0;
   uint64_t out = 0;
   uint32_t slot = 0;
+  uint64_t alt = 0;  // a tie's safe start (dir_start_e): an update is found optimistically
   if (a.dir && a.target_level == 0) {
     u32x4 e[4];
     bool fpform;
-    ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform);
+    ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform,
+                      match ? &alt : nullptr);
     if (match && fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
       // the prefix lies in one leaf and the entry holds its fingerprints: an
       // op whose key that leaf holds updates it without the summary line (a
@@ -124,6 +126,13 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
           }
           cand &= cand - 1;
         }
+        if (!slot && alt) {
+          // a tie's optimistic leaf does not hold k: a new key may belong to
+          // the leaf on its left, so walk again from the safe start
+          ptr = alt;
+          alt = 0;
+          continue;
+        }
         break;
       }
     }
@@ -150,6 +159,11 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
     }
     if (k >= highest && sibling != 0) {  // turn right (Tree.cpp:626-629)
       ptr = sibling;
+      continue;
+    }
+    if (k < lowest && alt) {  // a tie's optimistic leaf: k lies to its left
+      ptr = alt;
+      alt = 0;
       continue;
     }
     if (k < lowest || k >= highest || level < a.target_level) {

@@ -399,6 +399,14 @@ uint32_t dir_extra_bits() {
 
 int refresh_dir(shm_tree* t, hipStream_t s) {
   if (!dir_stale(t)) return SHM_OK;
+  static const bool trace = [] {
+    const char* e = getenv("SHM_TRACE_DIR");
+    return e && e[0] == '1';
+  }();
+  if (trace)
+    fprintf(stderr, "sherman_amd: leaf directory rebuild: pages %llu (last build %llu), %u reads "
+            "since the last insert\n", (unsigned long long)t->next_page,
+            (unsigned long long)t->dir_np, t->reads_since_write);
   uint32_t bits = 10;
   while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
   bits += dir_extra_bits();

@@ -1312,6 +1312,53 @@ def test_split_insert_beside_cu_hog(lib_ok, lists):
     t.close()
 
 
+def test_directory_ties_start_at_the_leaf(lib_ok):
+    """A directory entry's split points are the top 32 bits of each leaf's
+    lowest fence within the prefix, so a lookup of a leaf's FIRST key ties
+    with its split point (round 4: 2.7 % of C2's gets did, and started one
+    leaf to the left).  A tie now starts at the leaf itself and falls back to
+    the safe start only when the key is not there: with a fresh directory,
+    gets and in-place updates of every leaf's first key make no right move,
+    and keys just below / above those fences (absent) still come back
+    exactly as the oracle says."""
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18)
+    orc = OracleTree(512 << 20)
+    ks = hashed_keys(1, 300001)
+    for c in range(0, ks.size, 1 << 17):
+        gpu_insert(t, ks[c:c + (1 << 17)], ks[c:c + (1 << 17)] ^ U64(0x55))
+    orc.apply_batch(ks, ks ^ U64(0x55))
+    img, _ = t.dump_image()
+    pg = np.frombuffer(img, dtype=np.uint8)[1024:].reshape(-1, 1024)
+    leftmost = pg[:, 9:17].copy().view(U64).ravel()
+    lowest = pg[:, 28:36].copy().view(U64).ravel()
+    seps = np.unique(lowest[(leftmost == 0) & (lowest != 0)])
+    seps = seps[np.isin(seps, ks)]  # every leaf's first key (stored)
+    assert seps.size > 1000
+    for _ in range(6):  # a read phase: the directory is rebuilt exact
+        gpu_search(t, ks[:4096])
+    t.profile(False, index_stats=True)
+    gv, gf = gpu_search(t, seps)
+    st = t.index_stats()
+    assert st["right_moves"] == 0, st
+    assert_same(seps, *orc.search_batch(seps), gv, gf)
+    near = np.concatenate([seps - U64(1), seps + U64(1)])
+    gv, gf = gpu_search(t, near)
+    t.profile(False)
+    assert_same(near, *orc.search_batch(near), gv, gf)
+    # in-place updates of the first keys, then new keys right below them
+    # (they belong to the leaf on the left): contents equal the oracle
+    upd_v = seps ^ U64(0xABC)
+    gpu_insert(t, seps, upd_v)
+    orc.apply_batch(seps, upd_v)
+    below = seps[:2000] - U64(1)
+    below = below[~np.isin(below, ks)]
+    gpu_insert(t, below, below + U64(9))
+    orc.apply_batch(below, below + U64(9))
+    compare_contents(t, orc)
+    orc.close()
+    t.close()
+
+
 @pytest.mark.parametrize("start", ["dir", "lds", "root"])
 def test_get_start_modes_and_index_stats(lib_ok, start):
     """The summary walk from each start: the leaf directory, the LDS replica
