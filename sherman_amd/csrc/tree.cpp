@@ -385,13 +385,15 @@ bool dir_fp_on() {
 }
 
 // Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS,
-// default 1: two 64 B entries per page, so ~64 % of the prefixes lie inside
-// one leaf and carry its fingerprints; DESIGN §3 "Fingerprints in the
-// directory")
+// default 2: four 64 B entries per page, so ~76 % of C2's gets find their
+// prefix inside one leaf and are answered from the entry's fingerprints;
+// DESIGN §3 "Fingerprints in the directory".  Round 4, once ties no longer
+// started left: C2 17803 -> 17978 Mops/s over four paired runs against two
+// entries per page, C3 / C5 unchanged; 512 MB at C2's 2^26 keys)
 uint32_t dir_extra_bits() {
   static const uint32_t x = [] {
     const char* e = getenv("SHM_DIR_EXTRA_BITS");
-    const int v = e ? atoi(e) : 1;
+    const int v = e ? atoi(e) : 2;
     return (uint32_t)(v < 0 ? 0 : v > 3 ? 3 : v);
   }();
   return x;
