@@ -30,6 +30,8 @@
 //     out_new[page] = tag: only such pages are staged by the upsert (under
 //     their lock words), which skips the ops applied here.
 // Op keys arrive sorted, so neighbouring lanes read the same header lines.
+#include <stdlib.h>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -46,7 +48,7 @@ __device__ __forceinline__ uint64_t g_u64(const uint32_t* p, int d) {
 
 }  // namespace
 
-__global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
+__device__ __forceinline__ void locate_body(const WalkArgs& a) {
   const uint64_t i = (uint64_t)blockIdx.x * kLocBlock + threadIdx.x;
   const uint64_t n = a.n_dev ? *a.n_dev : a.n;
   if (i >= n) return;
@@ -199,10 +201,28 @@ __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) {
   }
 }
 
+__global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) { locate_body(a); }
+template <int W>
+__global__ __launch_bounds__(kLocBlock) __attribute__((amdgpu_waves_per_eu(W))) void k_locate_w(
+    WalkArgs a) {
+  locate_body(a);
+}
+
+// waves per SIMD (SHM_LOCATE_WAVES = 6 or 8, default: the compiler's 5; the A/B): the locate is
+// bound by its dependent random reads, so more lanes in flight may pay
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {
   if (n_upper == 0) return;
-  hipLaunchKernelGGL(k_locate, dim3((unsigned)((n_upper + kLocBlock - 1) / kLocBlock)),
-                     dim3(kLocBlock), 0, s, a);
+  static const int w = [] {
+    const char* e = getenv("SHM_LOCATE_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const dim3 g((unsigned)((n_upper + kLocBlock - 1) / kLocBlock));
+  if (w >= 8)
+    hipLaunchKernelGGL(k_locate_w<8>, g, dim3(kLocBlock), 0, s, a);
+  else if (w == 6)
+    hipLaunchKernelGGL(k_locate_w<6>, g, dim3(kLocBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_locate, g, dim3(kLocBlock), 0, s, a);
 }
 
 }  // namespace dev
