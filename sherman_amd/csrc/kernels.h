@@ -139,6 +139,9 @@ struct UpperCtl {
   uint32_t root_new[2][32];
   uint32_t lvl_sep[2][16];
   uint32_t done[2][32];  // blocks finished: the last one writes the superblock
+  // pages the upsert kernel's early splits took (leaf and internal), from the
+  // superblock's next_page on; k_upper's own pages follow them
+  uint64_t ualloc[2][16];
 };
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
@@ -186,7 +189,10 @@ struct SegArgs {
   uint32_t par;
   uint32_t up_nb;
 };
-void launch_leaf_upsert(const SegArgs& a, hipStream_t s);
+struct UpperArgs;
+// u: the split arguments of the chunk with u.early = 1 (small splits taken
+// by the upsert kernel itself, upsert.hip) or 0 (every split left to k_upper)
+void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s);
 
 // the device-driven split propagation (insert.hip)
 struct UpperArgs {
@@ -255,12 +261,18 @@ struct UpperArgs {
   // A/B (SHM_UPPER_PRELOCK=0): take the level-1 parent's word only after
   // the leaf pages are built (round 3's chain) instead of during the builds
   uint32_t no_prelock;
+  // the upsert kernel's copy (upsert.hip): small splits are built and
+  // propagated there, their pages counted in UpperCtl.ualloc; 0 in k_upper's
+  uint32_t early;
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins
 // + k_bin_unique's 7 x 256 phase words, then k_upper's per-block start (row 8)
 // and end (row 9) clocks
-constexpr int kStampWords = kUpperStamps + 10 * 256;
+// + the upsert kernel's per-block clocks (start, in-place groups done, end)
+// and early-split counts, rows of 1024 (tools/upper_stamps.py)
+constexpr int kUpsertStamps = kUpperStamps + 10 * 256;
+constexpr int kStampWords = kUpsertStamps + 4 * 1024;
 uint32_t upper_blocks();
 // k_upper's blocks (512 threads) fit a CU at all
 bool upper_resident();

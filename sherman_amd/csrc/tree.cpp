@@ -91,7 +91,8 @@ struct shm_tree {
   dev::UpperCtl* ctl = nullptr;
   uint64_t* leaf_rd = nullptr;
   // shm__upper_force: bit 0 = the next chunk's k_upper gives up at its first
-  // hand-off, bit 1 = it propagates through the level lists (no direct path)
+  // hand-off, bit 1 = it propagates through the level lists (no direct path),
+  // bit 2 = its upsert kernel leaves every split to k_upper (any bit does)
   uint32_t force_flags = 0;
   // shm_last_error: the last synchronising call that saw device error bits
   shm_error_t last_error{};
@@ -727,34 +728,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                       seg_from_slots() ? t->oslot : nullptr);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
-  dev::SegArgs a{};
-  a.arena = t->arena;
-  a.arena_bytes = t->arena_bytes;
-  a.node = t->cfg.node_id;
-  a.op_key = op_keys(t, tag);
-  a.op_val = op_vals(t, tag);
-  a.seg_start = t->seg_start;
-  a.seg_end = t->seg_end;
-  a.seg_page = t->seg_page;
-  a.num_seg = (uint32_t)n;
-  a.num_seg_dev = d_ns;
-  a.seg_T = t->seg_T;
-  a.seg_P = t->seg_P;
-  a.seg_newpages = t->seg_np;
-  a.seg_ver = t->seg_ver;
-  a.oslot = t->oslot;
-  a.locks = t->locks;
-  a.num_locks = t->cfg.num_locks;
-  a.tag = lock_tag;
-  a.err = t->d_err;
-  a.leaf_hw = t->leaf_hw;
-  a.sum = t->sum;
-  a.ctl = t->ctl;
-  a.par = tag & 1u;
-  a.up_nb = dev::upper_blocks();
-  dev::launch_leaf_upsert(a, s);
-  DBG(s, "leaf_upsert");
-  if (t->prof_on) HIP_OK(hipEventRecord(pr.e[2], s));
   dev::UpperArgs u{};
   u.arena = t->arena;
   u.arena_bytes = t->arena_bytes;
@@ -811,6 +784,42 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
     return e && e[0] == '0';
   }();
   u.no_prelock = no_prelock ? 1u : 0u;
+  // small splits built by the upsert kernel itself (SHM_EARLY_SPLIT=0: all
+  // left to k_upper, round 4's path); the forced k_upper paths keep theirs
+  static const bool no_early = [] {
+    const char* e = getenv("SHM_EARLY_SPLIT");
+    return e && e[0] == '0';
+  }();
+  dev::UpperArgs ue = u;
+  ue.early = no_early || (t->force_flags & 7u) ? 0u : 1u;
+  dev::SegArgs a{};
+  a.arena = t->arena;
+  a.arena_bytes = t->arena_bytes;
+  a.node = t->cfg.node_id;
+  a.op_key = op_keys(t, tag);
+  a.op_val = op_vals(t, tag);
+  a.seg_start = t->seg_start;
+  a.seg_end = t->seg_end;
+  a.seg_page = t->seg_page;
+  a.num_seg = (uint32_t)n;
+  a.num_seg_dev = d_ns;
+  a.seg_T = t->seg_T;
+  a.seg_P = t->seg_P;
+  a.seg_newpages = t->seg_np;
+  a.seg_ver = t->seg_ver;
+  a.oslot = t->oslot;
+  a.locks = t->locks;
+  a.num_locks = t->cfg.num_locks;
+  a.tag = lock_tag;
+  a.err = t->d_err;
+  a.leaf_hw = t->leaf_hw;
+  a.sum = t->sum;
+  a.ctl = t->ctl;
+  a.par = tag & 1u;
+  a.up_nb = dev::upper_blocks();
+  dev::launch_leaf_upsert(a, ue, s);
+  DBG(s, "leaf_upsert");
+  if (t->prof_on) HIP_OK(hipEventRecord(pr.e[2], s));
   t->force_flags = 0;
   dev::launch_upper(u, s);
   DBG(s, "upper");
@@ -1640,7 +1649,8 @@ uint32_t* shm__error_word(shm_tree* t) { return t ? t->d_err : nullptr; }
 // chunk's k_upper.  Bit 0: every block gives up at its first phase hand-off
 // (as a timed-out wait would; the launch's last block then completes the
 // chunk alone); bit 1: the chunk propagates its splits through the level
-// lists instead of the direct path.
+// lists instead of the direct path; bit 2 (or any bit): the chunk's upsert
+// kernel leaves every split to k_upper (no early splits).
 int shm__upper_force(shm_tree* t, uint32_t flags) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
@@ -1648,6 +1658,18 @@ int shm__upper_force(shm_tree* t, uint32_t flags) {
   return SHM_OK;
 }
 int shm__upper_force_abort(shm_tree* t) { return shm__upper_force(t, 1u); }
+
+// Diagnostics: the pages the last insert chunk's early splits took (its
+// upsert kernel's, upsert.hip), after synchronising the tree
+int shm__early_pages(shm_tree* t, uint64_t* out) {
+  if (!t || !out) return SHM_EINVAL;
+  const int rc = shm_synchronize(t);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(t->mu);
+  HIP_OK(hipMemcpy(out, &t->ctl->ualloc[t->chunks & 1u][0], sizeof(uint64_t),
+                   hipMemcpyDeviceToHost));
+  return SHM_OK;
+}
 
 // Diagnostics, not part of include/sherman_amd.h: `blocks` blocks that each
 // hold a whole CU (all of its LDS) for `ticks` of the 100 MHz wall clock, on

@@ -32,11 +32,57 @@
 #include "kernels.h"
 #include "lds_dma.h"
 #include "leaf_chunk.h"
+#include "split_wave.h"
 
 namespace shm {
 namespace dev {
 
 namespace {
+
+// A block's work queue in LDS.  Groups: wave w of the block takes the
+// block's next group k (k-th of b * 4 + (k & 3) + (k >> 2) * W, the same
+// groups the static w, w + W, ... assignment gave the block), so a wave that
+// spends time on an early split leaves its share to the block's other waves.
+// Early splits (split_wave.h split_early): queued by the wave that found
+// them (slot, fields, then its ready word), taken by any wave of the block
+// after its next group or once it has no group left; more than kEarlyMax in
+// a block: the rest go to k_upper as before.
+constexpr uint32_t kEarlyMax = 64;
+struct BlockQ {
+  uint32_t next;    // the block's next unclaimed group
+  uint32_t active;  // waves still taking groups
+  uint32_t ealloc;  // early split slots handed out
+  uint32_t eclaim;  // early splits taken
+  uint32_t ready[kEarlyMax];
+  EarlyItem item[kEarlyMax];
+};
+using EarlyList = BlockQ;
+
+// one queued early split for the wave (lane-0 LDS atomics, broadcast); false
+// when none is queued right now
+__device__ __forceinline__ bool take_early(BlockQ* q, uint32_t& x) {
+  uint32_t got = ~0u;
+  if (lane_id() == 0) {
+    for (;;) {
+      const uint32_t c = __hip_atomic_load(&q->eclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint32_t n = __hip_atomic_load(&q->ealloc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      n = n < kEarlyMax ? n : kEarlyMax;
+      if (c >= n) break;
+      if (atomicCAS(&q->eclaim, c, c + 1) == c) {
+        got = c;
+        break;
+      }
+    }
+    // its producer is a running wave of this block between taking the slot
+    // and publishing it
+    if (got != ~0u)
+      while (__hip_atomic_load(&q->ready[got], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+  }
+  got = rl32(got, 0);
+  x = got;
+  return got != ~0u;
+}
 
 }  // namespace
 
@@ -46,12 +92,15 @@ namespace {
 // segment's split plan (seg_T / seg_P / seg_newpages / seg_ver).  page / pok
 // are valid in lanes s < G; qst / qen / pk / pv per slot group.  Returns the
 // error bits.
+// early: small splits go to the block's list el (u: the split arguments,
+// cursor0 the superblock's next_page)
 template <int G>
 __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t* buf,
                                                 uint64_t g0, uint32_t num_seg, uint64_t page,
                                                 bool pok, bool locked, uint32_t qst,
                                                 uint32_t qen, uint64_t pk, uint64_t pv,
-                                                uint32_t po) {
+                                                uint32_t po, const UpperArgs& u, EarlyList* el,
+                                                bool early, uint64_t cursor0) {
   constexpr int L = kWave / G;                       // lanes per page
   constexpr int E = (kLeafCardinality + L - 1) / L;  // entries per lane
   constexpr int CD = kLeafEntry * E / 4;             // dwords per lane chunk
@@ -204,9 +253,28 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   if (li == 0 && q < G && gq < num_seg) {
     a.seg_T[gq] = live ? T : 0u;
     a.seg_P[gq] = P;
-    a.seg_newpages[gq] = P - 1;
     a.seg_ver[gq] = live ? fver : ~0u;
-    if (P > 1) {
+    // a small split when the block's list has room: its pages now (one
+    // atomic while the in-place groups go on), built after them
+    bool queued = false;
+    if (early && P > 1 && P <= kSmallSplit) {
+      const uint32_t x = atomicAdd(&el->ealloc, 1u);
+      if (x < kEarlyMax) {
+        queued = true;
+        EarlyItem& it = el->item[x];
+        it.page = qpage;
+        it.first = cursor0 + atomicAdd(reinterpret_cast<unsigned long long*>(&u.ctl->ualloc[u.par][0]),
+                                       (unsigned long long)(P - 1));
+        it.hint1 = dir_hint_page(u, pk, 1);  // pk: the segment's first op key (li == 0)
+        it.st = qst;
+        it.nb = qen - qst;
+        it.T = T;
+        it.pv = P | (fver << 8);
+        __hip_atomic_store(&el->ready[x], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    a.seg_newpages[gq] = queued ? 0u : P - 1;
+    if (P > 1 && !queued) {
       // k_upper block range of this segment (insert.hip block_range)
       const uint32_t r = (uint32_t)((gq * a.up_nb) / num_seg);
       atomicAdd(&a.ctl->leaf_np[a.par][r], P - 1);
@@ -217,24 +285,21 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   return err;
 }
 
+// The in-place groups of wave w (its first group g).
 // Software-pipelined: a grid of about one resident wave set; each wave loops
 // over groups
 // w, w + W, ... and, while it applies group g from one LDS buffer, the pages
 // of group g + W are already landing in the other (LDS-DMA) and the segment
 // records of g + 2W and the ops of g + W are in flight.  Per group the wave
 // then pays about the apply time instead of two dependent HBM round trips.
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
+template <int G, bool IL>
+__device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperArgs& u,
+                                                  BlockQ* el, bool early, uint64_t cursor0,
+                                                  uint64_t cap, uint64_t W, uint64_t ngroups,
+                                                  uint32_t num_seg, uint32_t* s_pg, WaveLds& Lw) {
   constexpr int L = kWave / G;
-  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * 2 * G * kPageDwords];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint64_t)wv;
-  const uint32_t num_seg = *a.num_seg_dev;
-  const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
-  uint64_t g = w;
-  if (g >= ngroups) return;  // wave-uniform
   const uint32_t* bufs = &s_pg[wv * 2 * G * kPageDwords];
   const uint32_t bufs_lds = lds_addr_of(bufs);
   const int q = lane / L;
@@ -281,6 +346,16 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
         glds16(a.arena + ga_offset(rl64(page, s)), bufs_lds + (uint32_t)((b * G + s) * kPageSize));
   };
 
+  // the block's next group (>= ngroups: none left)
+  auto claim = [&]() -> uint64_t {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(&el->next, 1u);
+    k = rl32(k, 0);
+    return (uint64_t)(k >> 2) * W + (uint64_t)blockIdx.x * kWavesPerBlock + (k & 3u);
+  };
+  uint64_t g = claim();
+  if (g >= ngroups) return err;
+  uint64_t gn = claim();
   uint64_t c_page, n_page, c_lk;
   uint32_t c_st, c_en, n_st, n_en;
   bool c_pok;
@@ -289,11 +364,11 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
   uint32_t c_po;
   rec(g, c_page, c_st, c_en);
   stage(g, c_page, c_st, c_en, 0, c_pok, c_lk, c_qst, c_qen, c_pk, c_pv, c_po);
-  rec(g + W, n_page, n_st, n_en);
+  rec(gn, n_page, n_st, n_en);
   for (uint32_t it = 0;; ++it) {
-    wait_vm<0>();  // group g's pages, lock words and ops, group g + W's records
+    wait_vm<0>();  // group g's pages, lock words and ops, group gn's records
     const uint32_t b = it & 1u;
-    const uint64_t gn = g + W;
+    uint64_t gm = ngroups;
     bool x_pok = false;
     uint64_t x_lk = 0;
     uint32_t x_qst = 0, x_qen = 0;
@@ -303,16 +378,26 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     uint32_t m_st = 0, m_en = 0;
     // a word held by a later tag is not this chunk's to take (never in a
     // serialised tree: reported as a lock failure, the segment left as is)
-    const bool held = c_lk <= a.tag;
+    // (tag | 1: an internal page's exclusive hold by an early split that
+    // shares the word, lock_index hashes pages of every level)
+    const bool held = c_lk <= (a.tag | 1ull);
     if (ballot(c_pok && !held)) err |= kErrLock;
     if (gn < ngroups) {  // wave-uniform
       stage(gn, n_page, n_st, n_en, b ^ 1u, x_pok, x_lk, x_qst, x_qen, x_pk, x_pv, x_po);
-      rec(gn + W, m_page, m_st, m_en);
+      gm = claim();
+      rec(gm, m_page, m_st, m_en);
     }
     err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
-                          true, c_qst, c_qen, c_pk, c_pv, c_po);
+                          true, c_qst, c_qen, c_pk, c_pv, c_po, u, el, early, cursor0);
+    // one queued early split between groups (the next group's pages keep
+    // landing meanwhile)
+    if constexpr (IL) {
+      uint32_t x;
+      if (early && take_early(el, x)) err |= split_early(u, Lw, el->item[x], cursor0, cap);
+    }
     if (gn >= ngroups) break;
     g = gn;
+    gn = gm;
     c_page = n_page;
     c_pok = x_pok;
     c_lk = x_lk;
@@ -325,23 +410,115 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a) {
     n_st = m_st;
     n_en = m_en;
   }
-  if (err) atomicOr(a.err, err);
+  return err;
 }
 
-void launch_leaf_upsert(const SegArgs& a, hipStream_t s) {
+// Early splits (u.early): a segment that would split into at most
+// kSmallSplit pages is queued in the block's LDS queue instead of being left
+// to k_upper, and a wave of the same block builds it and takes its separators
+// up (split_wave.h split_early) between its groups or after them, so C5's
+// splits run beside the in-place groups instead of in a kernel of their own.
+// A block's waves are resident together: a wave without groups waits (LDS)
+// for its block's last queued split, never for other blocks.
+// IL: a wave also takes a queued split between its groups (else only once
+// the block's groups are all taken)
+template <int G, bool IL>
+__device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * 2 * G * kPageDwords];
+  __shared__ __attribute__((aligned(16))) WaveLds s_wl[kWavesPerBlock];
+  __shared__ BlockQ s_q;
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t num_seg = *a.num_seg_dev;
+  const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
+  // early splits need a root above the leaves (a leaf root grows the tree:
+  // k_upper) and the direct path (SHM_UPPER_LISTS=1 sends all to the lists)
+  const Superblock* sb = reinterpret_cast<const Superblock*>(a.arena);
+  const uint64_t cursor0 = sb->next_page;
+  const uint64_t cap = sb->capacity_pages;
+  const bool early = u.early && sb->root_level >= 1 && !u.no_direct;
+  // diagnostic clocks (u.stamps, tools/upper_stamps.py)
+  uint64_t* clk = u.stamps && blockIdx.x < 1024 && threadIdx.x == 0
+                      ? u.stamps + kUpsertStamps + blockIdx.x
+                      : nullptr;
+  if (clk) clk[0] = wall_clock64();
+  if (threadIdx.x < kEarlyMax) s_q.ready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    s_q.next = 0;
+    s_q.active = kWavesPerBlock;
+    s_q.ealloc = 0;
+    s_q.eclaim = 0;
+  }
+  __syncthreads();
+  uint32_t err = upsert_groups<G, IL>(a, u, &s_q, early, cursor0, cap, W, ngroups, num_seg, s_pg,
+                                  s_wl[wv]);
+  // this wave queues nothing more
+  if (lane == 0) __hip_atomic_fetch_add(&s_q.active, ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (clk && early) clk[1024] = wall_clock64();
+  if (early) {
+    for (;;) {
+      uint32_t x;
+      if (take_early(&s_q, x)) {
+        err |= split_early(u, s_wl[wv], s_q.item[x], cursor0, cap);
+        continue;
+      }
+      uint32_t act = 0;
+      if (lane == 0) act = __hip_atomic_load(&s_q.active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (rl32(act, 0) == 0) {
+        if (take_early(&s_q, x)) {
+          err |= split_early(u, s_wl[wv], s_q.item[x], cursor0, cap);
+          continue;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  if (err && lane == 0) atomicOr(a.err, err);
+  if (clk) {
+    clk[2 * 1024] = wall_clock64();
+    clk[3 * 1024] = s_q.ealloc;
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a, UpperArgs u) {
+  upsert_body<G, false>(a, u);
+}
+// interleaved variants (SHM_UPSERT_IL=1: as many VGPRs as it takes, 2 waves
+// per SIMD; 2: held to 3 waves per SIMD, spilling)
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_leaf_upsert_il(SegArgs a, UpperArgs u) {
+  upsert_body<G, true>(a, u);
+}
+template <int G>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_leaf_upsert_il3(
+    SegArgs a, UpperArgs u) {
+  upsert_body<G, true>(a, u);
+}
+
+void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
   constexpr int G = 4;
   if (!a.num_seg) return;
-  static const unsigned blocks = [] {
+  static const int mode = [] {
+    const char* e = getenv("SHM_UPSERT_IL");
+    return e ? atoi(e) : 0;
+  }();
+  using K = void (*)(SegArgs, UpperArgs);
+  const K k = mode == 1 ? k_leaf_upsert_il<G> : mode == 2 ? k_leaf_upsert_il3<G> : k_leaf_upsert_pipe<G>;
+  static unsigned blocks[3] = {0, 0, 0};
+  unsigned& nb = blocks[mode >= 0 && mode <= 2 ? mode : 0];
+  if (!nb) {
     int per_cu = 0, cus = 0, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_leaf_upsert_pipe<G>, kBlock, 0);
-    return (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
-  }();
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0);
+    nb = (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
+  }
   const uint64_t groups = (a.num_seg + G - 1) / G;
   const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, blocks)),
-                     dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)std::min<uint64_t>(need, nb)), dim3(kBlock), 0, s, a, u);
 }
 
 }  // namespace dev

@@ -1312,6 +1312,72 @@ def test_split_insert_beside_cu_hog(lib_ok, lists):
     t.close()
 
 
+def early_pages(t):
+    x = ctypes.c_uint64()
+    assert shm._hooks().shm__early_pages(t.h, ctypes.byref(x)) == 0
+    return x.value
+
+
+def test_early_splits_match_k_upper_splits(lib_ok):
+    """Small splits built by the upsert kernel itself (early, upsert.hip) and
+    the same chunks with every split left to k_upper (shm__upper_force bit 2)
+    both give the oracle's contents and B-link invariants after every chunk;
+    early chunks took pages of their own, forced ones none."""
+    rng = np.random.default_rng(4242)
+    H = shm._hooks()
+    trees = {m: shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16) for m in ("early", "late")}
+    orc = OracleTree(256 << 20)
+    universe = hashed_keys(1, 120001)
+    pre = universe[:20000]
+    for t in trees.values():
+        gpu_insert(t, pre, pre + U64(5))
+    orc.apply_batch(pre, pre + U64(5))
+    took = []
+    for _ in range(6):
+        b = int(rng.integers(8000, 1 << 16))
+        ks = universe[rng.integers(0, universe.size, b)]
+        vs = rng.integers(1, 1 << 62, b).astype(U64)
+        vs[rng.random(b) < 0.05] = 0  # deletes
+        for mode, t in trees.items():
+            if mode == "late":
+                assert H.shm__upper_force(t.h, 4) == 0
+            gpu_insert(t, ks, vs)
+            ep = early_pages(t)
+            if mode == "late":
+                assert ep == 0
+            else:
+                took.append(ep)
+        orc.apply_batch(ks, vs)
+        for t in trees.values():
+            compare_contents(t, orc)
+    assert orc.check()[0] == 0
+    assert sum(took) > 0, took
+    for t in trees.values():
+        t.close()
+
+
+def test_early_split_block_list_overflow(lib_ok):
+    """Every leaf of a 3M-key tree splits in one chunk: a block of the upsert
+    kernel finds more small splits than its early list holds (64), so the
+    chunk has early splits and k_upper splits side by side.  Every key reads
+    back with its value and the tree keeps its invariants (size-independent
+    properties: the oracle would take minutes at this size)."""
+    n = 3_000_000
+    t = shm.Tree(arena_bytes=1 << 30, max_batch=1 << 22)
+    ev = np.arange(1, n + 1, dtype=U64) * U64(2)
+    gpu_insert(t, ev, ev + U64(1))  # a leaf root at first: all of it k_upper's
+    od = ev + U64(1)  # every leaf gets as many new keys as it holds
+    gpu_insert(t, od, od * U64(3))
+    assert early_pages(t) > 0
+    allk = np.concatenate([ev, od])
+    v, f = gpu_search(t, allk)
+    assert f.all(), int((f == 0).sum())
+    assert np.array_equal(v, np.concatenate([ev + U64(1), od * U64(3)]))
+    st = t.check()
+    assert st["keys"] == 2 * n, st
+    t.close()
+
+
 def test_directory_ties_start_at_the_leaf(lib_ok):
     """A directory entry's split points are the top 32 bits of each leaf's
     lowest fence within the prefix, so a lookup of a leaf's FIRST key ties

@@ -32,7 +32,7 @@ def main():
     fn = lib.shm__upper_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     fn(t.h, 1, None)
-    out = (ctypes.c_uint64 * (32 + 10 * 256))()
+    out = (ctypes.c_uint64 * (32 + 10 * 256 + 4 * 1024))()
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     for name, zn in (("c5", 2 * n), ("c3", n)):
@@ -57,6 +57,7 @@ def main():
                 v = [(x - t0) / 100.0 for x in bs[p] if x]
                 row.append("%.1f/%.1f" % (sum(v) / max(len(v), 1), max(v) if v else 0))
             print("   bin_unique phases (mean/max us):", " ".join(row), flush=True)
+            upsert_rows(out, ts[0])
             # k_upper per block: start and end clocks since block 0's first stamp
             st = [int(out[32 + 8 * 256 + x]) for x in range(256)]
             en = [int(out[32 + 9 * 256 + x]) for x in range(256)]
@@ -72,6 +73,36 @@ def main():
                       flush=True)
     fn(t.h, 0, None)
     t.close()
+
+
+def upsert_rows(out, s0):
+    """The upsert kernel's per-block clocks (us since k_upper's block 0
+    start of the same chunk is not comparable: relative to the earliest
+    upsert block start) and early-split counts."""
+    base = 32 + 10 * 256
+    st = [int(out[base + x]) for x in range(1024)]
+    mid = [int(out[base + 1024 + x]) for x in range(1024)]
+    en = [int(out[base + 2048 + x]) for x in range(1024)]
+    ne = [int(out[base + 3072 + x]) for x in range(1024)]
+    blocks = [i for i in range(1024) if st[i] and en[i] >= st[i]]
+    if not blocks:
+        return
+    t0 = min(st[i] for i in blocks)
+    q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))]  # noqa: E731
+    ss = sorted((st[i] - t0) / 100.0 for i in blocks)
+    mm = sorted((mid[i] - t0) / 100.0 for i in blocks if mid[i])
+    ee = sorted((en[i] - t0) / 100.0 for i in blocks)
+    sp = sorted((en[i] - mid[i]) / 100.0 for i in blocks if mid[i] and ne[i])
+    hist = {}
+    for i in blocks:
+        hist[ne[i]] = hist.get(ne[i], 0) + 1
+    print("   upsert blocks %d: start p50/max %.1f/%.1f, in-place done p50/p90/max %.1f/%.1f/%.1f, "
+          "end p50/p90/max %.1f/%.1f/%.1f; split time (blocks with splits) p50/p90/max %s; "
+          "early splits per block %s" %
+          (len(blocks), q(ss, .5), ss[-1], q(mm, .5) if mm else 0, q(mm, .9) if mm else 0,
+           mm[-1] if mm else 0, q(ee, .5), q(ee, .9), ee[-1],
+           "%.1f/%.1f/%.1f" % (q(sp, .5), q(sp, .9), sp[-1]) if sp else "-",
+           dict(sorted(hist.items()))), flush=True)
 
 
 if __name__ == "__main__":
