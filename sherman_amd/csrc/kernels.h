@@ -272,7 +272,7 @@ constexpr int kUpperStamps = 32;
 // + the upsert kernel's per-block clocks (start, in-place groups done, end)
 // and early-split counts, rows of 1024 (tools/upper_stamps.py)
 constexpr int kUpsertStamps = kUpperStamps + 10 * 256;
-constexpr int kStampWords = kUpsertStamps + 4 * 1024;
+constexpr int kStampWords = kUpsertStamps + 9 * 1024;
 uint32_t upper_blocks();
 // k_upper's blocks (512 threads) fit a CU at all
 bool upper_resident();

@@ -898,11 +898,15 @@ struct EarlyItem {
 
 // One early split, one wave (L: the wave's LDS); base = the superblock's
 // next_page (early allocations count from it).  Returns error bits.
+// clk (diagnostic, nullable): lane 0 records the wall clock at the start,
+// once the page is staged, after the builds, once the parent's word is
+// known and at the end, words 1024 apart
 __device__ __forceinline__ uint32_t split_early(const UpperArgs& a, WaveLds& L,
                                                 const EarlyItem& it, uint64_t base,
-                                                uint64_t cap) {
+                                                uint64_t cap, uint64_t* clk = nullptr) {
   uint32_t err = 0;
   const int lane = lane_id();
+  if (clk && lane == 0) clk[0] = wall_clock64();
   const int P = (int)(it.pv & 0xFFu);
   const uint32_t ver = it.pv >> 8;
   // the page, the ops (<= 64 staged) and the parent's word, in one round trip
@@ -934,6 +938,7 @@ __device__ __forceinline__ uint32_t split_early(const UpperArgs& a, WaveLds& L,
     L.o_val[lane] = ov0;
   }
   wave_lds_sync();
+  if (clk && lane == 0) clk[1024] = wall_clock64();
   const Ops o = few ? Ops{L.o_key, L.o_val, 0, it.nb} : Ops{a.op_key, a.op_val, it.st, it.nb};
   const int na = leaf_survivors(L, o);
   for (int p = 1; p < P; ++p) {
@@ -945,8 +950,11 @@ __device__ __forceinline__ uint32_t split_early(const UpperArgs& a, WaveLds& L,
     }
   }
   (void)build_leaf_page(a, L, h, na, o, SplitPage{0, P, it.T, it.first, it.page});
+  if (clk && lane == 0) clk[2 * 1024] = wall_clock64();
   const bool held = pre && rl64((uint64_t)lk_old, 0) <= a.tag;
+  if (clk && lane == 0) clk[3 * 1024] = wall_clock64() | (held ? 1ull << 63 : 0ull);
   propagate(a, L, (uint32_t)(P - 1), 1, base, cap, err, it.hint1, held);
+  if (clk && lane == 0) clk[4 * 1024] = wall_clock64();
   return err;
 }
 

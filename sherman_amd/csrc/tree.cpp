@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <mutex>
+#include <optional>
 #include <vector>
 
 #include "../../include/sherman_amd.h"
@@ -1420,11 +1421,19 @@ int shm_insert_order(shm_tree* t, const uint64_t* keys, const uint64_t* vals, ui
   std::lock_guard<std::mutex> g(t->mu);
   if (t->n_pend >= 2) return SHM_EAGAIN;  // two op-buffer parities
   hipStream_t s = pick(stream);
-  // with SHM_FLAG_SORT_GETS an ordered search shares the ordering scratch:
-  // the ordering is then ordered like an exclusive call
+  // The ordering reads only the batch and writes the insert workspace, whose
+  // users it waits for itself (insert_order: ord_ev, app_ev), so it takes no
+  // part in the tree's call ordering: it neither waits for the calls before
+  // it nor makes the next tree change wait for it (the apply waits for its
+  // own ticket only) -- chunk i + 1 is ordered beside chunk i's tree phase.
+  // With SHM_FLAG_SORT_GETS an ordered search shares the ordering scratch:
+  // the ordering is then ordered like an exclusive call.
   const bool sorted = (t->cfg.flags & SHM_FLAG_SORT_GETS) != 0;
-  Order ord(t, s, sorted);
-  if (ord.rc) return ord.rc;
+  std::optional<Order> ord;
+  if (sorted) {
+    ord.emplace(t, s, true);
+    if (ord->rc) return ord->rc;
+  }
   shm_tree::Pending& pd = t->pend[t->n_pend];
   pd.pr = shm_tree::ProfRec{};
   if (const int rc = insert_begin(t, s, keys, vals, n, false, &pd.tag, pd.pr)) return rc;

@@ -460,7 +460,10 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
     for (;;) {
       uint32_t x;
       if (take_early(&s_q, x)) {
-        err |= split_early(u, s_wl[wv], s_q.item[x], cursor0, cap);
+        err |= split_early(u, s_wl[wv], s_q.item[x], cursor0, cap,
+                           u.stamps && x == 0 && blockIdx.x < 1024
+                               ? u.stamps + kUpsertStamps + 4 * 1024 + blockIdx.x
+                               : nullptr);
         continue;
       }
       uint32_t act = 0;

@@ -32,7 +32,7 @@ def main():
     fn = lib.shm__upper_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     fn(t.h, 1, None)
-    out = (ctypes.c_uint64 * (32 + 10 * 256 + 4 * 1024))()
+    out = (ctypes.c_uint64 * (32 + 10 * 256 + 9 * 1024))()
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     for name, zn in (("c5", 2 * n), ("c3", n)):
@@ -103,6 +103,21 @@ def upsert_rows(out, s0):
            mm[-1] if mm else 0, q(ee, .5), q(ee, .9), ee[-1],
            "%.1f/%.1f/%.1f" % (q(sp, .5), q(sp, .9), sp[-1]) if sp else "-",
            dict(sorted(hist.items()))), flush=True)
+    # the first early split of each block: its phases (us)
+    ph = [[int(out[base + (4 + r) * 1024 + x]) for x in range(1024)] for r in range(5)]
+    rows = []
+    held = 0
+    for x in range(1024):
+        v = [ph[r][x] & ((1 << 63) - 1) for r in range(5)]
+        if all(v) and v[4] >= v[0] and v[0] >= t0:
+            held += ph[3][x] >> 63
+            rows.append([(v[r + 1] - v[r]) / 100.0 for r in range(4)])
+    if rows:
+        cols = list(zip(*rows))
+        desc = " ".join("%s p50/max %.1f/%.1f" % (nm, sorted(c)[len(c) // 2], max(c))
+                        for nm, c in zip(("load", "build", "lock", "propagate"), cols))
+        print("   first early split per block (%d, parent word held at once %d): %s" %
+              (len(rows), held, desc), flush=True)
 
 
 if __name__ == "__main__":
