@@ -14,7 +14,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsherman_amd.so")
+# SHM_LIB_PATH: another build of the library (A/B of builds, tools/ab_builds.sh)
+LIB_PATH = os.environ.get("SHM_LIB_PATH") or os.path.join(_HERE, "libsherman_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sherman_amd.h")
 
 SHM_OK = 0

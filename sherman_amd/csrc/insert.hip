@@ -193,6 +193,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
   const uint32_t v_nb = (uint32_t)t < nb ? ctl->leaf_nb[par][t] : 0u;
   const uint64_t n_del = *a.n_del;
+  const uint32_t late = ctl->late[par][0];
   // pages the upsert kernel's early splits took from next_page on (theirs
   // come first; failed takes past the capacity used no page)
   const uint64_t ua = ctl->ualloc[par][0];
@@ -204,18 +205,25 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     rn0 = __hip_atomic_load(&ctl->root_new[par][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     err0 = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // no split left to k_upper and no delete (C3's chunks, and C5's once its
+  // splits are early): block 0 alone zeroes the next chunk's counters and
+  // writes the superblock below; the other blocks leave at once
+  const bool quick = late == 0 && n_del == 0 && !a.force_abort;
+  if (quick && b != 0) return;
+  const uint64_t z0 = quick ? (uint64_t)t : tid, zs = quick ? (uint64_t)kUpT : T;
   // the other parity's counters and hand-off words start the next chunk at 0
-  for (uint64_t j = tid; j < (uint64_t)kMaxUpper; j += T) {
+  for (uint64_t j = z0; j < (uint64_t)kMaxUpper; j += zs) {
     ctl->leaf_np[par ^ 1][j] = 0;
     ctl->leaf_ns[par ^ 1][j] = 0;
     ctl->leaf_nb[par ^ 1][j] = 0;
   }
-  for (uint64_t j = tid; j < (uint64_t)kUpPhases * 32; j += T) {
+  for (uint64_t j = z0; j < (uint64_t)kUpPhases * 32; j += zs) {
     (&ctl->tk[par ^ 1][0][0])[j] = 0;
     (&ctl->dn[par ^ 1][0][0])[j] = 0;
   }
-  if (tid < 16) ctl->lvl_sep[par ^ 1][tid] = 0;
-  if (tid == 0) {
+  if (z0 < 16) ctl->lvl_sep[par ^ 1][z0] = 0;
+  if (z0 == 0) {
+    ctl->late[par ^ 1][0] = 0;
     ctl->abort[par ^ 1][0] = 0;
     ctl->alloc[par ^ 1][0] = 0;
     ctl->made[par ^ 1][0] = 0;
@@ -225,8 +233,8 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   }
   // leaf level: the upsert kernel left per-range new-page / split counts
   __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
-  uint32_t total, nsplit, nbig;
-  {
+  uint32_t total = 0, nsplit = 0, nbig = 0;
+  if (!quick) {
     const uint32_t xnp = block_scan(v_np, s_red, &total);
     const uint32_t xns = block_scan(v_ns, s_red, &nsplit);
     nbig = block_sum(v_nb, s_red);

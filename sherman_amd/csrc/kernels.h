@@ -142,6 +142,9 @@ struct UpperCtl {
   // pages the upsert kernel's early splits took (leaf and internal), from the
   // superblock's next_page on; k_upper's own pages follow them
   uint64_t ualloc[2][16];
+  // set (plain stores) by the upsert kernel when it leaves a split to k_upper:
+  // unset, a chunk without deletes needs only k_upper's block 0
+  uint32_t late[2][32];
 };
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid

@@ -114,6 +114,8 @@ struct shm_tree {
   // last build (stale entries only cost B-link right moves)
   bool err_pending = false;  // kernels ran since d_err was last read back
   uint32_t reads_since_write = 0;  // search calls since the last insert chunk (dir_stale)
+  uint64_t np_seen = 0;            // the page count the last insert chunk saw (dir_stale)
+  uint32_t quiet_chunks = 0;       // insert chunks in a row that saw it unchanged
   uint64_t* dir = nullptr;
   uint32_t dir_bits = 0;
   uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
@@ -372,9 +374,16 @@ bool dir_read_phase_on() {
   }();
   return on;
 }
+// ... and likewise once the tree has gone quiet: kQuietChunks insert chunks
+// in a row saw the same page count (updates only, C3's mix after the load),
+// so a write-heavy workload that no longer splits also gets one rebuild
+// instead of running on the directory of up to 1/32 growth ago (C3 lost 7 %
+// to 0.01 right moves per get when the load's last rebuild fell early)
+constexpr uint32_t kQuietChunks = 2;
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
-  return dir_read_phase_on() && t->reads_since_write >= kReadPhase && t->next_page != t->dir_np;
+  return dir_read_phase_on() && t->next_page != t->dir_np &&
+         (t->reads_since_write >= kReadPhase || t->quiet_chunks >= kQuietChunks);
 }
 
 // directory entries in fingerprint form (SHM_DIR_FP=0: the round-2 form, A/B)
@@ -701,6 +710,12 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
   t->reads_since_write = 0;
+  if (t->next_page == t->np_seen) {
+    if (t->quiet_chunks < kQuietChunks) ++t->quiet_chunks;
+  } else {
+    t->quiet_chunks = 0;
+    t->np_seen = t->next_page;
+  }
   // the byte marks repeat every 255 chunks: clear them when they wrap, so
   // no page still carries this chunk's mark from 255 chunks ago
   if (!seg_from_slots() && dev::new_mark(tag) == 1)

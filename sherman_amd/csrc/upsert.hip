@@ -275,6 +275,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     }
     a.seg_newpages[gq] = queued ? 0u : P - 1;
     if (P > 1 && !queued) {
+      a.ctl->late[a.par][0] = 1u;
       // k_upper block range of this segment (insert.hip block_range)
       const uint32_t r = (uint32_t)((gq * a.up_nb) / num_seg);
       atomicAdd(&a.ctl->leaf_np[a.par][r], P - 1);
