@@ -208,9 +208,10 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   // no split left to k_upper and no delete (C3's chunks, and C5's once its
   // splits are early): block 0 alone zeroes the next chunk's counters and
   // writes the superblock below; the other blocks leave at once
-  const bool quick = late == 0 && n_del == 0 && !a.force_abort;
-  if (quick && b != 0) return;
-  const uint64_t z0 = quick ? (uint64_t)t : tid, zs = quick ? (uint64_t)kUpT : T;
+  const bool quick = a.quick != 0 && late == 0 && n_del == 0 && !a.force_abort;
+  const bool solo0 = quick && a.quick == 2;
+  if (solo0 && b != 0) return;
+  const uint64_t z0 = solo0 ? (uint64_t)t : tid, zs = solo0 ? (uint64_t)kUpT : T;
   // the other parity's counters and hand-off words start the next chunk at 0
   for (uint64_t j = z0; j < (uint64_t)kMaxUpper; j += zs) {
     ctl->leaf_np[par ^ 1][j] = 0;
@@ -269,9 +270,12 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
                              __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.pub + 3, splits0 + (cursor0e - cursor0), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
+      // the chunk's tag: with new pages, or whenever the host asks (its
+      // directory is behind the tree: tree.cpp dir_stale's quiet rule)
+      if (a.pub && (cursor0e != cursor0 || a.pub_always))
+        __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       sb->batches = a.batch;
     }
     stamp();
@@ -580,8 +584,9 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       __hip_atomic_store(a.pub + 2, (uint64_t)root_level, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.pub + 3, splits0 + made, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (a.pub && (cursor != cursor0 || a.pub_always))
+      __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // every block's error bits are in (released before its `done` arrival):
     // the first chunk to see a bit other than kErrKeyMax names itself
     if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kErrKeyMax)

@@ -267,6 +267,13 @@ struct UpperArgs {
   // the upsert kernel's copy (upsert.hip): small splits are built and
   // propagated there, their pages counted in UpperCtl.ualloc; 0 in k_upper's
   uint32_t early;
+  // A/B (SHM_UPPER_QUICK): with no split left to k_upper and no delete, 0 =
+  // every block scans the counts as before, 1 = the scans are skipped, 2 =
+  // block 0 alone runs
+  uint32_t quick;
+  // publish the chunk's tag in the host mirror even without new pages (the
+  // host's directory is behind the tree and it watches for a quiet tree)
+  uint32_t pub_always;
 };
 constexpr int kUpperStamps = 32;
 // diagnostic clock words: k_upper's, then k_bin_unique's 8 phases x kCoarse bins

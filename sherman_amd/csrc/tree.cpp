@@ -114,8 +114,10 @@ struct shm_tree {
   // last build (stale entries only cost B-link right moves)
   bool err_pending = false;  // kernels ran since d_err was last read back
   uint32_t reads_since_write = 0;  // search calls since the last insert chunk (dir_stale)
-  uint64_t np_seen = 0;            // the page count the last insert chunk saw (dir_stale)
-  uint32_t quiet_chunks = 0;       // insert chunks in a row that saw it unchanged
+  uint64_t pub_batch = 0;          // the chunk tag the mirror last showed (mirror)
+  uint64_t pub_seen = 0;           // the tag at the last quiet-rule look (insert_apply)
+  uint64_t np_seen = 0;            // the page count then
+  uint32_t quiet_chunks = 0;       // published chunks in a row that left it unchanged
   uint64_t* dir = nullptr;
   uint32_t dir_bits = 0;
   uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
@@ -345,6 +347,7 @@ bool use_top(const shm_tree* t) {
 // next_page, root_level, splits}; exact once the device is idle
 void mirror(shm_tree* t) {
   const volatile uint64_t* p = reinterpret_cast<const volatile uint64_t*>(t->h_pin) + kPubWord / 2;
+  t->pub_batch = p[0];  // first: the words below are at least this chunk's
   t->next_page = p[1];
   t->root_level = (uint32_t)p[2];
   t->splits = p[3];
@@ -374,11 +377,14 @@ bool dir_read_phase_on() {
   }();
   return on;
 }
-// ... and likewise once the tree has gone quiet: kQuietChunks insert chunks
-// in a row saw the same page count (updates only, C3's mix after the load),
-// so a write-heavy workload that no longer splits also gets one rebuild
-// instead of running on the directory of up to 1/32 growth ago (C3 lost 7 %
-// to 0.01 right moves per get when the load's last rebuild fell early)
+// ... and likewise once the tree has gone quiet: the mirror showed
+// kQuietChunks newer chunk tags in a row with the same page count (updates
+// only, C3's mix after the load; while the directory is behind, every chunk
+// publishes its tag, UpperArgs.pub_always), so a write-heavy workload that no
+// longer splits also gets one rebuild instead of running on the directory of
+// up to 1/32 growth ago (C3 lost 7 % to 0.01 right moves per get when the
+// load's last rebuild fell early).  A mirror that merely lags (the host ahead
+// of the device) shows no newer tag, so it never looks quiet
 constexpr uint32_t kQuietChunks = 2;
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
@@ -710,11 +716,14 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
   t->reads_since_write = 0;
-  if (t->next_page == t->np_seen) {
-    if (t->quiet_chunks < kQuietChunks) ++t->quiet_chunks;
-  } else {
-    t->quiet_chunks = 0;
-    t->np_seen = t->next_page;
+  if (t->pub_batch != t->pub_seen) {  // a newer chunk published since the last look
+    if (t->next_page == t->np_seen) {
+      if (t->quiet_chunks < kQuietChunks) ++t->quiet_chunks;
+    } else {
+      t->quiet_chunks = 0;
+      t->np_seen = t->next_page;
+    }
+    t->pub_seen = t->pub_batch;
   }
   // the byte marks repeat every 255 chunks: clear them when they wrap, so
   // no page still carries this chunk's mark from 255 chunks ago
@@ -800,6 +809,12 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
     return e && e[0] == '0';
   }();
   u.no_prelock = no_prelock ? 1u : 0u;
+  static const uint32_t quick = [] {
+    const char* e = getenv("SHM_UPPER_QUICK");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
+  u.quick = quick;
+  u.pub_always = t->next_page != t->dir_np ? 1u : 0u;
   // small splits built by the upsert kernel itself (SHM_EARLY_SPLIT=0: all
   // left to k_upper, round 4's path); the forced k_upper paths keep theirs
   static const bool no_early = [] {
