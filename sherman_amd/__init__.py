@@ -211,22 +211,32 @@ def _stream_ptr(stream):
     return stream.cuda_stream or None
 
 
+class _StreamDone:
+    """Completion of the work queued so far on a raw hipStream_t (None = the
+    null stream) of `device`, for a pending result: .synchronize() waits for
+    that stream.  No event is recorded at issue time -- a record between two
+    kernels leaves the device idle ~5-7 us (tools/event_gap.hip) -- so the
+    wait may also cover work queued there later, never less."""
+
+    def __init__(self, stream_ptr, device):
+        self.stream_ptr, self.device = stream_ptr, device
+
+    def synchronize(self):
+        import torch
+        s = (torch.cuda.ExternalStream(self.stream_ptr, device=self.device) if self.stream_ptr
+             else torch.cuda.default_stream(self.device))
+        s.synchronize()
+
+
 def _record_on(stream_ptr, device):
-    """A torch event recorded on the raw hipStream_t `stream_ptr` (None = the
-    null stream) of `device`: completion of the work queued there so far."""
-    import torch
-    ev = torch.cuda.Event()
-    s = (torch.cuda.ExternalStream(stream_ptr, device=device) if stream_ptr
-         else torch.cuda.default_stream(device))
-    ev.record(s)
-    return ev
+    return _StreamDone(stream_ptr, device)
 
 
 class PendingRange:
     """Result of Tree.range_query_batch_async: (counts, values) once the
-    scans have run.  tot = device (total, error bits); done = a torch event
-    recorded on the stream the scans were queued on (resolved when they were
-    issued, so .result() waits for them whatever stream is current then)."""
+    scans have run.  tot = device (total, error bits); done = the stream the
+    scans were queued on (_StreamDone: resolved when they were issued, so
+    .result() waits for them whatever stream is current then)."""
 
     def __init__(self, tree, counts, vals, tot=None, done=None):
         self.tree, self.counts, self.vals, self.tot, self.done = tree, counts, vals, tot, done

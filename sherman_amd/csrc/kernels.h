@@ -145,6 +145,10 @@ struct UpperCtl {
   // set (plain stores) by the upsert kernel when it leaves a split to k_upper:
   // unset, a chunk without deletes needs only k_upper's block 0
   uint32_t late[2][32];
+  // the tag of the last chunk whose k_upper has finished with the chunk's op
+  // buffers (system-scope store): the ordering two chunks on waits for it
+  // with a stream wait-value (tree.cpp insert_order) instead of an event
+  uint64_t applied[16];
 };
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid

@@ -162,26 +162,32 @@ struct shm_tree {
   };
   GetWs gws[2];           // gws[0] aliases the insert workspace (ka, kb, ia, ib, part_*)
   int next_gws = 0;
-  struct StreamEv {
-    hipStream_t s;
-    hipEvent_t ev;
+  // A call's completion point on its stream, recorded lazily (Order): the
+  // event is recorded at the stream's tail only when a call on another
+  // stream first has to follow it -- an event record between two kernels
+  // leaves the device idle ≈ 4.6 µs (tools/event_gap.hip), so none is placed
+  // where nobody waits.  The tail then holds everything issued there so far:
+  // the first waiter may wait for a little more than it needs, never less.
+  struct Mark {
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    bool valid = false;     // a call to follow exists
+    bool recorded = false;  // ev marks it (recorded at the first wait)
   };
-  std::vector<StreamEv> shared_ev;  // last shared call per stream
-  hipEvent_t ex_ev = nullptr;       // last exclusive call
-  hipStream_t ex_s = nullptr;
-  bool ex_valid = false;
+  std::vector<Mark> shared_ev;  // last shared calls per stream, since the last exclusive one
+  Mark ex;                      // last exclusive call
   // insert ordering pipeline.  The ordering of chunk `tag` writes the op
   // buffers of parity tag & 1 (uk / uv / dk / counts, op_keys() below),
   // which the apply of chunk tag - 2 read last (app_ev); every ordering
   // reuses the ordering scratch (ka .. bins), so it follows the previous
   // ordering (ord_ev).  A later chunk's ordering may therefore run on
   // another stream beside this chunk's apply.
-  hipEvent_t app_ev[2] = {nullptr, nullptr};
+  // (app: the chunk tag whose k_upper stores UpperCtl.applied, waited for
+  // with hipStreamWaitValue64; ord: a lazily recorded mark)
+  uint64_t app_tag[2] = {0, 0};
   hipStream_t app_s[2] = {nullptr, nullptr};
   bool app_valid[2] = {false, false};
-  hipEvent_t ord_ev = nullptr;
-  hipStream_t ord_s = nullptr;
-  bool ord_valid = false;
+  Mark ord;
   // chunks ordered by shm_insert_order and not yet applied, oldest first
   struct Pending {
     uint32_t tag;
@@ -192,9 +198,7 @@ struct shm_tree {
   };
   Pending pend[2];
   int n_pend = 0;
-  hipEvent_t gws_ev[2] = {nullptr, nullptr};  // last user of each get workspace
-  hipStream_t gws_s[2] = {nullptr, nullptr};
-  bool gws_valid[2] = {false, false};
+  Mark gws_m[2];  // last user of each get workspace
 };
 
 namespace {
@@ -255,10 +259,27 @@ hipEvent_t new_event() {
   return e;
 }
 
+// stream s follows the call mark m notes (its stream's tail, recorded at the
+// first wait: shm_tree::Mark)
+int follow(shm_tree::Mark& m, hipStream_t s) {
+  if (!m.valid || m.s == s) return SHM_OK;
+  if (!m.recorded) {
+    if (!m.ev) m.ev = new_event();
+    if (!m.ev || hipEventRecord(m.ev, m.s) != hipSuccess) return SHM_EIO;
+    m.recorded = true;
+  }
+  return hipStreamWaitEvent(s, m.ev, 0) == hipSuccess ? SHM_OK : SHM_EIO;
+}
+void note(shm_tree::Mark& m, hipStream_t s) {
+  m.s = s;
+  m.valid = true;
+  m.recorded = false;
+}
+
 // Cross-stream ordering of one API call (shm_tree: shared / exclusive calls).
 // Constructed under t->mu before the call's first launch; the destructor
-// records the call's completion event on its stream.  Waits are skipped for
-// events of the same stream (stream order already covers them).
+// notes the call's stream (no event: shm_tree::Mark).  Waits are skipped for
+// marks of the same stream (stream order already covers them).
 struct Order {
   shm_tree* t;
   hipStream_t s;
@@ -266,63 +287,50 @@ struct Order {
   int ws = -1;  // get workspace used by a shared call (-1: none)
   int rc = SHM_OK;
   Order(shm_tree* tt, hipStream_t ss, bool exclusive) : t(tt), s(ss), ex(exclusive) {
-    if (t->ex_valid && t->ex_s != s) wait(t->ex_ev);
+    wait(t->ex);
     if (ex) {
-      for (const auto& r : t->shared_ev)
-        if (r.s != s) wait(r.ev);
-      for (int j = 0; j < 2; ++j)
-        if (t->gws_valid[j] && t->gws_s[j] != s) wait(t->gws_ev[j]);
+      for (auto& m : t->shared_ev) wait(m);
+      for (int j = 0; j < 2; ++j) wait(t->gws_m[j]);
     }
   }
   // a shared call that turns exclusive (a directory rebuild)
   void make_exclusive() {
     if (ex) return;
     ex = true;
-    for (const auto& r : t->shared_ev)
-      if (r.s != s) wait(r.ev);
-    for (int j = 0; j < 2; ++j)
-      if (t->gws_valid[j] && t->gws_s[j] != s) wait(t->gws_ev[j]);
+    for (auto& m : t->shared_ev) wait(m);
+    for (int j = 0; j < 2; ++j) wait(t->gws_m[j]);
   }
   // take the next get workspace; returns its index
   int take_ws() {
     ws = t->next_gws;
     t->next_gws ^= 1;
-    if (!ex && t->gws_valid[ws] && t->gws_s[ws] != s) wait(t->gws_ev[ws]);
+    if (!ex) wait(t->gws_m[ws]);
     return ws;
   }
-  void wait(hipEvent_t e) {
-    if (hipStreamWaitEvent(s, e, 0) != hipSuccess) rc = SHM_EIO;
+  void wait(shm_tree::Mark& m) {
+    if (follow(m, s) != SHM_OK) rc = SHM_EIO;
   }
   ~Order() {
     if (ex) {
-      if (!t->ex_ev) t->ex_ev = new_event();
-      if (t->ex_ev && hipEventRecord(t->ex_ev, s) == hipSuccess) {
-        t->ex_s = s;
-        t->ex_valid = true;
-        // the waits above ordered this call after every earlier one
-        for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
-        t->shared_ev.clear();
-        t->gws_valid[0] = t->gws_valid[1] = false;
-      }
+      // the waits above ordered this call after every earlier one
+      note(t->ex, s);
+      for (auto& m : t->shared_ev) m.valid = false;
+      t->gws_m[0].valid = t->gws_m[1].valid = false;
       return;
     }
-    shm_tree::StreamEv* r = nullptr;
-    for (auto& x : t->shared_ev)
-      if (x.s == s) r = &x;
+    shm_tree::Mark* r = nullptr;
+    for (auto& m : t->shared_ev)
+      if (m.s == s) r = &m;
     if (!r) {
-      hipEvent_t e = new_event();
-      if (!e) return;
-      t->shared_ev.push_back({s, e});
-      r = &t->shared_ev.back();
-    }
-    (void)hipEventRecord(r->ev, s);
-    if (ws >= 0) {
-      if (!t->gws_ev[ws]) t->gws_ev[ws] = new_event();
-      if (t->gws_ev[ws] && hipEventRecord(t->gws_ev[ws], s) == hipSuccess) {
-        t->gws_s[ws] = s;
-        t->gws_valid[ws] = true;
+      for (auto& m : t->shared_ev)
+        if (!m.valid) r = &m;  // a slot of a stream no call waits for any more
+      if (!r) {
+        t->shared_ev.push_back(shm_tree::Mark{});
+        r = &t->shared_ev.back();
       }
     }
+    note(*r, s);
+    if (ws >= 0) note(t->gws_m[ws], s);
   }
 };
 
@@ -637,15 +645,6 @@ uint64_t* op_dels(shm_tree* t, uint32_t tag) { return t->dk + (uint64_t)(tag & 1
 // {upserts, deletes} of the chunk (k_bin_unique)
 uint64_t* op_counts(shm_tree* t, uint32_t tag) { return t->d_counts + 16 * (tag & 1u); }
 
-int record(shm_tree* t, hipEvent_t* ev, hipStream_t* es, bool* valid, hipStream_t s) {
-  if (!*ev) *ev = new_event();
-  if (!*ev) return SHM_EIO;
-  HIP_OK(hipEventRecord(*ev, s));
-  *es = s;
-  *valid = true;
-  return SHM_OK;
-}
-
 // One insert chunk (n <= nmax ops), issued without a host wait:
 //   1. ordering: k_tile_dedup, coarse partition, k_bin_unique
 //      -> uk / uv (upserts, key order, last writer) and dk (deletes); counts
@@ -664,9 +663,13 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                  uint64_t n, uint32_t tag, bool skip_pad) {
   // the scratch's last user (the previous ordering) and the op buffers'
   // (the apply of tag - 2), when they ran on another stream
-  if (t->ord_valid && t->ord_s != s) HIP_OK(hipStreamWaitEvent(s, t->ord_ev, 0));
+  if (const int rc = follow(t->ord, s)) return rc;
   const uint32_t p = tag & 1u;
-  if (t->app_valid[p] && t->app_s[p] != s) HIP_OK(hipStreamWaitEvent(s, t->app_ev[p], 0));
+  // the apply of tag - 2 is done with the op buffers once k_upper stored its
+  // tag (a wait-value packet: the producer stream gets no event record)
+  if (t->app_valid[p] && t->app_s[p] != s)
+    HIP_OK(hipStreamWaitValue64(s, &t->ctl->applied[0], t->app_tag[p], hipStreamWaitValueGte,
+                                ~0ull));
   // Tile mode (chunks of <= kMaxTiles tiles, i.e. <= 1 Mi ops): the tiles
   // write their survivors sorted by coarse bin and k_bin_unique gathers its
   // bin's runs from every tile, so there is no coarse scatter pass (round 4;
@@ -696,7 +699,8 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                          t->d_err, t->part_S, &t->ctl->gate,
                          tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, tr, s);
   DBG(s, "ordering");
-  return record(t, &t->ord_ev, &t->ord_s, &t->ord_valid, s);
+  note(t->ord, s);
+  return SHM_OK;
 }
 
 // steps 2-5 on the ordered chunk of tag (the leaf directory is current)
@@ -882,8 +886,12 @@ int insert_finish(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag, shm_tree
   }
   const int rc = insert_apply(t, s, n, tag, pr);
   if (rc != SHM_OK) return rc;
+  // k_upper was queued: it stores the tag into UpperCtl.applied at its end
   const uint32_t p = tag & 1u;
-  return record(t, &t->app_ev[p], &t->app_s[p], &t->app_valid[p], s);
+  t->app_tag[p] = tag;
+  t->app_s[p] = s;
+  t->app_valid[p] = true;
+  return SHM_OK;
 }
 
 int insert_chunk(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_t* vals,
@@ -960,15 +968,14 @@ void free_all(shm_tree* t) {
     shm_tree::GetWs& w = t->gws[1];
     F(w.keys1); F(w.keys_out); F(w.pos1); F(w.src); F(w.M); F(w.S); F(w.chunks);
   }
-  for (auto& r : t->shared_ev) (void)hipEventDestroy(r.ev);
-  if (t->ex_ev) (void)hipEventDestroy(t->ex_ev);
-  for (hipEvent_t e : t->app_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (t->ord_ev) (void)hipEventDestroy(t->ord_ev);
+  for (auto& r : t->shared_ev)
+    if (r.ev) (void)hipEventDestroy(r.ev);
+  if (t->ex.ev) (void)hipEventDestroy(t->ex.ev);
+  if (t->ord.ev) (void)hipEventDestroy(t->ord.ev);
   for (auto& pd : t->pend)
     if (pd.ev) (void)hipEventDestroy(pd.ev);
-  for (hipEvent_t e : t->gws_ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& m : t->gws_m)
+    if (m.ev) (void)hipEventDestroy(m.ev);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
 }
