@@ -278,7 +278,9 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
         __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       sb->batches = a.batch;
       // no block of this launch reads the op buffers on this path
-      __hip_atomic_store(&ctl->applied[0], a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.pub)
+        __hip_atomic_store(a.pub + kPubApplied, a.batch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
     stamp();
     if (bclk) bclk[256] = wall_clock64();
@@ -589,12 +591,14 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     if (a.pub && (cursor != cursor0 || a.pub_always))
       __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // every block has finished (the `done` count): the op buffers are free
-    __hip_atomic_store(&ctl->applied[0], a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // every block's error bits are in (released before its `done` arrival):
     // the first chunk to see a bit other than kErrKeyMax names itself
     if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kErrKeyMax)
       atomicCAS(a.err + 1, 0u, (uint32_t)a.batch);
+    // every block has finished (the `done` count): the op buffers are free
+    if (a.pub)
+      __hip_atomic_store(a.pub + kPubApplied, a.batch, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

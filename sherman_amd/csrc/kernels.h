@@ -145,11 +145,10 @@ struct UpperCtl {
   // set (plain stores) by the upsert kernel when it leaves a split to k_upper:
   // unset, a chunk without deletes needs only k_upper's block 0
   uint32_t late[2][32];
-  // the tag of the last chunk whose k_upper has finished with the chunk's op
-  // buffers (system-scope store): the ordering two chunks on waits for it
-  // with a stream wait-value (tree.cpp insert_order) instead of an event
-  uint64_t applied[16];
 };
+// UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
+// the chunk's op buffers (tree.cpp insert_order's flow control)
+constexpr int kPubApplied = 4;
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
 constexpr uint32_t kSmallSplit = 4;

@@ -17,9 +17,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <mutex>
 #include <optional>
+#include <thread>
 #include <vector>
 
 #include "../../include/sherman_amd.h"
@@ -36,6 +38,7 @@ constexpr uint32_t kRangeStage = 160;      // staged values per range scan
 constexpr uint64_t kRangeStageBytes = 256ull << 20;  // staging budget
 constexpr uint32_t kFlagWord = 512;        // read-back sequence word: byte 2048 of h_pin
 constexpr uint32_t kPubWord = 768;         // superblock mirror: u64 words 384.. of h_pin
+constexpr int kAppWaitMs = 2000;           // insert_order's host wait before an event fallback
 
 }  // namespace
 
@@ -182,11 +185,12 @@ struct shm_tree {
   // reuses the ordering scratch (ka .. bins), so it follows the previous
   // ordering (ord_ev).  A later chunk's ordering may therefore run on
   // another stream beside this chunk's apply.
-  // (app: the chunk tag whose k_upper stores UpperCtl.applied, waited for
-  // with hipStreamWaitValue64; ord: a lazily recorded mark)
+  // (app: the apply's chunk tag, which its k_upper publishes in the host
+  // mirror once it is done with the op buffers, and a lazily recorded mark
+  // of its stream; ord: a lazily recorded mark)
   uint64_t app_tag[2] = {0, 0};
-  hipStream_t app_s[2] = {nullptr, nullptr};
   bool app_valid[2] = {false, false};
+  Mark app_m[2];
   Mark ord;
   // chunks ordered by shm_insert_order and not yet applied, oldest first
   struct Pending {
@@ -665,11 +669,27 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   // (the apply of tag - 2), when they ran on another stream
   if (const int rc = follow(t->ord, s)) return rc;
   const uint32_t p = tag & 1u;
-  // the apply of tag - 2 is done with the op buffers once k_upper stored its
-  // tag (a wait-value packet: the producer stream gets no event record)
-  if (t->app_valid[p] && t->app_s[p] != s)
-    HIP_OK(hipStreamWaitValue64(s, &t->ctl->applied[0], t->app_tag[p], hipStreamWaitValueGte,
-                                ~0ull));
+  // The apply of tag - 2 (another stream) last read these op buffers.  Flow
+  // control on the host: its k_upper publishes its tag in the host mirror
+  // once it is done with them, and this call waits for that (in a pipeline
+  // the host then runs at most about two chunks ahead of the device).  The
+  // apply's stream gets no event record (≈ 4.6 µs of idle device between
+  // kernels, tools/event_gap.hip), and the device no polling wait (a
+  // wait-value kernel: a profiler that serialises kernels deadlocks on it).
+  // A wait past kAppWaitMs (the apply's stream held up by the caller) falls
+  // back to an event at that stream's tail.
+  if (t->app_valid[p] && t->app_m[p].s != s) {
+    const volatile uint64_t* ap =
+        reinterpret_cast<const volatile uint64_t*>(t->h_pin) + kPubWord / 2 + dev::kPubApplied;
+    if (*ap < t->app_tag[p]) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (*ap < t->app_tag[p] &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(kAppWaitMs))
+        std::this_thread::yield();
+      if (*ap < t->app_tag[p])
+        if (const int rc = follow(t->app_m[p], s)) return rc;
+    }
+  }
   // Tile mode (chunks of <= kMaxTiles tiles, i.e. <= 1 Mi ops): the tiles
   // write their survivors sorted by coarse bin and k_bin_unique gathers its
   // bin's runs from every tile, so there is no coarse scatter pass (round 4;
@@ -886,11 +906,11 @@ int insert_finish(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag, shm_tree
   }
   const int rc = insert_apply(t, s, n, tag, pr);
   if (rc != SHM_OK) return rc;
-  // k_upper was queued: it stores the tag into UpperCtl.applied at its end
+  // k_upper was queued: it publishes the tag once done with the op buffers
   const uint32_t p = tag & 1u;
   t->app_tag[p] = tag;
-  t->app_s[p] = s;
   t->app_valid[p] = true;
+  note(t->app_m[p], s);
   return SHM_OK;
 }
 
@@ -972,6 +992,8 @@ void free_all(shm_tree* t) {
     if (r.ev) (void)hipEventDestroy(r.ev);
   if (t->ex.ev) (void)hipEventDestroy(t->ex.ev);
   if (t->ord.ev) (void)hipEventDestroy(t->ord.ev);
+  for (auto& m : t->app_m)
+    if (m.ev) (void)hipEventDestroy(m.ev);
   for (auto& pd : t->pend)
     if (pd.ev) (void)hipEventDestroy(pd.ev);
   for (auto& m : t->gws_m)
