@@ -19,8 +19,10 @@ RX="k_tile_dedup|k_part_|k_bin_|k_locate|k_seg_|k_leaf_|k_tile_s|k_int_|k_new_ro
 B="$R/bench.py --workload $WL --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run \
   -- python3 $B --steps 20 --warmup 3 --profile-steps 0 > $OUT/trace_bench.json 2> $OUT/trace_bench.err || exit $?
+echo "profile_write $WL: trace done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $OUT/pmc_fetch -o run \
   -- python3 $B --steps 4 --warmup 1 --profile-steps 0 > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit $?
+echo "profile_write $WL: FETCH_SIZE done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $OUT/pmc_write -o run \
   -- python3 $B --steps 4 --warmup 1 --profile-steps 0 > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit $?
 python3 $R/tools/write_summary.py $OUT $WL > $OUT/summary.json || exit $?
