@@ -155,6 +155,11 @@ int shm_insert_batch_async(shm_tree *t, const uint64_t *keys, const uint64_t *va
  * call on the handle, before every later one).  At most two tickets are
  * outstanding (SHM_EAGAIN), applied oldest first (else SHM_EINVAL); other
  * insert calls are refused (SHM_EINVAL) while a ticket is outstanding.
+ * The ordering reuses the buffers of the chunk two tickets back: when that
+ * chunk was applied on another stream, shm_insert_order waits on the host
+ * until the device has finished with them (flow control: a pipelined caller
+ * stays about two chunks ahead of the device; after 2 s it queues a
+ * device-side wait instead and returns).
  * Errors are reported as for shm_insert_batch_async.  Tree::insert
  * (src/Tree.cpp:353-403) for a batch, as shm_insert_batch_async. */
 int shm_insert_order(shm_tree *t, const uint64_t *keys, const uint64_t *vals, uint64_t n,
