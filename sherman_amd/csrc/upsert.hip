@@ -432,6 +432,7 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
   const int wv = threadIdx.x >> 6;
   const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t num_seg = *a.num_seg_dev;
+  if (num_seg == 0) return;  // every op applied in place (C3's chunks): the block's only load
   const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
   // early splits need a root above the leaves (a leaf root grows the tree:
   // k_upper) and the direct path (SHM_UPPER_LISTS=1 sends all to the lists)
