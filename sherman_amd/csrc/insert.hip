@@ -39,6 +39,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "split_wave.h"
+#include "upper_quick.h"
 
 namespace shm {
 namespace dev {
@@ -159,6 +160,8 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   __shared__ uint32_t s_tk;  // the block's ticket
   __shared__ uint32_t s_list[kUpT];  // segment heads of one separator chunk
   __shared__ __attribute__((aligned(16))) LvlLds s_lvl;  // levels >= 2: one chunk
+  // completed by the segmentation kernel (no new key, no delete)
+  if (a.ctl->skip[a.par][0] == a.batch) return;
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t b = blockIdx.x, nb = gridDim.x;
   const uint64_t W = (uint64_t)nb * kUpWaves;
@@ -212,26 +215,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   const bool solo0 = quick && a.quick == 2;
   if (solo0 && b != 0) return;
   const uint64_t z0 = solo0 ? (uint64_t)t : tid, zs = solo0 ? (uint64_t)kUpT : T;
-  // the other parity's counters and hand-off words start the next chunk at 0
-  for (uint64_t j = z0; j < (uint64_t)kMaxUpper; j += zs) {
-    ctl->leaf_np[par ^ 1][j] = 0;
-    ctl->leaf_ns[par ^ 1][j] = 0;
-    ctl->leaf_nb[par ^ 1][j] = 0;
-  }
-  for (uint64_t j = z0; j < (uint64_t)kUpPhases * 32; j += zs) {
-    (&ctl->tk[par ^ 1][0][0])[j] = 0;
-    (&ctl->dn[par ^ 1][0][0])[j] = 0;
-  }
-  if (z0 < 16) ctl->lvl_sep[par ^ 1][z0] = 0;
-  if (z0 == 0) {
-    ctl->late[par ^ 1][0] = 0;
-    ctl->abort[par ^ 1][0] = 0;
-    ctl->alloc[par ^ 1][0] = 0;
-    ctl->made[par ^ 1][0] = 0;
-    ctl->root_new[par ^ 1][0] = 0;
-    ctl->done[par ^ 1][0] = 0;
-    ctl->ualloc[par ^ 1][0] = 0;
-  }
+  upper_zero_next(ctl, par, z0, zs);
   // leaf level: the upsert kernel left per-range new-page / split counts
   __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
   uint32_t total = 0, nsplit = 0, nbig = 0;

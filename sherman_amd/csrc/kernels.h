@@ -145,6 +145,9 @@ struct UpperCtl {
   // set (plain stores) by the upsert kernel when it leaves a split to k_upper:
   // unset, a chunk without deletes needs only k_upper's block 0
   uint32_t late[2][32];
+  // the tag of a chunk the segmentation kernel completed (no new key, no
+  // delete: upper_quick.h); its k_upper returns at once
+  uint64_t skip[2][16];
 };
 // UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
 // the chunk's op buffers (tree.cpp insert_order's flow control)
@@ -380,7 +383,7 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot = nullptr);
+                    const uint32_t* oslot = nullptr, const UpperArgs* quick = nullptr);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
 // wraps); tot = {total, *err} for the range scan's one read-back

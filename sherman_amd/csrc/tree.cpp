@@ -772,11 +772,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
-  dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
-                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
-                      seg_from_slots() ? t->oslot : nullptr);
-  DBG(s, "segment");
-  if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::UpperArgs u{};
   u.arena = t->arena;
   u.arena_bytes = t->arena_bytes;
@@ -847,6 +842,13 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   }();
   dev::UpperArgs ue = u;
   ue.early = no_early || (t->force_flags & 7u) ? 0u : 1u;
+  // a chunk with no new key and no delete is completed by the segmentation
+  // kernel's block 0 (u: k_upper's quick path; k_upper then returns at once)
+  dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
+                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
+                      seg_from_slots() ? t->oslot : nullptr, u.quick && !u.force_abort ? &u : nullptr);
+  DBG(s, "segment");
+  if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
   a.arena = t->arena;
   a.arena_bytes = t->arena_bytes;

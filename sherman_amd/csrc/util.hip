@@ -2,6 +2,7 @@
 // scans, multi-GPU routing, key generation).
 #include "device_common.h"
 #include "kernels.h"
+#include "upper_quick.h"
 
 namespace shm {
 namespace dev {
@@ -71,16 +72,33 @@ __device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint3
 // segments: seg_start / seg_page at each staged head, seg_end at its run's
 // last op (the count of staged heads up to and including that op is the
 // segment's position + 1).
+// A chunk without a new key (every op applied in place by k_locate, C3's
+// chunks): block 0 also completes it when it has no delete either -- k_upper's
+// quick path (upper_quick.h) -- and tags it in UpperCtl.skip, so the upsert
+// kernel (no segment) and k_upper return after one load
+__device__ __forceinline__ void seg_complete_unchanged(const UpperArgs& q) {
+  if (*q.n_del != 0) return;  // the deletes are k_upper's
+  upper_zero_next(q.ctl, q.par, threadIdx.x, blockDim.x);
+  if (threadIdx.x == 0) {
+    upper_finish_unchanged(q, __hip_atomic_load(q.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    q.ctl->skip[q.par][0] = q.batch;
+  }
+}
+
 __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t n,
                                                  const uint64_t* n_dev, uint64_t* lbw,
                                                  uint32_t* seg_start, uint32_t* seg_end,
                                                  uint64_t* seg_page, uint32_t* num_seg,
                                                  const uint8_t* pnew, uint32_t tag,
-                                                 const uint32_t* any_new, uint32_t* err) {
+                                                 const uint32_t* any_new, uint32_t* err,
+                                                 UpperArgs q, int has_q) {
   __shared__ uint32_t s_pre[kT / kWave];
   const uint32_t b = blockIdx.x;
   if (any_new && *any_new != tag) {  // no op of this chunk marked a page
-    if (b == 0 && threadIdx.x == 0) *num_seg = 0;
+    if (b == 0) {
+      if (threadIdx.x == 0) *num_seg = 0;
+      if (has_q) seg_complete_unchanged(q);
+    }
     return;
   }
   const uint64_t nv = dev_n(n_dev, n);
@@ -153,14 +171,18 @@ __global__ __launch_bounds__(kT) void k_seg_fill_slot(const uint64_t* page, uint
                                                       uint32_t* seg_start, uint32_t* seg_end,
                                                       uint64_t* seg_page, uint32_t* num_seg,
                                                       const uint32_t* oslot, uint32_t tag,
-                                                      const uint32_t* any_new, uint32_t* err) {
+                                                      const uint32_t* any_new, uint32_t* err,
+                                                      UpperArgs q, int has_q) {
   __shared__ uint32_t s_nw[kSegTile + 1];  // new ops before tile index j
   __shared__ uint32_t s_hd[kSegTile + 1];  // tile-relative run heads, in order
   __shared__ uint32_t s_pre[kT / kWave];
   __shared__ uint32_t s_ext_end, s_ext_new;
   const uint32_t b = blockIdx.x;
   if (any_new && *any_new != tag) {  // no op of this chunk is new
-    if (b == 0 && threadIdx.x == 0) *num_seg = 0;
+    if (b == 0) {
+      if (threadIdx.x == 0) *num_seg = 0;
+      if (has_q) seg_complete_unchanged(q);
+    }
     return;
   }
   const uint64_t nv = dev_n(n_dev, n);
@@ -296,15 +318,18 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot) {
+                    const uint32_t* oslot, const UpperArgs* quick) {
   if (!n) return;
+  const UpperArgs q = quick ? *quick : UpperArgs{};
+  const int has_q = quick && any_new ? 1 : 0;
   if (oslot)
     hipLaunchKernelGGL(k_seg_fill_slot, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n,
                        n_dev, lbw, seg_start, seg_end, seg_page, num_seg, oslot, tag, any_new,
-                       err);
+                       err, q, has_q);
   else
     hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev,
-                       lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err);
+                       lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q,
+                       has_q);
 }
 
 // Exclusive scan of u64 counts in one launch: every 1024-element tile
