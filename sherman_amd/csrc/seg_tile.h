@@ -1,0 +1,119 @@
+// seg_tile.h — one 1024-op tile of the insert segmentation (the staged
+// segments: runs of ops on one page that gets a new key), shared by
+// k_seg_fill (util.hip, one tile per block) and the fused upsert kernel
+// (upsert.hip, tiles claimed in order by its blocks).
+#pragma once
+#include "device_common.h"
+#include "kernels.h"
+
+namespace shm {
+namespace dev {
+namespace segt {
+
+constexpr int kT = 256;                       // threads per block
+constexpr int kPer = (int)kSegTile / kT;      // consecutive ops per thread
+static_assert(kPer * kT == (int)kSegTile, "tile shape");
+
+// exclusive scan of v over the block's 256 threads; *total = the block sum
+template <class T>
+__device__ __forceinline__ T block_scan(T v, T* total) {
+  __shared__ T ws[kT / kWave];
+  T incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const T y = __shfl_up(incl, off);
+    if (lane_id() >= off) incl += y;
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == kWave - 1) ws[w] = incl;
+  __syncthreads();
+  T base = 0, sum = 0;
+#pragma unroll
+  for (int i = 0; i < kT / kWave; ++i) {
+    base += i < w ? ws[i] : T(0);
+    sum += ws[i];
+  }
+  __syncthreads();
+  *total = sum;
+  return base + incl - v;
+}
+
+__device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, uint64_t nv) {
+  return i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
+}
+
+// Only segments whose page gets a new key (pnew[page] == new_mark(tag), set by
+// k_locate) need the upsert and split kernels: the others were applied in
+// place by k_locate.
+__device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint32_t tag) {
+  return pnew[ga_offset(pg) >> 10] == new_mark(tag);
+}
+
+// Tile b (whole block): count its staged heads, publish the count in its
+// tagged word (chunk tag << 32 | count), sum the words of the tiles before it
+// (a tile waits only on tiles of smaller index, taken before it by running
+// blocks, so nothing waits on a tile that is not running), and fill its
+// segments: seg_start / seg_page at each staged head, seg_end at its run's
+// last op + 1 (the run may end in the next tile: read, not waited for), and
+// the total at the thread holding the last op.
+__device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint64_t b,
+                                         uint64_t* lbw, uint32_t* seg_start, uint32_t* seg_end,
+                                         uint64_t* seg_page, uint32_t* num_seg,
+                                         const uint8_t* pnew, uint32_t tag, uint32_t* err) {
+  __shared__ uint32_t s_pre[kT / kWave];
+  const uint64_t i0 = b * kSegTile + (uint64_t)threadIdx.x * kPer;
+  uint32_t h[kPer], c = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    h[j] = seg_head(page, i0 + j, nv);
+    if (h[j]) h[j] = page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
+    c += h[j];
+  }
+  uint32_t total;
+  const uint32_t local = block_scan<uint32_t>(c, &total);
+  const uint64_t tg = (uint64_t)tag << 32;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the counts of the tiles before this one
+  uint32_t v = 0;
+  for (uint64_t x = threadIdx.x; x < b; x += kT) {
+    uint64_t w = 0;
+    for (uint32_t spin = 0;; ++spin) {
+      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & ~0xFFFFFFFFull) == tg) break;
+      if (spin > (1u << 24)) {
+        atomicOr(err, kErrSegSpin);
+        w = tg;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    v += (uint32_t)w;
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = v;
+  __syncthreads();
+  uint32_t pos = local;
+#pragma unroll
+  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t i = i0 + j;
+    if (i >= nv) break;
+    const uint64_t pg = page[i];
+    if (h[j]) {
+      seg_start[pos] = (uint32_t)i;
+      seg_page[pos] = pg;
+    }
+    pos += h[j];
+    const bool tail = i + 1 == nv || page[i + 1] != pg;
+    if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
+    if (i + 1 == nv) *num_seg = pos;
+  }
+  __syncthreads();  // s_pre and the scan's words are reused by the next tile
+}
+
+}  // namespace segt
+}  // namespace dev
+}  // namespace shm

@@ -33,6 +33,8 @@ __device__ __forceinline__ void upper_zero_next(UpperCtl* ctl, uint32_t par, uin
     ctl->root_new[par ^ 1][0] = 0;
     ctl->done[par ^ 1][0] = 0;
     ctl->ualloc[par ^ 1][0] = 0;
+    ctl->seg_next[par ^ 1][0] = 0;
+    ctl->seg_done[par ^ 1][0] = 0;
   }
 }
 
@@ -48,6 +50,20 @@ __device__ __forceinline__ void upper_finish_unchanged(const UpperArgs& a, uint3
     if (a.pub_always)
       __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(a.pub + kPubApplied, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+
+// A chunk without a new key (every op applied in place by k_locate, C3's
+// chunks): block 0 also completes it when it has no delete either -- k_upper's
+// quick path (upper_quick.h) -- and tags it in UpperCtl.skip, so the upsert
+// kernel (no segment) and k_upper return after one load
+__device__ __forceinline__ void seg_complete_unchanged(const UpperArgs& q) {
+  if (*q.n_del != 0) return;  // the deletes are k_upper's
+  upper_zero_next(q.ctl, q.par, threadIdx.x, blockDim.x);
+  if (threadIdx.x == 0) {
+    upper_finish_unchanged(q, __hip_atomic_load(q.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    q.ctl->skip[q.par][0] = q.batch;
   }
 }
 

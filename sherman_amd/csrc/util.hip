@@ -3,6 +3,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "upper_quick.h"
+#include "seg_tile.h"
 
 namespace shm {
 namespace dev {
@@ -52,18 +53,8 @@ __device__ __forceinline__ T block_scan(T v, T* total) {
   return base + incl - v;
 }
 
-__device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, uint64_t nv) {
-  return i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
-}
 }  // namespace
 
-// Only segments whose page gets a new key (pnew[page] == new_mark(tag), set by
-// k_locate) need the upsert and split kernels: the others were applied in
-// place by k_locate.  The list holds just those ("staged" segments), so the
-// later kernels' grids and block ranges cover only them.
-__device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint32_t tag) {
-  return pnew[ga_offset(pg) >> 10] == new_mark(tag);
-}
 
 // One launch: every 1024-op tile counts its staged heads, publishes the
 // count in its tagged word (chunk tag << 32 | count), sums the words of the
@@ -72,18 +63,6 @@ __device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint3
 // segments: seg_start / seg_page at each staged head, seg_end at its run's
 // last op (the count of staged heads up to and including that op is the
 // segment's position + 1).
-// A chunk without a new key (every op applied in place by k_locate, C3's
-// chunks): block 0 also completes it when it has no delete either -- k_upper's
-// quick path (upper_quick.h) -- and tags it in UpperCtl.skip, so the upsert
-// kernel (no segment) and k_upper return after one load
-__device__ __forceinline__ void seg_complete_unchanged(const UpperArgs& q) {
-  if (*q.n_del != 0) return;  // the deletes are k_upper's
-  upper_zero_next(q.ctl, q.par, threadIdx.x, blockDim.x);
-  if (threadIdx.x == 0) {
-    upper_finish_unchanged(q, __hip_atomic_load(q.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    q.ctl->skip[q.par][0] = q.batch;
-  }
-}
 
 __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t n,
                                                  const uint64_t* n_dev, uint64_t* lbw,
@@ -92,7 +71,6 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err,
                                                  UpperArgs q, int has_q) {
-  __shared__ uint32_t s_pre[kT / kWave];
   const uint32_t b = blockIdx.x;
   if (any_new && *any_new != tag) {  // no op of this chunk marked a page
     if (b == 0) {
@@ -106,56 +84,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
     if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
     return;
   }
-  const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
-  uint32_t h[kScanPer], c = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    h[j] = seg_head(page, i0 + j, nv);
-    if (h[j]) h[j] = page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
-    c += h[j];
-  }
-  uint32_t total;
-  const uint32_t local = block_scan<uint32_t>(c, &total);
-  const uint64_t tg = (uint64_t)tag << 32;
-  if (threadIdx.x == 0)
-    __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the counts of the tiles before this one
-  uint32_t v = 0;
-  for (uint32_t x = threadIdx.x; x < b; x += kT) {
-    uint64_t w = 0;
-    for (uint32_t spin = 0;; ++spin) {
-      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((w & ~0xFFFFFFFFull) == tg) break;
-      if (spin > (1u << 24)) {
-        atomicOr(err, kErrSegSpin);
-        w = tg;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    v += (uint32_t)w;
-  }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = v;
-  __syncthreads();
-  uint32_t pos = local;
-#pragma unroll
-  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const uint64_t i = i0 + j;
-    if (i >= nv) break;
-    const uint64_t pg = page[i];
-    if (h[j]) {
-      seg_start[pos] = (uint32_t)i;
-      seg_page[pos] = pg;
-    }
-    pos += h[j];
-    const bool tail = i + 1 == nv || page[i + 1] != pg;
-    if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
-    if (i + 1 == nv) *num_seg = pos;
-  }
+  segt::seg_tile(page, nv, b, lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, err);
 }
 
 // The same list from the ops' own verdicts (round 4): a run is staged when
@@ -197,7 +126,7 @@ __global__ __launch_bounds__(kT) void k_seg_fill_slot(const uint64_t* page, uint
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const uint64_t i = t0 + j0 + j;
-    h[j] = seg_head(page, i, nv);
+    h[j] = segt::seg_head(page, i, nv);
     nw[j] = i < nv && !(oslot[i] & 0x80000000u) ? 1u : 0u;
     ch += h[j];
     cn += nw[j];
