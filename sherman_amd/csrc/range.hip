@@ -311,6 +311,10 @@ __global__ void k_readback(uint32_t* dst, uint32_t* src, uint32_t nw, uint32_t* 
     dst[l] = clear ? atomicExch(src + l, 0u) : src[l];
   const uint32_t l = threadIdx.x;
   __threadfence_system();
+  // the fence's write-back performed before the flag (the returned exchanges
+  // above let the compiler drop the fence's own wait: MI355X_MICROARCH.md
+  // "Compiler hazard")
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (l == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -416,6 +416,7 @@ __device__ __forceinline__ bool handoff(UpperCtl* ctl, uint32_t par, uint32_t ph
     uint32_t* abort = &ctl->abort[par][0];
     uint32_t* d = &ctl->dn[par][ph][0];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back before the count
     if (sum) __hip_atomic_fetch_add(d, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t ok = force ? 0u : 1u;
     for (uint32_t spin = 0; ok; ++spin) {
@@ -633,6 +634,7 @@ __device__ __forceinline__ void delete_key(const UpperArgs& a, uint64_t k, uint3
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back before the release
       __hip_atomic_store(a.locks + lw, a.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -468,6 +468,9 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
       __syncthreads();
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // the write-back performed before the count (the compiler may drop the
+        // fence's own wait: MI355X_MICROARCH.md "Compiler hazard")
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
