@@ -96,6 +96,9 @@ def parse():
                         "stream (shm_insert_order), so it runs beside the previous "
                         "batch's gets / scans and tree changes (shm_insert_apply); 0 = "
                         "shm_mixed_batch (c3) / shm_insert_batch_async (c5)")
+    p.add_argument("--prio", type=int, default=0, choices=(0, 1),
+                   help="c3 / c5 pipelined: 1 = the gets' / scans' and tree changes' "
+                        "stream at high priority, the ordering's at normal")
     p.add_argument("--dir-fp", type=int, default=None, choices=(0, 1),
                    help="leaf-directory entries of one-leaf prefixes carry the leaf's "
                         "fingerprints (SHM_DIR_FP; library default 1; 0 = round-2 form)")
@@ -362,7 +365,11 @@ def main():
         applied = [0]  # batches applied so far (all step loops)
         s_scan = s_ins = None
         if route is None and args.streams == 2:
-            s_scan, s_ins = torch.cuda.Stream(), torch.cuda.Stream()
+            # --prio 1: the stream that carries the step's chain (scans and
+            # tree changes when pipelined) at high priority, so the ordering
+            # beside it takes the CUs it leaves
+            s_scan = torch.cuda.Stream(priority=-1 if args.prio else 0)
+            s_ins = torch.cuda.Stream()
             s_scan.wait_stream(torch.cuda.current_stream())
             s_ins.wait_stream(torch.cuda.current_stream())
 
@@ -459,7 +466,8 @@ def main():
         if c3_pipe:
             # gets and tree changes on one stream, the orderings on their own:
             # batch i + 1 is ordered while batch i's gets and inserts run
-            c3_main, c3_ord = torch.cuda.Stream(), torch.cuda.Stream()
+            c3_main = torch.cuda.Stream(priority=-1 if args.prio else 0)
+            c3_ord = torch.cuda.Stream()
             c3_main.wait_stream(torch.cuda.current_stream())
             c3_ord.wait_stream(torch.cuda.current_stream())
 

@@ -148,10 +148,6 @@ struct UpperCtl {
   // the tag of a chunk the segmentation kernel completed (no new key, no
   // delete: upper_quick.h); its k_upper returns at once
   uint64_t skip[2][16];
-  // the fused upsert kernel's segmentation tiles: the next unclaimed one and
-  // those whose segments are written (per parity, zeroed with the others)
-  uint32_t seg_next[2][32];
-  uint32_t seg_done[2][32];
 };
 // UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
 // the chunk's op buffers (tree.cpp insert_order's flow control)
@@ -201,23 +197,6 @@ struct SegArgs {
   UpperCtl* ctl;
   uint32_t par;
   uint32_t up_nb;
-  // fused (SHM_FUSED_SEG): the kernel lists the segments itself first
-  // (seg_tile.h over the ops' pages, k_locate's marks), instead of
-  // k_seg_fill in a launch of its own; quick_ok: it may complete a chunk
-  // without a new key and a delete (upper_quick.h)
-  uint32_t fused;
-  uint32_t quick_ok;
-  const uint64_t* op_page;     // k_locate's page per op
-  uint64_t n_ops;              // upper bound of *n_dev
-  const uint64_t* n_dev;       // device op count
-  uint64_t* lbw;               // the tiles' tagged count words
-  const uint8_t* pnew;         // per-page new-key marks
-  const uint32_t* any_new;     // == seg_tag when some op is new
-  uint32_t seg_tag;            // the chunk's tag
-  uint32_t* seg_start_w;       // the segment arrays above, written here
-  uint32_t* seg_end_w;
-  uint64_t* seg_page_w;
-  uint32_t* num_seg_w;
 };
 struct UpperArgs;
 // u: the split arguments of the chunk with u.early = 1 (small splits taken

@@ -1,7 +1,7 @@
 // seg_tile.h — one 1024-op tile of the insert segmentation (the staged
-// segments: runs of ops on one page that gets a new key), shared by
-// k_seg_fill (util.hip, one tile per block) and the fused upsert kernel
-// (upsert.hip, tiles claimed in order by its blocks).
+// segments: runs of ops on one page that gets a new key): k_seg_fill's body
+// (util.hip, one tile per block), kept apart for a kernel that lists its own
+// segments (fusing the segmentation into the upsert kernel).
 #pragma once
 #include "device_common.h"
 #include "kernels.h"

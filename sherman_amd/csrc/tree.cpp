@@ -501,9 +501,17 @@ void set_dir(shm_tree* t, const uint64_t** dir, uint64_t* lo, uint32_t* shift, u
 bool debug_sync_enabled() {
   static const int on = [] {
     const char* e = getenv("SHM_DEBUG");
-    return e && e[0] == '1' ? 1 : 0;
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
   }();
   return on != 0;
+}
+// SHM_DEBUG=2: also name every step as it completes (a hang's last line)
+bool debug_trace_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_DEBUG");
+    return e && e[0] == '2';
+  }();
+  return on;
 }
 int dbg(hipStream_t s, const char* what) {
   if (!debug_sync_enabled()) return SHM_OK;
@@ -513,6 +521,7 @@ int dbg(hipStream_t s, const char* what) {
     fprintf(stderr, "sherman_amd[debug]: %s failed: %s\n", what, hipGetErrorString(e));
     return SHM_EIO;
   }
+  if (debug_trace_enabled()) fprintf(stderr, "sherman_amd[debug]: %s done\n", what);
   return SHM_OK;
 }
 #define DBG(s, what)                   \
@@ -728,15 +737,6 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
 // page marks: SHM_SEG_SLOTS=1.  Measured slower (one gpurun call, C5 4517
 // against 4678 Mops/s with the marks, whose random byte reads hit L2), so
 // the marks stay the default
-// the segmentation inside the upsert kernel (SHM_FUSED_SEG=1; upsert.hip
-// upsert_body FUSED): one launch fewer per insert chunk
-bool fused_seg() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_FUSED_SEG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 bool seg_from_slots() {
   static const bool on = [] {
     const char* e = getenv("SHM_SEG_SLOTS");
@@ -853,15 +853,11 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   ue.early = no_early || (t->force_flags & 7u) ? 0u : 1u;
   // a chunk with no new key and no delete is completed by the segmentation
   // kernel's block 0 (u: k_upper's quick path; k_upper then returns at once).
-  // Fused (SHM_FUSED_SEG=1): the upsert kernel lists the segments itself.
   const bool quick_ok = u.quick && !u.force_abort;
-  const bool fused = fused_seg() && !seg_from_slots();
-  if (!fused) {
-    dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
-                        t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
-                        seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr);
-    DBG(s, "segment");
-  }
+  dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
+                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
+                      seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr);
+  DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
   a.arena = t->arena;
@@ -888,21 +884,6 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.ctl = t->ctl;
   a.par = tag & 1u;
   a.up_nb = dev::upper_blocks();
-  if (fused) {
-    a.fused = 1;
-    a.quick_ok = quick_ok ? 1u : 0u;
-    a.op_page = t->pages;
-    a.n_ops = n;
-    a.n_dev = cnt + 0;
-    a.lbw = t->seg_lb;
-    a.pnew = t->pnew;
-    a.any_new = w.any_new;
-    a.seg_tag = tag;
-    a.seg_start_w = t->seg_start;
-    a.seg_end_w = t->seg_end;
-    a.seg_page_w = t->seg_page;
-    a.num_seg_w = d_ns;
-  }
   dev::launch_leaf_upsert(a, ue, s);
   DBG(s, "leaf_upsert");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[2], s));

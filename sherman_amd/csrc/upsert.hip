@@ -33,8 +33,6 @@
 #include "lds_dma.h"
 #include "leaf_chunk.h"
 #include "split_wave.h"
-#include "seg_tile.h"
-#include "upper_quick.h"
 
 namespace shm {
 namespace dev {
@@ -425,14 +423,7 @@ __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperA
 // for its block's last queued split, never for other blocks.
 // IL: a wave also takes a queued split between its groups (else only once
 // the block's groups are all taken)
-// FUSED (SHM_FUSED_SEG): the kernel first lists the chunk's segments itself
-// -- k_seg_fill's tiles (seg_tile.h), claimed in order by the running blocks,
-// each published after its records are written back -- and every block
-// waits until all tiles are listed (all are taken by then, by running
-// blocks, so the wait never depends on a block that is not resident); a
-// chunk without a new key is completed by block 0 (upper_quick.h).  One
-// launch fewer per insert chunk.
-template <int G, bool IL, bool FUSED>
+template <int G, bool IL>
 __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * 2 * G * kPageDwords];
   __shared__ __attribute__((aligned(16))) WaveLds s_wl[kWavesPerBlock];
@@ -440,58 +431,7 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint32_t num_seg;
-  if constexpr (FUSED) {
-    static_assert(kBlock == segt::kT, "the segmentation tile's block shape");
-    if (*a.any_new != a.seg_tag) {  // no op of the chunk is new: nothing to stage
-      if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) *a.num_seg_w = 0;
-        if (a.quick_ok) seg_complete_unchanged(u);
-      }
-      return;
-    }
-    const uint64_t nv = a.n_dev ? *a.n_dev : a.n_ops;
-    const uint64_t ntiles = (nv + kSegTile - 1) / kSegTile;
-    __shared__ uint32_t s_tile, s_ns;
-    uint32_t* next = &u.ctl->seg_next[u.par][0];
-    uint32_t* done = &u.ctl->seg_done[u.par][0];
-    for (;;) {
-      if (threadIdx.x == 0) s_tile = atomicAdd(next, 1u);
-      __syncthreads();
-      const uint64_t tt = s_tile;
-      __syncthreads();
-      if (tt >= ntiles) break;
-      segt::seg_tile(a.op_page, nv, tt, a.lbw, a.seg_start_w, a.seg_end_w, a.seg_page_w,
-                     a.num_seg_w, a.pnew, a.seg_tag, a.err);
-      // the tile's records performed and written back, then it counts as done
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        // the write-back performed before the count (the compiler may drop the
-        // fence's own wait: MI355X_MICROARCH.md "Compiler hazard")
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (threadIdx.x == 0) {
-      for (uint32_t spin = 0;
-           __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles; ++spin) {
-        if (spin > (1u << 24)) {
-          atomicOr(a.err, kErrSegSpin);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      s_ns = ntiles ? __hip_atomic_load(a.num_seg_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      if (!ntiles && blockIdx.x == 0) *a.num_seg_w = 0;
-    }
-    __syncthreads();
-    num_seg = s_ns;
-  } else {
-    num_seg = *a.num_seg_dev;
-  }
+  const uint32_t num_seg = *a.num_seg_dev;
   if (num_seg == 0) return;  // every op applied in place (C3's chunks): the block's only load
   const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
   // early splits need a root above the leaves (a leaf root grows the tree:
@@ -549,22 +489,18 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
 
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a, UpperArgs u) {
-  upsert_body<G, false, false>(a, u);
-}
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_leaf_upsert_fused(SegArgs a, UpperArgs u) {
-  upsert_body<G, false, true>(a, u);
+  upsert_body<G, false>(a, u);
 }
 // interleaved variants (SHM_UPSERT_IL=1: as many VGPRs as it takes, 2 waves
 // per SIMD; 2: held to 3 waves per SIMD, spilling)
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_leaf_upsert_il(SegArgs a, UpperArgs u) {
-  upsert_body<G, true, false>(a, u);
+  upsert_body<G, true>(a, u);
 }
 template <int G>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_leaf_upsert_il3(
     SegArgs a, UpperArgs u) {
-  upsert_body<G, true, false>(a, u);
+  upsert_body<G, true>(a, u);
 }
 
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
@@ -575,12 +511,9 @@ void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
     return e ? atoi(e) : 0;
   }();
   using K = void (*)(SegArgs, UpperArgs);
-  const int m = a.fused ? 3 : mode >= 0 && mode <= 2 ? mode : 0;
-  const K k = m == 3   ? k_leaf_upsert_fused<G>
-              : m == 1 ? k_leaf_upsert_il<G>
-              : m == 2 ? k_leaf_upsert_il3<G>
-                       : k_leaf_upsert_pipe<G>;
-  static unsigned blocks[4] = {0, 0, 0, 0};
+  const int m = mode >= 0 && mode <= 2 ? mode : 0;
+  const K k = m == 1 ? k_leaf_upsert_il<G> : m == 2 ? k_leaf_upsert_il3<G> : k_leaf_upsert_pipe<G>;
+  static unsigned blocks[3] = {0, 0, 0};
   unsigned& nb = blocks[m];
   if (!nb) {
     int per_cu = 0, cus = 0, dev = 0;
