@@ -775,9 +775,17 @@ def main():
             out["config"]["scan_out"] = (("slots of %d values" % args.slot_cap)
                                          if world == 1 and args.async_scans and
                                          args.scan_out == "slots" else "compact")
+            pipelined = out["config"]["insert_pipeline"]
             out["roofline"].update({
                 "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                "kernel": "insert_batch chunk (ordering + locate + k_leaf_upsert + splits)",
+                # pipelined, the profile times the chunk's tree phase alone: its
+                # ordering ran one step earlier beside the scans and the previous
+                # chunk (shm_insert_order); step_alg_GBps below covers the whole step
+                "kernel": ("insert_apply chunk (locate + k_leaf_upsert + splits; the ordering "
+                           "runs one chunk ahead on its own stream)" if pipelined else
+                           "insert_batch chunk (ordering + locate + k_leaf_upsert + splits)"),
+                "step_alg_GBps": round(ins_per_launch * ALG_BYTES_PER_INSERT /
+                                       (elapsed / args.steps) / 1e9, 1),
                 "alg_bytes_per_insert": ALG_BYTES_PER_INSERT,
                 "insert_ms_per_launch": round(ins_ms, 4),
                 "upsert_ms_per_launch": round(ups_ms, 4),
