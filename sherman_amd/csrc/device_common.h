@@ -54,6 +54,28 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// A block's index in a decoupled look-back launch (k_bin_unique, k_seg_fill,
+// k_scan_u64), taken by one atomic add as the block starts: a block waits
+// only on smaller indices, which blocks already running (or done) hold, so
+// the look-back cannot wait on a block the dispatcher has not placed.  With
+// blockIdx it could: another kernel or another process on the card may hold
+// the CUs a smaller blockIdx needs while larger ones spin (seen with two
+// ranks sharing one GPU: k_bin_unique's spin bound, kErrBinSpin).  The
+// launch's last taker resets the counter for the next launch of the kernel
+// (launches sharing a counter are stream-ordered).  Every block must call
+// this first, unconditionally; ctr == nullptr keeps blockIdx.
+__device__ __forceinline__ uint32_t lookback_index(uint32_t* ctr) {
+  if (!ctr) return blockIdx.x;
+  __shared__ uint32_t s_idx;
+  if (threadIdx.x == 0) {
+    const uint32_t i = atomicAdd(ctr, 1u);
+    if (i == gridDim.x - 1) atomicExch(ctr, 0u);
+    s_idx = i;
+  }
+  __syncthreads();
+  return s_idx;
+}
+
 __device__ __forceinline__ u32x4 load_page_slice(const uint8_t* arena,
                                                   uint64_t off) {
   return *reinterpret_cast<const u32x4*>(arena + off + 16 * lane_id());

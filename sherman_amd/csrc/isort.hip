@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
                                                    uint32_t* __restrict__ S,
                                                    const uint32_t* gate, uint32_t tag,
                                                    uint64_t* __restrict__ stamps,
-                                                   TileRuns tr) {
+                                                   TileRuns tr, uint32_t* ids) {
   constexpr int SPT = kUniqSlots / kIT;  // hash slots per thread
   __shared__ unsigned long long hkey[kUniqSlots];  // hash, then the sorted keys
   __shared__ uint32_t hidx[kUniqSlots];            // 1 + op index, then op index
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kIT) void k_bin_unique(uint64_t* __restrict__ keys1
   __shared__ uint32_t s_tpre[kMaxTiles + 1];
   __shared__ uint32_t s_tbase[kMaxTiles];
   const int t = threadIdx.x;
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = lookback_index(ids);  // the bin (bin_prefix waits on smaller ones)
   const uint32_t tiles = tr.tiles;
   // the coarse pass is complete: clear its group sums for the next batch
   // (tile mode: the last bin, once every bin has read them, bin_prefix)
@@ -714,10 +714,12 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, hipStream_t s) {
+                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, uint32_t* ids,
+                       hipStream_t s) {
   const KeyRange kr{key_lo, key_bits};
   hipLaunchKernelGGL(k_bin_unique, dim3(kCoarse), dim3(kIT), 0, s, keys1, pay1, bins, kr, vals,
-                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag, stamps, tr);
+                     lrank, lbw, kscr, iscr, uk, uv, dk, counts, err, S, gate, tag, stamps, tr,
+                     ids);
 }
 
 }  // namespace dev

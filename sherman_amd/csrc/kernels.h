@@ -115,6 +115,7 @@ constexpr int kMaxUpper = 512;
 // 0 = sibling pages of large leaf splits, 1 = leaf splits (dn[.][0] counts
 // both), 1 + L = internal level L (L = 1 .. kMaxLevelOfTree)
 constexpr int kUpPhases = 16;
+constexpr int kLbBin = 0, kLbSeg = 1, kLbScan = 2;
 struct UpperCtl {
   // Phase hand-offs (insert.hip handoff), each word on a 128 B line of its
   // own: tk = the next unclaimed task of a phase (tickets, taken in dispatch
@@ -126,6 +127,10 @@ struct UpperCtl {
   uint32_t dn[2][kUpPhases][32];
   uint32_t abort[2][32];
   uint32_t gate;    // tag of the last chunk rejected by its ordering (kKeyMax)
+  // block-index counters of the look-back kernels (lookback_index,
+  // device_common.h), one 128 B line each: kLbBin k_bin_unique, kLbSeg
+  // k_seg_fill(_slot), kLbScan k_scan_u64
+  uint32_t lb_ids[3][32];
   // leaf split counts of the upsert kernel per k_upper block range, double
   // buffered by chunk parity (k_upper zeroes the other parity)
   uint32_t leaf_np[2][kMaxUpper];  // new pages
@@ -360,7 +365,8 @@ void launch_bin_unique(uint64_t* keys1, uint32_t* pay1, const uint32_t* bins, ui
                        uint32_t key_bits, const uint64_t* vals, uint32_t* lrank, uint64_t* lbw,
                        uint64_t* kscr, uint32_t* iscr, uint64_t* uk, uint64_t* uv, uint64_t* dk,
                        uint64_t* counts, uint32_t* err, uint32_t* S, const uint32_t* gate,
-                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, hipStream_t s);
+                       uint32_t tag, uint64_t* stamps, const TileRuns& tr, uint32_t* ids,
+                       hipStream_t s);
 // out[i] = vals1[pos1[i]], found[i] = out[i] != 0
 void launch_unpartition(const uint64_t* vals1, const uint32_t* pos1, uint64_t n,
                         uint64_t* out, uint8_t* found, hipStream_t s);
@@ -383,13 +389,14 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot = nullptr, const UpperArgs* quick = nullptr);
+                    const uint32_t* oslot = nullptr, const UpperArgs* quick = nullptr,
+                    uint32_t* ids = nullptr);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
 // wraps); tot = {total, *err} for the range scan's one read-back
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* lbw,
                            uint32_t tag, const uint32_t* err, uint64_t* tot, uint32_t* err_out,
-                           hipStream_t s);
+                           uint32_t* ids, hipStream_t s);
 
 // ---- generators and multi-GPU routing (util.hip) -------------------------------
 void launch_gen_keys(uint64_t first, uint64_t n, uint64_t keyspace,

@@ -726,7 +726,8 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                          tile_mode ? t->kc : t->kb, tile_mode ? t->id : t->ic,
                          op_keys(t, tag), op_vals(t, tag), op_dels(t, tag), op_counts(t, tag),
                          t->d_err, t->part_S, &t->ctl->gate,
-                         tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, tr, s);
+                         tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, tr,
+                         t->ctl->lb_ids[dev::kLbBin], s);
   DBG(s, "ordering");
   note(t->ord, s);
   return SHM_OK;
@@ -856,7 +857,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   const bool quick_ok = u.quick && !u.force_abort;
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
                       t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
-                      seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr);
+                      seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr,
+                      t->ctl->lb_ids[dev::kLbSeg]);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -1610,7 +1612,8 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
     int rc = range_launch(t, s, rargs(off, m, nullptr, nullptr));
     if (rc) return rc;
     dev::launch_scan_u64_total(counts_out + off, offsets_out + off, m, t->bsum64,
-                               scan_tag(t, s), t->d_err, t->d_counts + 12, t->d_err, s);
+                               scan_tag(t, s), t->d_err, t->d_counts + 12, t->d_err,
+                               t->ctl->lb_ids[dev::kLbScan], s);
     rc = readback(t, s, t->d_counts + 12, 2 * sizeof(uint64_t));
     if (rc) return rc;
     if (t->h_pin[1]) return check_err(t, s);
@@ -1664,7 +1667,7 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   // count pass -> offsets and (total, error word) into total_dev, then the
   // fill pass bounded by vals_cap; no host synchronisation
   dev::launch_scan_u64_total(counts_out, offsets_out, n, t->bsum64, scan_tag(t, s), t->d_err,
-                             total_dev, t->d_err, s);
+                             total_dev, t->d_err, t->ctl->lb_ids[dev::kLbScan], s);
   if (!vals_cap) return SHM_OK;
   a.offsets = offsets_out;
   a.vals = vals_out;
@@ -1715,7 +1718,7 @@ int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n, ui
     return SHM_OK;
   }
   dev::launch_scan_u64_total(in, out, n, t->bsum64, scan_tag(t, s), t->d_err, tot_dev, t->d_err,
-                             s);
+                             t->ctl->lb_ids[dev::kLbScan], s);
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }

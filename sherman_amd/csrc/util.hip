@@ -70,8 +70,8 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  uint64_t* seg_page, uint32_t* num_seg,
                                                  const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err,
-                                                 UpperArgs q, int has_q) {
-  const uint32_t b = blockIdx.x;
+                                                 UpperArgs q, int has_q, uint32_t* ids) {
+  const uint32_t b = lookback_index(ids);  // the tile
   if (any_new && *any_new != tag) {  // no op of this chunk marked a page
     if (b == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
@@ -101,12 +101,12 @@ __global__ __launch_bounds__(kT) void k_seg_fill_slot(const uint64_t* page, uint
                                                       uint64_t* seg_page, uint32_t* num_seg,
                                                       const uint32_t* oslot, uint32_t tag,
                                                       const uint32_t* any_new, uint32_t* err,
-                                                      UpperArgs q, int has_q) {
+                                                      UpperArgs q, int has_q, uint32_t* ids) {
   __shared__ uint32_t s_nw[kSegTile + 1];  // new ops before tile index j
   __shared__ uint32_t s_hd[kSegTile + 1];  // tile-relative run heads, in order
   __shared__ uint32_t s_pre[kT / kWave];
   __shared__ uint32_t s_ext_end, s_ext_new;
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = lookback_index(ids);  // the tile
   if (any_new && *any_new != tag) {  // no op of this chunk is new
     if (b == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
@@ -247,18 +247,18 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot, const UpperArgs* quick) {
+                    const uint32_t* oslot, const UpperArgs* quick, uint32_t* ids) {
   if (!n) return;
   const UpperArgs q = quick ? *quick : UpperArgs{};
   const int has_q = quick && any_new ? 1 : 0;
   if (oslot)
     hipLaunchKernelGGL(k_seg_fill_slot, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n,
                        n_dev, lbw, seg_start, seg_end, seg_page, num_seg, oslot, tag, any_new,
-                       err, q, has_q);
+                       err, q, has_q, ids);
   else
     hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev,
                        lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q,
-                       has_q);
+                       has_q, ids);
 }
 
 // Exclusive scan of u64 counts in one launch: every 1024-element tile
@@ -269,9 +269,9 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
 __global__ __launch_bounds__(kT) void k_scan_u64(const uint64_t* in, uint64_t n, uint64_t* lbw,
                                                  uint32_t tag, uint64_t* out,
                                                  const uint32_t* err, uint64_t* tot,
-                                                 uint32_t* err_out) {
+                                                 uint32_t* err_out, uint32_t* ids) {
   __shared__ uint64_t s_pre[kT / kWave];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = lookback_index(ids);  // the tile
   const uint64_t i0 = (uint64_t)b * kSegTile + (uint64_t)threadIdx.x * kScanPer;
   uint64_t v[kScanPer], c = 0;
 #pragma unroll
@@ -320,10 +320,10 @@ __global__ __launch_bounds__(kT) void k_scan_u64(const uint64_t* in, uint64_t n,
 
 void launch_scan_u64_total(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* lbw,
                            uint32_t tag, const uint32_t* err, uint64_t* tot, uint32_t* err_out,
-                           hipStream_t s) {
+                           uint32_t* ids, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_scan_u64, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, in, n, lbw, tag, out,
-                     err, tot, err_out);
+                     err, tot, err_out, ids);
 }
 
 // to_key without / with the modulus (test/benchmark.cpp:43-46)
