@@ -1312,6 +1312,48 @@ def test_split_insert_beside_cu_hog(lib_ok, lists):
     t.close()
 
 
+def test_lookback_kernels_of_two_trees_side_by_side(lib_ok):
+    """The decoupled look-backs (k_bin_unique's bin prefix, k_seg_fill,
+    k_scan_u64) of two trees queued side by side on two streams: each
+    ordering's 256 bin blocks want a CU each, so the two launches share the
+    card.  Blocks take their look-back index by ticket (lookback_index,
+    device_common.h) and wait only on running blocks: every chunk ends with
+    no error bit (kErrBinSpin / kErrSegSpin / kErrScanSpin among them) and
+    both trees hold the oracle's contents and scan counts."""
+    rng = np.random.default_rng(777)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    trees = [shm.Tree(arena_bytes=256 << 20, max_batch=1 << 16) for _ in range(2)]
+    orcs = [OracleTree(256 << 20) for _ in range(2)]
+    keep = []  # the queued batches' tensors stay alive until the end
+    for r in range(6):
+        batches = []
+        keep.append(batches)
+        for i in range(2):
+            k = rng.integers(1, 1 << 62, size=1 << 16, dtype=np.int64).astype(U64)
+            v = k ^ U64(0x55)
+            batches.append((dev(k), dev(v)))
+            orcs[i].apply_batch(k, v)
+        torch.cuda.synchronize()
+        for i in range(2):
+            trees[i].insert_batch_async(*batches[i], stream=streams[i])
+    lo = np.sort(rng.integers(1, 1 << 62, size=1 << 14, dtype=np.int64).astype(U64))
+    hi = lo + U64(1 << 52)
+    pend = [trees[i].range_query_batch_async(dev(lo), dev(hi), stream=streams[i])
+            for i in range(2)]
+    for i in range(2):
+        counts, _ = pend[i].result()
+        trees[i].synchronize()
+        ok, _ = orcs[i].dump()
+        ok = np.sort(ok)
+        want = np.searchsorted(ok, hi, side="right") - np.searchsorted(ok, lo, side="left")
+        assert np.array_equal(host(counts).astype(np.int64), want.astype(np.int64))
+        assert trees[i].last_error()["bits"] == 0
+        compare_contents(trees[i], orcs[i])
+    for i in range(2):
+        orcs[i].close()
+        trees[i].close()
+
+
 def early_pages(t):
     x = ctypes.c_uint64()
     assert shm._hooks().shm__early_pages(t.h, ctypes.byref(x)) == 0
