@@ -358,8 +358,8 @@ __device__ void big_bin_unique(uint64_t* __restrict__ keys1, uint32_t* __restric
 // Bin b's place among the bins: publish its (upserts, deletes) in its
 // tagged word (chunk tag << 48 | upserts << 24 | deletes), then wave 0 waits
 // for the words of bins < b and sums them (the last bin sums all of them into
-// counts[0..1]).  All kCoarse bins are resident together (one block per CU),
-// and a bin waits only on bins of smaller index, dispatched before it.
+// counts[0..1]).  b is the block's ticket (lookback_index): a bin waits only
+// on bins taken before it by running blocks, whatever else holds the CUs.
 __device__ void bin_prefix(uint64_t* lbw, uint32_t b, uint32_t tag, uint32_t ups, uint32_t dels,
                            uint32_t* red, uint32_t& bu, uint32_t& bd, uint64_t* counts,
                            uint32_t* err) {

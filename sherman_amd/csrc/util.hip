@@ -58,8 +58,8 @@ __device__ __forceinline__ T block_scan(T v, T* total) {
 
 // One launch: every 1024-op tile counts its staged heads, publishes the
 // count in its tagged word (chunk tag << 32 | count), sums the words of the
-// tiles before it (a tile waits only on tiles of smaller index, dispatched
-// before it, so nothing waits on a tile that is not running), and fills its
+// tiles before it (tile indices are tickets, lookback_index: a tile waits only
+// on tiles taken before it by running blocks), and fills its
 // segments: seg_start / seg_page at each staged head, seg_end at its run's
 // last op (the count of staged heads up to and including that op is the
 // segment's position + 1).
