@@ -1713,6 +1713,10 @@ int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n, ui
   if (n > t->nmax) return SHM_E2BIG;
   std::lock_guard<std::mutex> g(t->mu);
   hipStream_t s = pick(stream);
+  // the tile words and the look-back counter are the tree's: no other scan
+  // of the tree (shm_range_query_*) may run beside this one
+  Order ord(t, s, true);
+  if (ord.rc) return ord.rc;
   if (n == 0) {
     HIP_OK(hipMemsetAsync(tot_dev, 0, 2 * sizeof(uint64_t), s));
     return SHM_OK;
