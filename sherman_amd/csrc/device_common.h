@@ -62,8 +62,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // the CUs a smaller blockIdx needs while larger ones spin (seen with two
 // ranks sharing one GPU: k_bin_unique's spin bound, kErrBinSpin).  The
 // launch's last taker resets the counter for the next launch of the kernel
-// (launches sharing a counter are stream-ordered).  Every block must call
-// this first, unconditionally; ctr == nullptr keeps blockIdx.
+// (launches sharing a counter are stream-ordered).  Either every block of a
+// launch calls this or none does (an exit taken before it must be uniform
+// over the grid); ctr == nullptr keeps blockIdx.
 __device__ __forceinline__ uint32_t lookback_index(uint32_t* ctr) {
   if (!ctr) return blockIdx.x;
   __shared__ uint32_t s_idx;

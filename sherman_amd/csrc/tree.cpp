@@ -428,6 +428,24 @@ uint32_t dir_extra_bits() {
   return x;
 }
 
+// The look-back kernels' block-index counters (lookback_index).
+// SHM_LB_TICKETS, a mask over kLbBin / kLbSeg / kLbScan, default 5 (the
+// ordering's bin prefix and the scans): a kernel whose bit is clear gets none
+// and its blocks use blockIdx.  k_bin_unique needs its ticket (256 blocks, one
+// per CU: two ranks on one GPU spun on each other, kErrBinSpin) and it costs
+// nothing measurable; k_seg_fill's 1024 blocks per C5 chunk serialise on the
+// counter (C5 5.19-5.23 K against 5.33-5.38 K Mops/s without, C3 -2 %), and
+// its 9 KB blocks (8 per CU, 2048 slots) only wait on an unplaced block when
+// other grids fill every slot, which the ticketed kernels cannot do for good
+// (DESIGN §3 "Batched insert" 4).
+uint32_t* lb_ctr(shm_tree* t, int which) {
+  static const uint32_t mask = [] {
+    const char* e = getenv("SHM_LB_TICKETS");
+    return e ? (uint32_t)atoi(e) : 5u;
+  }();
+  return (mask >> which) & 1u ? t->ctl->lb_ids[which] : nullptr;
+}
+
 int refresh_dir(shm_tree* t, hipStream_t s) {
   if (!dir_stale(t)) return SHM_OK;
   static const bool trace = [] {
@@ -727,7 +745,7 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
                          op_keys(t, tag), op_vals(t, tag), op_dels(t, tag), op_counts(t, tag),
                          t->d_err, t->part_S, &t->ctl->gate,
                          tag, t->stamps ? t->stamps + dev::kUpperStamps : nullptr, tr,
-                         t->ctl->lb_ids[dev::kLbBin], s);
+                         lb_ctr(t, dev::kLbBin), s);
   DBG(s, "ordering");
   note(t->ord, s);
   return SHM_OK;
@@ -858,7 +876,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
                       t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
                       seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr,
-                      t->ctl->lb_ids[dev::kLbSeg]);
+                      lb_ctr(t, dev::kLbSeg));
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -1613,7 +1631,7 @@ int shm_range_query_batch(shm_tree* t, const uint64_t* from, const uint64_t* to,
     if (rc) return rc;
     dev::launch_scan_u64_total(counts_out + off, offsets_out + off, m, t->bsum64,
                                scan_tag(t, s), t->d_err, t->d_counts + 12, t->d_err,
-                               t->ctl->lb_ids[dev::kLbScan], s);
+                               lb_ctr(t, dev::kLbScan), s);
     rc = readback(t, s, t->d_counts + 12, 2 * sizeof(uint64_t));
     if (rc) return rc;
     if (t->h_pin[1]) return check_err(t, s);
@@ -1667,7 +1685,7 @@ int shm_range_query_batch_async(shm_tree* t, const uint64_t* from, const uint64_
   // count pass -> offsets and (total, error word) into total_dev, then the
   // fill pass bounded by vals_cap; no host synchronisation
   dev::launch_scan_u64_total(counts_out, offsets_out, n, t->bsum64, scan_tag(t, s), t->d_err,
-                             total_dev, t->d_err, t->ctl->lb_ids[dev::kLbScan], s);
+                             total_dev, t->d_err, lb_ctr(t, dev::kLbScan), s);
   if (!vals_cap) return SHM_OK;
   a.offsets = offsets_out;
   a.vals = vals_out;
@@ -1722,7 +1740,7 @@ int shm__scan_u64(shm_tree* t, const uint64_t* in, uint64_t* out, uint64_t n, ui
     return SHM_OK;
   }
   dev::launch_scan_u64_total(in, out, n, t->bsum64, scan_tag(t, s), t->d_err, tot_dev, t->d_err,
-                             t->ctl->lb_ids[dev::kLbScan], s);
+                             lb_ctr(t, dev::kLbScan), s);
   HIP_OK(hipGetLastError());
   return SHM_OK;
 }

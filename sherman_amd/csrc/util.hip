@@ -58,8 +58,8 @@ __device__ __forceinline__ T block_scan(T v, T* total) {
 
 // One launch: every 1024-op tile counts its staged heads, publishes the
 // count in its tagged word (chunk tag << 32 | count), sums the words of the
-// tiles before it (tile indices are tickets, lookback_index: a tile waits only
-// on tiles taken before it by running blocks), and fills its
+// tiles before it (tile index = blockIdx, or a ticket when the tree passes a
+// counter, lookback_index; tree.cpp lb_ctr says which and why), and fills its
 // segments: seg_start / seg_page at each staged head, seg_end at its run's
 // last op (the count of staged heads up to and including that op is the
 // segment's position + 1).
@@ -71,14 +71,15 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err,
                                                  UpperArgs q, int has_q, uint32_t* ids) {
-  const uint32_t b = lookback_index(ids);  // the tile
-  if (any_new && *any_new != tag) {  // no op of this chunk marked a page
-    if (b == 0) {
+  if (any_new && *any_new != tag) {  // no op of this chunk marked a page (every block)
+    if (blockIdx.x == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
       if (has_q) seg_complete_unchanged(q);
     }
     return;
   }
+  // the look-back's tile: a ticket, taken by every block past the check above
+  const uint32_t b = lookback_index(ids);
   const uint64_t nv = dev_n(n_dev, n);
   if ((uint64_t)b * kSegTile >= nv) {  // past the device count (the grid covers n)
     if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
@@ -106,14 +107,15 @@ __global__ __launch_bounds__(kT) void k_seg_fill_slot(const uint64_t* page, uint
   __shared__ uint32_t s_hd[kSegTile + 1];  // tile-relative run heads, in order
   __shared__ uint32_t s_pre[kT / kWave];
   __shared__ uint32_t s_ext_end, s_ext_new;
-  const uint32_t b = lookback_index(ids);  // the tile
-  if (any_new && *any_new != tag) {  // no op of this chunk is new
-    if (b == 0) {
+  if (any_new && *any_new != tag) {  // no op of this chunk is new (every block)
+    if (blockIdx.x == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
       if (has_q) seg_complete_unchanged(q);
     }
     return;
   }
+  // the look-back's tile: a ticket, taken by every block past the check above
+  const uint32_t b = lookback_index(ids);
   const uint64_t nv = dev_n(n_dev, n);
   if ((uint64_t)b * kSegTile >= nv) {  // past the device count (the grid covers n)
     if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;

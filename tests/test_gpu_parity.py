@@ -1316,8 +1316,9 @@ def test_lookback_kernels_of_two_trees_side_by_side(lib_ok):
     """The decoupled look-backs (k_bin_unique's bin prefix, k_seg_fill,
     k_scan_u64) of two trees queued side by side on two streams: each
     ordering's 256 bin blocks want a CU each, so the two launches share the
-    card.  Blocks take their look-back index by ticket (lookback_index,
-    device_common.h) and wait only on running blocks: every chunk ends with
+    card.  The bin prefix and the scans take their block index by ticket
+    (lookback_index, device_common.h; k_seg_fill keeps blockIdx by default,
+    tree.cpp lb_ctr) and wait only on running blocks: every chunk ends with
     no error bit (kErrBinSpin / kErrSegSpin / kErrScanSpin among them) and
     both trees hold the oracle's contents and scan counts."""
     rng = np.random.default_rng(777)
