@@ -382,15 +382,14 @@ constexpr uint32_t kSegTile = 1024;
 inline uint64_t seg_tiles(uint64_t n) { return (n + kSegTile - 1) / kSegTile; }
 // any_new (nullable): the locate's any-page-marked word (== tag: some page
 // gets a new key; otherwise there are no staged segments)
-// oslot (non-null, round 4): a run is staged when one of its ops was not
-// applied in place (oslot[i] == 0, k_locate's verdict) -- coalesced reads of
-// the ops instead of the page marks pnew (then unused)
+// self_after: a tile that has waited this many polls for an earlier tile's
+// word counts that tile's staged heads itself (0: at once, the test knob), so
+// no tile depends on another being placed (seg_tile.h)
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot = nullptr, const UpperArgs* quick = nullptr,
-                    uint32_t* ids = nullptr);
+                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
 // wraps); tot = {total, *err} for the range scan's one read-back

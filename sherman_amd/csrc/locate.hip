@@ -202,27 +202,10 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
 }
 
 __global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) { locate_body(a); }
-template <int W>
-__global__ __launch_bounds__(kLocBlock) __attribute__((amdgpu_waves_per_eu(W))) void k_locate_w(
-    WalkArgs a) {
-  locate_body(a);
-}
-
-// waves per SIMD (SHM_LOCATE_WAVES = 6 or 8, default: the compiler's 5; the A/B): the locate is
-// bound by its dependent random reads, so more lanes in flight may pay
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {
   if (n_upper == 0) return;
-  static const int w = [] {
-    const char* e = getenv("SHM_LOCATE_WAVES");
-    return e ? atoi(e) : 0;
-  }();
   const dim3 g((unsigned)((n_upper + kLocBlock - 1) / kLocBlock));
-  if (w >= 8)
-    hipLaunchKernelGGL(k_locate_w<8>, g, dim3(kLocBlock), 0, s, a);
-  else if (w == 6)
-    hipLaunchKernelGGL(k_locate_w<6>, g, dim3(kLocBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL(k_locate, g, dim3(kLocBlock), 0, s, a);
+  hipLaunchKernelGGL(k_locate, g, dim3(kLocBlock), 0, s, a);
 }
 
 }  // namespace dev

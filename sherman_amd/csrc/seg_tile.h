@@ -49,17 +49,43 @@ __device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint3
   return pnew[ga_offset(pg) >> 10] == new_mark(tag);
 }
 
+// The staged heads of tile x, counted by one thread (seg_tile's fallback):
+// the same count tile x publishes, from the same ops and page marks.
+__device__ __noinline__ uint32_t tile_heads(const uint64_t* page, uint64_t nv, uint64_t x,
+                                            const uint8_t* pnew, uint32_t tag) {
+  const uint64_t s0 = x * kSegTile;
+  const uint64_t e = s0 + kSegTile < nv ? s0 + kSegTile : nv;
+  uint32_t c = 0;
+  uint64_t prev = s0 ? page[s0 - 1] : ~0ull;
+  for (uint64_t i = s0; i < e; i += 8) {
+    uint64_t pg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pg[j] = i + j < e ? page[i + j] : prev;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool hd = i + j < e && (i + j == 0 || pg[j] != prev);
+      if (hd && page_new(pnew, pg[j], tag)) ++c;
+      prev = pg[j];
+    }
+  }
+  return c;
+}
+
 // Tile b (whole block): count its staged heads, publish the count in its
-// tagged word (chunk tag << 32 | count), sum the words of the tiles before it
-// (a tile waits only on tiles of smaller index, taken before it by running
-// blocks, so nothing waits on a tile that is not running), and fill its
-// segments: seg_start / seg_page at each staged head, seg_end at its run's
-// last op + 1 (the run may end in the next tile: read, not waited for), and
-// the total at the thread holding the last op.
+// tagged word (chunk tag << 32 | count), sum the words of the tiles before it,
+// and fill its segments: seg_start / seg_page at each staged head, seg_end at
+// its run's last op + 1 (the run may end in the next tile: read, not waited
+// for), and the total at the thread holding the last op.
+// Forward progress: a tile waits for an earlier
+// tile's word at most `self_after` polls and then counts that tile's staged
+// heads itself (tile_heads), so a tile whose block is not placed -- other
+// grids holding every slot -- delays the list but never blocks or corrupts
+// it, and no wait bound can leave a guessed prefix behind.  In the common
+// case the word is there within a few polls and nothing is recounted.
 __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint64_t b,
                                          uint64_t* lbw, uint32_t* seg_start, uint32_t* seg_end,
                                          uint64_t* seg_page, uint32_t* num_seg,
-                                         const uint8_t* pnew, uint32_t tag, uint32_t* err) {
+                                         const uint8_t* pnew, uint32_t tag, uint32_t self_after) {
   __shared__ uint32_t s_pre[kT / kWave];
   const uint64_t i0 = b * kSegTile + (uint64_t)threadIdx.x * kPer;
   uint32_t h[kPer], c = 0;
@@ -79,13 +105,12 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   for (uint64_t x = threadIdx.x; x < b; x += kT) {
     uint64_t w = 0;
     for (uint32_t spin = 0;; ++spin) {
-      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((w & ~0xFFFFFFFFull) == tg) break;
-      if (spin > (1u << 24)) {
-        atomicOr(err, kErrSegSpin);
-        w = tg;
+      if (spin >= self_after) {
+        w = tg | tile_heads(page, nv, x, pnew, tag);
         break;
       }
+      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & ~0xFFFFFFFFull) == tg) break;
       __builtin_amdgcn_s_sleep(1);
     }
     v += (uint32_t)w;

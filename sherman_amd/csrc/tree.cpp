@@ -38,7 +38,11 @@ constexpr uint32_t kRangeStage = 160;      // staged values per range scan
 constexpr uint64_t kRangeStageBytes = 256ull << 20;  // staging budget
 constexpr uint32_t kFlagWord = 512;        // read-back sequence word: byte 2048 of h_pin
 constexpr uint32_t kPubWord = 768;         // superblock mirror: u64 words 384.. of h_pin
-constexpr int kAppWaitMs = 2000;           // insert_order's host wait before an event fallback
+constexpr int kAppWaitMs = 5;              // insert_order's host wait before an event fallback
+// polls of an earlier segmentation tile's word before a tile counts that
+// tile's staged heads itself (seg_tile.h; ~1 ms, far past a placed tile's
+// few microseconds)
+constexpr uint32_t kSegSelfAfter = 1024;
 
 }  // namespace
 
@@ -181,7 +185,7 @@ struct shm_tree {
   Mark ex;                      // last exclusive call
   // insert ordering pipeline.  The ordering of chunk `tag` writes the op
   // buffers of parity tag & 1 (uk / uv / dk / counts, op_keys() below),
-  // which the apply of chunk tag - 2 read last (app_ev); every ordering
+  // which the apply of chunk tag - 2 read last (app_tag / app_m); every ordering
   // reuses the ordering scratch (ka .. bins), so it follows the previous
   // ordering (ord_ev).  A later chunk's ordering may therefore run on
   // another stream beside this chunk's apply.
@@ -237,17 +241,9 @@ hipStream_t pick(void* s) { return (hipStream_t)s; }
 // copies or the read-back kernel's own system-scope fence, never through
 // these events).  Default HIP events fence at system scope: a write-back of
 // the L2s at every record, measured as 12-22 us gaps around each C5 step's
-// cross-stream wait (tools/c5_trace.sh).  SHM_EVENT_SYSFENCE=1: the default
-// events (the A/B, tools/ab_events.sh: 59 GPU tests green with device scope;
-// C2 +0.7 %, C3 +4.7 %, C5 +3.1 % on one box).
-unsigned event_flags() {
-  static const unsigned f = [] {
-    const char* e = getenv("SHM_EVENT_SYSFENCE");
-    return (e && e[0] == '1') ? (unsigned)hipEventDisableTiming
-                              : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
-  }();
-  return f;
-}
+// cross-stream wait (round 4 A/B, tools/ab_events.sh: C2 +0.7 %, C3 +4.7 %,
+// C5 +3.1 % with device scope; the system-fence switch is gone).
+unsigned event_flags() { return (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence); }
 
 // INVARIANT: events from new_event() order streams of this device and
 // nothing else.  They are only ever passed to hipEventRecord and
@@ -382,13 +378,6 @@ void publish_host(shm_tree* t) {
 // this rule: each one a header and a summary read)
 // (SHM_DIR_READ_PHASE=0: only the growth rule, the A/B)
 constexpr uint32_t kReadPhase = 4;
-bool dir_read_phase_on() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_DIR_READ_PHASE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 // ... and likewise once the tree has gone quiet: the mirror showed
 // kQuietChunks newer chunk tags in a row with the same page count (updates
 // only, C3's mix after the load; while the directory is behind, every chunk
@@ -400,17 +389,8 @@ bool dir_read_phase_on() {
 constexpr uint32_t kQuietChunks = 2;
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
-  return dir_read_phase_on() && t->next_page != t->dir_np &&
+  return t->next_page != t->dir_np &&
          (t->reads_since_write >= kReadPhase || t->quiet_chunks >= kQuietChunks);
-}
-
-// directory entries in fingerprint form (SHM_DIR_FP=0: the round-2 form, A/B)
-bool dir_fp_on() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_DIR_FP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 // Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS,
@@ -428,22 +408,16 @@ uint32_t dir_extra_bits() {
   return x;
 }
 
-// The look-back kernels' block-index counters (lookback_index).
-// SHM_LB_TICKETS, a mask over kLbBin / kLbSeg / kLbScan, default 5 (the
-// ordering's bin prefix and the scans): a kernel whose bit is clear gets none
-// and its blocks use blockIdx.  k_bin_unique needs its ticket (256 blocks, one
-// per CU: two ranks on one GPU spun on each other, kErrBinSpin) and it costs
-// nothing measurable; k_seg_fill's 1024 blocks per C5 chunk serialise on the
-// counter (C5 5.19-5.23 K against 5.33-5.38 K Mops/s without, C3 -2 %), and
-// its 9 KB blocks (8 per CU, 2048 slots) only wait on an unplaced block when
-// other grids fill every slot, which the ticketed kernels cannot do for good
-// (DESIGN §3 "Batched insert" 4).
+// The look-back kernels' block-index counters (lookback_index): the
+// ordering's bin prefix (k_bin_unique: 256 blocks, one per CU; two ranks on
+// one GPU spun on each other with blockIdx, kErrBinSpin) and the scans take a
+// ticket, which costs nothing measurable there.  k_seg_fill keeps blockIdx:
+// its 1024 blocks per C5 chunk serialised on a counter (C5 5.19-5.23 K
+// against 5.33-5.38 K Mops/s, round-4 A/B), and it needs none for forward
+// progress: a tile that waits too long for an earlier tile counts that
+// tile's staged heads itself (seg_tile.h).
 uint32_t* lb_ctr(shm_tree* t, int which) {
-  static const uint32_t mask = [] {
-    const char* e = getenv("SHM_LB_TICKETS");
-    return e ? (uint32_t)atoi(e) : 5u;
-  }();
-  return (mask >> which) & 1u ? t->ctl->lb_ids[which] : nullptr;
+  return which == dev::kLbSeg ? nullptr : t->ctl->lb_ids[which];
 }
 
 int refresh_dir(shm_tree* t, hipStream_t s) {
@@ -476,7 +450,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   }
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
                        t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint,
-                       t->hint_ok ? 1 : 0, dir_fp_on() ? t->sum : nullptr, t->d_err, s);
+                       t->hint_ok ? 1 : 0, t->sum, t->d_err, s);
   t->dir_np = t->next_page;
   t->dir_valid = true;
   t->hint_ok = true;
@@ -703,8 +677,10 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   // apply's stream gets no event record (≈ 4.6 µs of idle device between
   // kernels, tools/event_gap.hip), and the device no polling wait (a
   // wait-value kernel: a profiler that serialises kernels deadlocks on it).
-  // A wait past kAppWaitMs (the apply's stream held up by the caller) falls
-  // back to an event at that stream's tail.
+  // A wait past kAppWaitMs (5 ms: the apply's stream held up by the caller,
+  // or the card shared) falls back to an event at that stream's tail, so a
+  // stalled apply costs this call (which holds the tree's mutex) at most
+  // that long on the host.
   if (t->app_valid[p] && t->app_m[p].s != s) {
     const volatile uint64_t* ap =
         reinterpret_cast<const volatile uint64_t*>(t->h_pin) + kPubWord / 2 + dev::kPubApplied;
@@ -719,16 +695,13 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
   }
   // Tile mode (chunks of <= kMaxTiles tiles, i.e. <= 1 Mi ops): the tiles
   // write their survivors sorted by coarse bin and k_bin_unique gathers its
-  // bin's runs from every tile, so there is no coarse scatter pass (round 4;
-  // SHM_TILE_MODE=0 restores the coarse pass, the A/B).  The tiles' output
+  // bin's runs from every tile, so there is no coarse scatter pass (round 4:
+  // C3 9612 -> 10231, C5 4425 -> 4703 Mops/s); a larger chunk takes the
+  // coarse pass.  The tiles' output
   // (kb / ia) stays live through k_bin_unique, so a bin over kUniqCap ops
   // sorts in ka / ib with kc / id as scratch and ic for its ranks.
-  static const bool tile_mode_on = [] {
-    const char* e = getenv("SHM_TILE_MODE");
-    return !(e && e[0] == '0');
-  }();
   const uint64_t tiles = (n + dev::kIsortTile - 1) / dev::kIsortTile;
-  const bool tile_mode = tile_mode_on && tiles <= (uint64_t)dev::kMaxTiles;
+  const bool tile_mode = tiles <= (uint64_t)dev::kMaxTiles;
   // tile mode: M and Mx bin-major in part_mt / part_mx (part_hist keeps the
   // coarse pass's tile-major layout for the other path and ordered gets)
   dev::launch_tile_dedup(keys, n, t->kb, t->ia, t->gcount, t->d_err, &t->ctl->gate, tag,
@@ -752,18 +725,6 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
 }
 
 // steps 2-5 on the ordered chunk of tag (the leaf directory is current)
-// segmentation from the ops' own verdicts (k_seg_fill_slot) instead of the
-// page marks: SHM_SEG_SLOTS=1.  Measured slower (one gpurun call, C5 4517
-// against 4678 Mops/s with the marks, whose random byte reads hit L2), so
-// the marks stay the default
-bool seg_from_slots() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_SEG_SLOTS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
@@ -779,7 +740,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   }
   // the byte marks repeat every 255 chunks: clear them when they wrap, so
   // no page still carries this chunk's mark from 255 chunks ago
-  if (!seg_from_slots() && dev::new_mark(tag) == 1)
+  if (dev::new_mark(tag) == 1)
     HIP_OK(hipMemsetAsync(t->pnew, 0, t->cap_pages, s));
   dev::WalkArgs w = walk_args(t);
   uint64_t* const cnt = op_counts(t, tag);
@@ -789,7 +750,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.out_page = t->pages;
   w.target_level = 0;
   w.out_slot = t->oslot;
-  w.out_new = seg_from_slots() ? nullptr : t->pnew;  // the page marks: the old segmentation only
+  w.out_new = t->pnew;  // the page marks the segmentation reads
   w.out_new_tag = tag;
   w.any_new = reinterpret_cast<uint32_t*>(t->d_counts + 10);
   w.vals = op_vals(t, tag);
@@ -846,37 +807,23 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   if (u.dir) u.dir_hint = t->dir_hint;
   u.stamps = t->stamps;
   u.force_abort = (t->force_flags & 1u) ? 1u : 0u;
-  static const bool lists_only = [] {
-    const char* e = getenv("SHM_UPPER_LISTS");
-    return e && e[0] == '1';
-  }();
-  u.no_direct = lists_only || (t->force_flags & 2u) ? 1u : 0u;
-  static const bool no_prelock = [] {
-    const char* e = getenv("SHM_UPPER_PRELOCK");
-    return e && e[0] == '0';
-  }();
-  u.no_prelock = no_prelock ? 1u : 0u;
-  static const uint32_t quick = [] {
-    const char* e = getenv("SHM_UPPER_QUICK");
-    return e ? (uint32_t)atoi(e) : 1u;
-  }();
-  u.quick = quick;
+  u.no_direct = (t->force_flags & 2u) ? 1u : 0u;
+  u.no_prelock = 0;
+  u.quick = 1;
   u.pub_always = t->next_page != t->dir_np ? 1u : 0u;
-  // small splits built by the upsert kernel itself (SHM_EARLY_SPLIT=0: all
-  // left to k_upper, round 4's path); the forced k_upper paths keep theirs
-  static const bool no_early = [] {
-    const char* e = getenv("SHM_EARLY_SPLIT");
-    return e && e[0] == '0';
-  }();
+  // small splits built by the upsert kernel itself; the forced k_upper paths
+  // (force flags 1, 2, 4) leave them all to k_upper
   dev::UpperArgs ue = u;
-  ue.early = no_early || (t->force_flags & 7u) ? 0u : 1u;
+  ue.early = (t->force_flags & 7u) ? 0u : 1u;
   // a chunk with no new key and no delete is completed by the segmentation
   // kernel's block 0 (u: k_upper's quick path; k_upper then returns at once).
   const bool quick_ok = u.quick && !u.force_abort;
+  // force flag bit 3: every tile counts its predecessors itself (the
+  // look-back's fallback, exercised by a test)
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
                       t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
-                      seg_from_slots() ? t->oslot : nullptr, quick_ok ? &u : nullptr,
-                      lb_ctr(t, dev::kLbSeg));
+                      quick_ok ? &u : nullptr, lb_ctr(t, dev::kLbSeg),
+                      (t->force_flags & 8u) ? 0u : kSegSelfAfter);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
@@ -1547,8 +1494,9 @@ int shm_insert_apply(shm_tree* t, uint32_t ticket, void* stream) {
   Order ord(t, s, true);
   if (ord.rc) return ord.rc;
   if (pd.s != s) HIP_OK(hipStreamWaitEvent(s, pd.ev, 0));
-  // the slot is free once its apply is queued (the buffers' reuse waits for
-  // app_ev on the device)
+  // the slot is free once its apply is queued (the buffers' reuse waits on
+  // the host for this chunk's kPubApplied tag in the mirror, with an event
+  // at the apply stream's tail as the fallback: insert_order)
   std::swap(t->pend[0], t->pend[1]);
   --t->n_pend;
   mirror(t);

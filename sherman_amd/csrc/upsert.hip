@@ -293,7 +293,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
 // of group g + W are already landing in the other (LDS-DMA) and the segment
 // records of g + 2W and the ops of g + W are in flight.  Per group the wave
 // then pays about the apply time instead of two dependent HBM round trips.
-template <int G, bool IL>
+template <int G>
 __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperArgs& u,
                                                   BlockQ* el, bool early, uint64_t cursor0,
                                                   uint64_t cap, uint64_t W, uint64_t ngroups,
@@ -390,12 +390,6 @@ __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperA
     }
     err |= apply_group<G>(a, bufs + b * G * kPageDwords, g * G, num_seg, c_page, c_pok && held,
                           true, c_qst, c_qen, c_pk, c_pv, c_po, u, el, early, cursor0);
-    // one queued early split between groups (the next group's pages keep
-    // landing meanwhile)
-    if constexpr (IL) {
-      uint32_t x;
-      if (early && take_early(el, x)) err |= split_early(u, Lw, el->item[x], cursor0, cap);
-    }
     if (gn >= ngroups) break;
     g = gn;
     gn = gm;
@@ -421,9 +415,10 @@ __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperA
 // splits run beside the in-place groups instead of in a kernel of their own.
 // A block's waves are resident together: a wave without groups waits (LDS)
 // for its block's last queued split, never for other blocks.
-// IL: a wave also takes a queued split between its groups (else only once
-// the block's groups are all taken)
-template <int G, bool IL>
+// A wave takes queued splits once the block's groups are all taken (taking
+// them between groups, round 4's interleaved variant, needed more VGPRs than
+// the pipelined loop leaves and measured slower).
+template <int G>
 __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[kWavesPerBlock * 2 * G * kPageDwords];
   __shared__ __attribute__((aligned(16))) WaveLds s_wl[kWavesPerBlock];
@@ -453,7 +448,7 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
     s_q.eclaim = 0;
   }
   __syncthreads();
-  uint32_t err = upsert_groups<G, IL>(a, u, &s_q, early, cursor0, cap, W, ngroups, num_seg, s_pg,
+  uint32_t err = upsert_groups<G>(a, u, &s_q, early, cursor0, cap, W, ngroups, num_seg, s_pg,
                                   s_wl[wv]);
   // this wave queues nothing more
   if (lane == 0) __hip_atomic_fetch_add(&s_q.active, ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -489,42 +484,24 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
 
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a, UpperArgs u) {
-  upsert_body<G, false>(a, u);
-}
-// interleaved variants (SHM_UPSERT_IL=1: as many VGPRs as it takes, 2 waves
-// per SIMD; 2: held to 3 waves per SIMD, spilling)
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_leaf_upsert_il(SegArgs a, UpperArgs u) {
-  upsert_body<G, true>(a, u);
-}
-template <int G>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_leaf_upsert_il3(
-    SegArgs a, UpperArgs u) {
-  upsert_body<G, true>(a, u);
+  upsert_body<G>(a, u);
 }
 
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
   constexpr int G = 4;
   if (!a.num_seg) return;
-  static const int mode = [] {
-    const char* e = getenv("SHM_UPSERT_IL");
-    return e ? atoi(e) : 0;
-  }();
-  using K = void (*)(SegArgs, UpperArgs);
-  const int m = mode >= 0 && mode <= 2 ? mode : 0;
-  const K k = m == 1 ? k_leaf_upsert_il<G> : m == 2 ? k_leaf_upsert_il3<G> : k_leaf_upsert_pipe<G>;
-  static unsigned blocks[3] = {0, 0, 0};
-  unsigned& nb = blocks[m];
+  static unsigned nb = 0;
   if (!nb) {
     int per_cu = 0, cus = 0, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_leaf_upsert_pipe<G>, kBlock, 0);
     nb = (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
   }
   const uint64_t groups = (a.num_seg + G - 1) / G;
   const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(k, dim3((unsigned)std::min<uint64_t>(need, nb)), dim3(kBlock), 0, s, a, u);
+  hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, nb)), dim3(kBlock),
+                     0, s, a, u);
 }
 
 }  // namespace dev

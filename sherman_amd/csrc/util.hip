@@ -70,7 +70,8 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  uint64_t* seg_page, uint32_t* num_seg,
                                                  const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err,
-                                                 UpperArgs q, int has_q, uint32_t* ids) {
+                                                 UpperArgs q, int has_q, uint32_t* ids,
+                                                 uint32_t self_after) {
   if (any_new && *any_new != tag) {  // no op of this chunk marked a page (every block)
     if (blockIdx.x == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
@@ -85,182 +86,20 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
     if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
     return;
   }
-  segt::seg_tile(page, nv, b, lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, err);
-}
-
-// The same list from the ops' own verdicts (round 4): a run is staged when
-// any of its ops was not applied in place (oslot[i] == 0, k_locate), which a
-// tile reads with the ops -- coalesced -- instead of one random byte of the
-// page marks per run head and tail.  A tile owns the runs whose HEAD it
-// holds: a prefix count of its new ops gives each run's verdict, and the
-// last run, when it goes on past the tile, is followed by the whole block
-// 1024 ops at a time (a bulk load's run over thousands of ops included), so
-// seg_end is written by the head's tile and no tile waits on a later one.
-__global__ __launch_bounds__(kT) void k_seg_fill_slot(const uint64_t* page, uint64_t n,
-                                                      const uint64_t* n_dev, uint64_t* lbw,
-                                                      uint32_t* seg_start, uint32_t* seg_end,
-                                                      uint64_t* seg_page, uint32_t* num_seg,
-                                                      const uint32_t* oslot, uint32_t tag,
-                                                      const uint32_t* any_new, uint32_t* err,
-                                                      UpperArgs q, int has_q, uint32_t* ids) {
-  __shared__ uint32_t s_nw[kSegTile + 1];  // new ops before tile index j
-  __shared__ uint32_t s_hd[kSegTile + 1];  // tile-relative run heads, in order
-  __shared__ uint32_t s_pre[kT / kWave];
-  __shared__ uint32_t s_ext_end, s_ext_new;
-  if (any_new && *any_new != tag) {  // no op of this chunk is new (every block)
-    if (blockIdx.x == 0) {
-      if (threadIdx.x == 0) *num_seg = 0;
-      if (has_q) seg_complete_unchanged(q);
-    }
-    return;
-  }
-  // the look-back's tile: a ticket, taken by every block past the check above
-  const uint32_t b = lookback_index(ids);
-  const uint64_t nv = dev_n(n_dev, n);
-  if ((uint64_t)b * kSegTile >= nv) {  // past the device count (the grid covers n)
-    if (nv == 0 && b == 0 && threadIdx.x == 0) *num_seg = 0;
-    return;
-  }
-  const uint64_t t0 = (uint64_t)b * kSegTile;
-  const uint32_t len = (uint32_t)min((uint64_t)kSegTile, nv - t0);
-  const uint32_t j0 = threadIdx.x * kScanPer;
-  uint32_t h[kScanPer], nw[kScanPer], ch = 0, cn = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const uint64_t i = t0 + j0 + j;
-    h[j] = segt::seg_head(page, i, nv);
-    nw[j] = i < nv && !(oslot[i] & 0x80000000u) ? 1u : 0u;
-    ch += h[j];
-    cn += nw[j];
-  }
-  uint32_t nh, tnw;
-  const uint32_t xh = block_scan<uint32_t>(ch, &nh);
-  const uint32_t xn = block_scan<uint32_t>(cn, &tnw);
-  {
-    uint32_t ph = xh, pn = xn;
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j) {
-      s_nw[j0 + j] = pn;
-      pn += nw[j];
-      if (h[j]) s_hd[ph++] = j0 + j;
-    }
-  }
-  if (threadIdx.x == 0) {
-    s_nw[kSegTile] = tnw;  // (entries past len are not read)
-    s_hd[nh] = len;
-    s_ext_end = 0xFFFFFFFFu;
-    s_ext_new = 0;
-  }
-  __syncthreads();
-  // the last run goes on past the tile: follow it
-  const uint64_t t1 = t0 + len;
-  bool ext = nh > 0 && t1 < nv && page[t1] == page[t1 - 1];
-  uint64_t ext_end = t1;
-  uint32_t ext_new = 0;
-  if (ext) {
-    const uint64_t rp = page[t1 - 1];
-    for (uint64_t c = t1;; c += kSegTile) {
-#pragma unroll
-      for (int j = 0; j < kScanPer; ++j) {
-        const uint64_t i = c + j0 + j;
-        if (i >= nv) {
-          atomicMin(&s_ext_end, (uint32_t)(i - t1));
-        } else if (page[i] != rp) {
-          atomicMin(&s_ext_end, (uint32_t)(i - t1));
-        }
-      }
-      __syncthreads();
-      const uint32_t e = s_ext_end;  // block-uniform
-#pragma unroll
-      for (int j = 0; j < kScanPer; ++j) {
-        const uint64_t i = c + j0 + j;
-        if (i - t1 < (uint64_t)e && i < nv && !(oslot[i] & 0x80000000u)) s_ext_new = 1;
-      }
-      __syncthreads();
-      if (e != 0xFFFFFFFFu) {
-        ext_end = t1 + e;
-        ext_new = s_ext_new;
-        break;
-      }
-    }
-  }
-  // staged runs among this tile's heads (thread x handles heads x, x + kT, ...)
-  constexpr int kHP = (int)kSegTile / kT;
-  uint32_t st[kHP], cst = 0;
-#pragma unroll
-  for (int r = 0; r < kHP; ++r) {
-    const uint32_t q = threadIdx.x + (uint32_t)r * kT;
-    st[r] = 0;
-    if (q < nh) {
-      // new ops in [a0, a1): s_nw holds the prefix at every index <= len
-      // (ops past len are past nv: never new), the run's tail past the tile
-      // counted by ext_new
-      const uint32_t a0 = s_hd[q], a1 = s_hd[q + 1];
-      const bool last = q + 1 == nh;
-      st[r] = (s_nw[a1] - s_nw[a0] + (last ? ext_new : 0u)) ? 1u : 0u;
-    }
-    cst += st[r];
-  }
-  uint32_t total;
-  const uint32_t local = block_scan<uint32_t>(cst, &total);
-  const uint64_t tg = (uint64_t)tag << 32;
-  if (threadIdx.x == 0)
-    __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the counts of the tiles before this one
-  uint32_t v = 0;
-  for (uint32_t x = threadIdx.x; x < b; x += kT) {
-    uint64_t w = 0;
-    for (uint32_t spin = 0;; ++spin) {
-      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((w & ~0xFFFFFFFFull) == tg) break;
-      if (spin > (1u << 24)) {
-        atomicOr(err, kErrSegSpin);
-        w = tg;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    v += (uint32_t)w;
-  }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = v;
-  __syncthreads();
-  uint32_t pos = local;
-#pragma unroll
-  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
-#pragma unroll
-  for (int r = 0; r < kHP; ++r) {
-    const uint32_t q = threadIdx.x + (uint32_t)r * kT;
-    if (q < nh && st[r]) {
-      const uint32_t a0 = s_hd[q], a1 = s_hd[q + 1];
-      seg_start[pos] = (uint32_t)(t0 + a0);
-      seg_page[pos] = page[t0 + a0];
-      seg_end[pos] = (uint32_t)(q + 1 < nh ? t0 + a1 : (ext ? ext_end : t1));
-      ++pos;
-    }
-  }
-  // the tile holding the last op: the list's length (this tile's prefix + its
-  // own staged runs)
-  if (t1 == nv && threadIdx.x == kT - 1) *num_seg = pos;
+  segt::seg_tile(page, nv, b, lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, self_after);
 }
 
 void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uint64_t* lbw,
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const uint32_t* oslot, const UpperArgs* quick, uint32_t* ids) {
+                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after) {
   if (!n) return;
   const UpperArgs q = quick ? *quick : UpperArgs{};
   const int has_q = quick && any_new ? 1 : 0;
-  if (oslot)
-    hipLaunchKernelGGL(k_seg_fill_slot, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n,
-                       n_dev, lbw, seg_start, seg_end, seg_page, num_seg, oslot, tag, any_new,
-                       err, q, has_q, ids);
-  else
-    hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev,
-                       lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q,
-                       has_q, ids);
+  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev,
+                     lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q,
+                     has_q, ids, self_after);
 }
 
 // Exclusive scan of u64 counts in one launch: every 1024-element tile
