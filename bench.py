@@ -54,7 +54,17 @@ ALG_BYTES_PER_GET = 1040     # 1024 B leaf + 8 B key + 8 B value: 
 # L2 line (directory entry, the 64 B leaf summary, the matching entry) + 8 B
 # key + 8 B value
 ALG_BYTES_PER_GET_SUM = 3 * 128 + 16
-ALG_BYTES_PER_INSERT = 1074  # 1024 B leaf + 18 B entry + 16 B k/v + 16 B lock
+ALG_BYTES_PER_INSERT = 1074  # the reference's per-op leaf read (context only)
+# A batched insert chunk's algorithmic bytes, per touched leaf rather than per
+# op: the random 128 B lines and whole pages the
+# sorted, de-duplicated chunk must touch (Tree.cpp:828-991 restated per leaf)
+LINE = 128                   # a random read is served as one 128 B line
+ALG_UPSERT = 16 + 2 * LINE + 64   # sorted op in + directory entry + slot line + entry write
+ALG_DELETE = 8 + 2 * LINE + 64    # sorted key in + directory entry + slot line + entry write
+ALG_STAGED_LEAF = 1024       # a leaf that gets a new key is read whole (free-slot search)
+ALG_NEW_PAGE = 1024 + LINE   # a split's new page written + its separator's parent line
+ALG_ORDER_PER_OP = 16        # the ordering reads each op (key + value) ...
+ALG_ORDER_PER_UNIQUE = 16    # ... and writes each surviving op once
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 N_BATCHES = 8                # distinct resident batches the steps cycle over
 
@@ -99,9 +109,6 @@ def parse():
     p.add_argument("--prio", type=int, default=0, choices=(0, 1),
                    help="c3 / c5 pipelined: 1 = the gets' / scans' and tree changes' "
                         "stream at high priority, the ordering's at normal")
-    p.add_argument("--dir-fp", type=int, default=None, choices=(0, 1),
-                   help="leaf-directory entries of one-leaf prefixes carry the leaf's "
-                        "fingerprints (SHM_DIR_FP; library default 1; 0 = round-2 form)")
     p.add_argument("--dir-extra-bits", type=int, default=None,
                    help="leaf directory with 2^x entries per tree page (SHM_DIR_EXTRA_BITS)")
     p.add_argument("--order-first", type=int, default=0, choices=(0, 1),
@@ -144,6 +151,62 @@ def parse():
     if a.steps is None:
         a.steps = 20 if a.workload == "c5" else 200
     return a
+
+
+def insert_alg_bytes(ops, uniq, dels, staged, new_pages, ordering):
+    """Algorithmic bytes of insert chunks (per touched leaf):
+    every unique upsert / delete reads its sorted op, its directory entry and
+    the line holding its slot and writes its entry; a leaf that gets a new
+    key is read whole; a split writes its new pages and their parents' lines;
+    with the ordering inside the window, the ops in and the survivors out."""
+    b = uniq * ALG_UPSERT + dels * ALG_DELETE + staged * ALG_STAGED_LEAF + new_pages * ALG_NEW_PAGE
+    if ordering:
+        b += ops * ALG_ORDER_PER_OP + (uniq + dels) * ALG_ORDER_PER_UNIQUE
+    return b
+
+
+def cap_fracs(d, keys):
+    """Refuse a roofline fraction above 1 (it would claim more than the HBM
+    peak): the field becomes null and the value moves to d["refused"]."""
+    for k in keys:
+        v = d.get(k)
+        if v is not None and v > 1.0:
+            d[k] = None
+            d.setdefault("refused", {})[k] = v
+
+
+class Region:
+    """rocprofv3 --selected-regions: collection only between
+    roctxProfilerResume(0) and roctxProfilerPause(0).  SHM_BENCH_REGION names
+    the window a profiling run wants (tools/roofline_pass.sh): "profile" =
+    the roofline pass whose HIP-event times give roofline.achieved, "timed" =
+    the timed steps; unset = no markers."""
+
+    def __init__(self):
+        self.want = os.environ.get("SHM_BENCH_REGION")
+        self.lib = None
+        if self.want:
+            import ctypes
+            for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                         "libroctx64.so.4"):
+                try:
+                    self.lib = ctypes.CDLL(name)
+                    break
+                except OSError:
+                    pass
+            assert self.lib is not None, "SHM_BENCH_REGION set but no roctx library"
+            for f in (self.lib.roctxProfilerResume, self.lib.roctxProfilerPause):
+                f.argtypes, f.restype = [ctypes.c_uint64], None
+
+    def begin(self, name):
+        if self.lib is not None and name == self.want:
+            self.lib.roctxProfilerResume(0)
+
+    def end(self, name):
+        if self.lib is not None and name == self.want:
+            import torch
+            torch.cuda.synchronize()
+            self.lib.roctxProfilerPause(0)
 
 
 def log(*a):
@@ -189,8 +252,6 @@ def build_shard(tree, n_keys, world, rank, dev):
 
 def main():
     args = parse()
-    if args.dir_fp is not None:  # read by the library when it loads
-        os.environ["SHM_DIR_FP"] = str(args.dir_fp)
     if args.dir_extra_bits is not None:
         os.environ["SHM_DIR_EXTRA_BITS"] = str(args.dir_extra_bits)
     import torch
@@ -511,8 +572,10 @@ def main():
         rewarm(tree, dev)
     for i in range(args.warmup):
         step(i)
+    region = Region()
     barrier()
     splits0 = tree.stats()["splits"]
+    region.begin("timed")
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -523,6 +586,7 @@ def main():
         cshard.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    region.end("timed")
     tree.synchronize()  # raises any error of the queued batches
     rank_mops = batch * args.steps / elapsed / 1e6
     cluster_sum = rank_mops
@@ -589,11 +653,17 @@ def main():
     # runs these batches one at a time on one stream, so each launch's
     # duration is the kernel's own (the timed steps overlap two walks) -----
     tree.profile(True)
+    tree.profile_read(reset=True)
+    prof_splits0 = tree.stats()["splits"]
+    region.begin("profile")
     for i in range(args.profile_steps):
         (one if args.workload == "c2" else step)(i)
     torch.cuda.synchronize()
+    region.end("profile")
     prof = tree.profile_read(reset=True)
     tree.profile(False)
+    # pages the profiled chunks' splits made (early and in k_upper)
+    prof_new_pages = tree.stats()["splits"] - prof_splits0
     idx = None
     if args.workload in ("c2", "c3") and args.sort != "on" and (args.profile_steps > 0 or
                                                                 args.index_stats):
@@ -763,54 +833,100 @@ def main():
             req = _request_roofline(batch, args.keys_log2, mops * 1e6 / world, page_walk)
             if req:
                 rf.update(req)
+        if args.workload in ("c3", "c5"):
+            # the insert chunks of the profile pass, counted on the device
+            ic = max(prof["insert_calls"], 1)
+            per = {"ops": prof["insert_ops"] / ic, "uniq": prof["insert_unique"] / ic,
+                   "dels": prof["insert_dels"] / ic, "staged": prof["insert_staged"] / ic,
+                   "new_pages": prof_new_pages / ic}
+            pipelined = (args.pipeline and world == 1 and
+                         (args.workload == "c3" or bool(args.async_scans and
+                                                        args.scan_out == "slots" and
+                                                        args.streams == 2)))
+            # the profiled window: the tree phase alone when pipelined (the
+            # ordering ran a step earlier on its own stream), else the chunk
+            alg_win = insert_alg_bytes(per["ops"], per["uniq"], per["dels"], per["staged"],
+                                       per["new_pages"], ordering=not pipelined)
+            alg_chunk = insert_alg_bytes(per["ops"], per["uniq"], per["dels"], per["staged"],
+                                         per["new_pages"], ordering=True)
+            pmc = _step_traffic(args.workload, batch, args.keys_log2)
+            ins = {
+                "insert_ms_per_launch": round(ins_ms, 4),
+                "upsert_ms_per_launch": round(ups_ms, 4),
+                "window": ("insert_apply chunk (locate + segmentation + upsert + k_upper; the "
+                           "ordering runs one chunk ahead on its own stream)" if pipelined else
+                           "insert chunk (ordering + locate + segmentation + upsert + k_upper)"),
+                "per_chunk": {k: round(v, 1) for k, v in per.items()},
+                "alg_bytes_per_chunk": round(alg_win),
+                "alg_model": "DESIGN §5: %d B per unique upsert, %d B per delete, %d B per leaf "
+                             "read whole, %d B per new page%s" % (
+                                 ALG_UPSERT, ALG_DELETE, ALG_STAGED_LEAF, ALG_NEW_PAGE,
+                                 "" if pipelined else ", + 16 B per op in and per survivor out"),
+                "alg_GBps": round(alg_win / (ins_ms * 1e-3) / 1e9, 1) if ins_ms else None,
+                "reference_bytes_per_insert": ALG_BYTES_PER_INSERT,
+            }
+            ins["alg_frac"] = round(ins["alg_GBps"] / HBM_PEAK_GBS, 4) if ins["alg_GBps"] else None
+            if pmc is not None:
+                tb = pmc["apply_bytes_per_chunk"] + (0 if pipelined else pmc["order_bytes_per_chunk"])
+                ins.update({"traffic": tb,
+                            "traffic_GBps": round(tb / (ins_ms * 1e-3) / 1e9, 1) if ins_ms else None,
+                            "traffic_source": pmc["source"]})
+                ins["traffic_frac"] = (round(ins["traffic_GBps"] / HBM_PEAK_GBS, 4)
+                                       if ins["traffic_GBps"] else None)
+            cap_fracs(ins, ("alg_frac", "traffic_frac"))
         if args.workload == "c5":
-            # the insert pipeline dominates: ops x 1074 B over its measured
-            # chunk time (HIP events on the insert stream)
-            ach = ins_per_launch * ALG_BYTES_PER_INSERT / (ins_ms * 1e-3) / 1e9 if ins_ms else 0.0
             out["config"]["hit_rate"] = None
             out["config"]["values_per_scan"] = round(hit_rate, 2)
-            out["config"]["insert_pipeline"] = bool(world == 1 and args.async_scans and
-                                                    args.scan_out == "slots" and
-                                                    args.pipeline and args.streams == 2)
+            out["config"]["insert_pipeline"] = bool(pipelined)
             out["config"]["scan_out"] = (("slots of %d values" % args.slot_cap)
                                          if world == 1 and args.async_scans and
                                          args.scan_out == "slots" else "compact")
-            pipelined = out["config"]["insert_pipeline"]
-            out["roofline"].update({
-                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                # pipelined, the profile times the chunk's tree phase alone: its
-                # ordering ran one step earlier beside the scans and the previous
-                # chunk (shm_insert_order); step_alg_GBps below covers the whole step
-                "kernel": ("insert_apply chunk (locate + k_leaf_upsert + splits; the ordering "
-                           "runs one chunk ahead on its own stream)" if pipelined else
-                           "insert_batch chunk (ordering + locate + k_leaf_upsert + splits)"),
-                "step_alg_GBps": round(ins_per_launch * ALG_BYTES_PER_INSERT /
-                                       (elapsed / args.steps) / 1e9, 1),
-                "alg_bytes_per_insert": ALG_BYTES_PER_INSERT,
-                "insert_ms_per_launch": round(ins_ms, 4),
-                "upsert_ms_per_launch": round(ups_ms, 4),
-                "inserts_per_launch": int(ins_per_launch),
-                "range_ms_per_launch": round(range_ms, 4),
-                "walk_ms_per_launch": None, "order_ms_per_launch": None,
-                "queries_per_launch": None, "alg_bytes_per_get": None,
-                "traffic": (_profile_traffic("pmc_insert.json", "hbm_bytes_per_chunk",
-                                             batch, args.keys_log2)
-                            if args.start == "dir" else None)})
             rf = out["roofline"]
-            # the bytes the chunk really moves (PMC) over its measured time:
-            # the real-traffic fraction beside the survey's 1074 B per op
-            rf["traffic_GBps"] = (round(rf["traffic"] / (ins_ms * 1e-3) / 1e9, 1)
-                                  if rf["traffic"] and ins_ms else None)
-            rf["traffic_frac"] = (round(rf["traffic_GBps"] / HBM_PEAK_GBS, 4)
-                                  if rf["traffic_GBps"] else None)
+            for k in ("walk_ms_per_launch", "order_ms_per_launch", "queries_per_launch",
+                      "alg_bytes_per_get", "reference_bytes_per_get", "reference_bytes_GBps",
+                      "traffic_per_get", "step_alg_GBps", "full_path_bytes_per_get"):
+                rf.pop(k, None)
+            rf.update(ins)
+            # the headline is the real traffic of the chunk's kernels (PMC) over
+            # its measured time, the per-leaf model beside it
+            real = ins.get("traffic_GBps") is not None
+            rf["kernel"] = ins["window"]
+            rf["achieved"] = ins["traffic_GBps"] if real else ins["alg_GBps"]
+            rf["achieved_basis"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE of the window's kernels"
+                                    if real else "algorithmic (per touched leaf)")
+            rf["frac"] = ins["traffic_frac"] if real else ins["alg_frac"]
+            rf["traffic"] = ins.get("traffic")
+            rf["range_ms_per_launch"] = round(range_ms, 4)
+            rf["inserts_per_launch"] = int(ins_per_launch)
+            # the whole step: the chunk's algorithmic bytes (ordering included)
+            # over the step time
+            rf["step_alg_GBps"] = round(alg_chunk / (elapsed / args.steps) / 1e9, 1)
+            rf["step_frac"] = round(rf["step_alg_GBps"] / HBM_PEAK_GBS, 4)
         if args.workload == "c3":
-            # whole-step algorithmic rate (gets as walked, inserts 1074 B per op)
+            # the whole step: its gets as walked + its insert chunk (ordering
+            # included), over the step time; and the step's PMC bytes
             step_s = elapsed / args.steps
             b0 = mixed[0]
-            alg = (b0[0].numel() * bpg + b0[1].numel() * ALG_BYTES_PER_INSERT)
+            alg = b0[0].numel() * bpg + alg_chunk
             out["config"]["insert_pipeline"] = bool(args.pipeline and world == 1)
-            out["roofline"]["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
-            out["roofline"]["step_frac"] = round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4)
+            rf = out["roofline"]
+            rf["insert"] = ins
+            rf["walk_frac"] = rf["frac"]  # the get walk alone (k_get_sum), as C2
+            rf["step_alg_GBps"] = round(alg / step_s / 1e9, 1)
+            rf["step_frac"] = round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4)
+            if pmc is not None and pmc.get("step_bytes"):
+                rf["step_traffic"] = pmc["step_bytes"]
+                rf["step_traffic_GBps"] = round(pmc["step_bytes"] / step_s / 1e9, 1)
+                rf["step_traffic_frac"] = round(rf["step_traffic_GBps"] / HBM_PEAK_GBS, 4)
+                # the headline: the step's real traffic
+                rf["frac"] = rf["step_traffic_frac"]
+                rf["achieved"] = rf["step_traffic_GBps"]
+                rf["achieved_basis"] = ("PMC bytes of one step's kernels (gets, ordering, "
+                                        "tree phase) over the timed step")
+                rf["kernel"] = "C3 step (k_get_sum + insert chunk)"
+        cap_fracs(out["roofline"], ("frac", "step_frac", "walk_frac", "step_traffic_frac",
+                                    "reference_bytes_frac", "request_frac", "alg_frac",
+                                    "traffic_frac"))
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
@@ -847,6 +963,20 @@ def _profile_traffic(name, field, batch, keys_log2, kernel=None):
     return None
 
 
+def _step_traffic(workload, batch, keys_log2):
+    """The C3 / C5 PMC bytes measured over the bench's own profile window
+    (profiles/pmc_steps.json, tools/roofline_pass.sh -> tools/fold_roofline.py)
+    when taken at this batch and key count: {apply_bytes_per_chunk,
+    order_bytes_per_chunk, step_bytes, source} or None."""
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_steps.json")))[workload]
+    except (OSError, ValueError, KeyError):
+        return None
+    if pmc.get("batch") == batch and pmc.get("keys_log2") == keys_log2:
+        return pmc
+    return None
+
+
 def _request_roofline(batch, keys_log2, gets_per_s, page_walk):
     """requests/get from the committed PMC pass (profiles/pmc_walk.json,
     TCC_EA0_RDREQ per launch, tools/fold_c2.py) when it was taken at this
@@ -874,7 +1004,7 @@ def make_cshard(tree, world, rank, dist, dev, args, keys_local):
     """The C-ABI shard (sherman_amd.CShard: routed get / insert in C++ over
     its own RCCL communicators) when the backend is nccl and --router allows;
     with "auto" it must first return the Python route's results on one batch
-    of stored keys (every rank agrees, else all fall back)."""
+    of stored keys on every rank, else the run fails."""
     import torch
     import sherman_amd as shm
     from sherman_amd.shard import ShardRouter
@@ -896,9 +1026,10 @@ def make_cshard(tree, world, rank, dist, dev, args, keys_local):
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if int(ok.item()) == 1:
         return cs, "cabi"
-    log("[bench] C-ABI shard route disagreed with the Python route: using Python")
+    # a routing bug must fail the run, not hide behind the slower Python path
     cs.close()
-    return None, "python (C-ABI self-check failed)"
+    raise RuntimeError("C-ABI shard route (shm_shard_search) disagreed with the Python "
+                       "route on a self-check batch of stored keys and misses")
 
 
 def latency_pass(one, args, dist):

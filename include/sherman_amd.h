@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 8
+#define SHM_ABI_VERSION 9
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -275,6 +275,11 @@ typedef struct shm_profile_t {
   uint64_t range_calls;  /* shm_range_query launches timed (count + fill) */
   uint64_t range_queries;/* scans in those launches */
   double range_ms;       /* sum of k_range kernel time */
+  /* the timed insert chunks' work, counted on the device (ABI 9): the
+   * per-touched-leaf algorithmic bytes of bench.py's insert roofline */
+  uint64_t insert_unique;/* unique upserts after the batch's last-writer fold */
+  uint64_t insert_dels;  /* unique deletes */
+  uint64_t insert_staged;/* staged segments: leaves read whole (they get a new key) */
 } shm_profile_t;
 /* on: bit 0 = the event timing above, bit 1 = the index statistics below */
 int shm_profile_enable(shm_tree *t, int on);

@@ -101,11 +101,14 @@ class ShmProfile(ctypes.Structure):
         ("range_calls", u64),
         ("range_queries", u64),
         ("range_ms", ctypes.c_double),
+        ("insert_unique", u64),
+        ("insert_dels", u64),
+        ("insert_staged", u64),
     ]
 
 
 _lib = None
-ABI_VERSION = 8  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 9  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [

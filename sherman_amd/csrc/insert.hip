@@ -220,6 +220,11 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   if (t == 0) s_ndel = *a.n_del;
   __syncthreads();
   const uint64_t n_del = s_ndel;
+  if (a.prof && b == 0 && t == 0) {  // the chunk's counts (profiling)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.prof), (unsigned long long)a.n_del[-1]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.prof) + 1, (unsigned long long)n_del);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.prof) + 2, (unsigned long long)ns);
+  }
   const uint32_t late = ctl->late[par][0];
   // pages the upsert kernel's early splits took from next_page on (theirs
   // come first; failed takes past the capacity used no page)
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   // no split left to k_upper and no delete (C5's chunks once their splits
   // are early): the blocks skip the count scans, block 0 writes the
   // superblock below, and every block only arrives (quick_arrive)
-  const bool quick = a.quick != 0 && late == 0 && n_del == 0 && !a.force_abort;
+  const bool quick = late == 0 && n_del == 0 && !a.force_abort;
   upper_zero_next(ctl, par, tid, T);
   // leaf level: the upsert kernel left per-range new-page / split counts
   __shared__ uint32_t s_pnp[kMaxUpper + 1], s_pns[kMaxUpper + 1];
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       // in the direct path its exclusive word, taken while the leaf pages are
       // built: one atomic whose result is looked at after the builds
       const uint64_t hint1 = direct ? dir_hint_page(a, first_key, 1) : 0ull;
-      const bool pre = direct && !grow0 && !a.no_prelock && hint1 != 0 &&
+      const bool pre = direct && !grow0 && hint1 != 0 &&
                        ptr_ok(hint1, a.node, a.arena_bytes);
       unsigned long long lk_old = ~0ull;
       if (pre && lane == 0)

@@ -269,19 +269,17 @@ struct UpperArgs {
   // hand-off of this launch, as if its wait had timed out (the last block
   // then completes the chunk alone)
   uint32_t force_abort;
-  // diagnostics (SHM_UPPER_LISTS=1 in the environment): never propagate
-  // directly, every chunk through the level lists and grid barriers
+  // diagnostics (shm__upper_force bit 1): never propagate directly, every
+  // chunk through the level lists and their hand-offs
   uint32_t no_direct;
-  // A/B (SHM_UPPER_PRELOCK=0): take the level-1 parent's word only after
-  // the leaf pages are built (round 3's chain) instead of during the builds
-  uint32_t no_prelock;
   // the upsert kernel's copy (upsert.hip): small splits are built and
   // propagated there, their pages counted in UpperCtl.ualloc; 0 in k_upper's
   uint32_t early;
-  // A/B (SHM_UPPER_QUICK): with no split left to k_upper and no delete, 0 =
-  // every block scans the counts as before, 1 = the scans are skipped, 2 =
-  // block 0 alone runs
-  uint32_t quick;
+  // nullable (profiling on): per chunk, {unique upserts, deletes, staged
+  // segments} added by whichever kernel completes the chunk's counts --
+  // k_upper's block 0, or the segmentation's block 0 for a chunk it
+  // completes -- before the op buffers are published free
+  uint64_t* prof;
   // publish the chunk's tag in the host mirror even without new pages (the
   // host's directory is behind the tree and it watches for a quiet tree)
   uint32_t pub_always;

@@ -919,7 +919,7 @@ __device__ __forceinline__ uint32_t split_early(const UpperArgs& a, WaveLds& L,
     ov0 = a.op_val[it.st + lane];
   }
   const u32x4 w = load_page_slice(a.arena, ga_offset(it.page));
-  const bool pre = !a.no_prelock && it.hint1 != 0 && ptr_ok(it.hint1, a.node, a.arena_bytes);
+  const bool pre = it.hint1 != 0 && ptr_ok(it.hint1, a.node, a.arena_bytes);
   unsigned long long lk_old = ~0ull;
   if (pre && lane == 0)
     lk_old = atomicMax(reinterpret_cast<unsigned long long*>(a.locks) +

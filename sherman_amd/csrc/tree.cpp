@@ -141,6 +141,9 @@ struct shm_tree {
   bool top_valid = false;
   // index statistics of the get walk (shm_index_stats), when prof_stats
   uint64_t* idx_stats = nullptr;
+  // per-chunk insert counts while profiling (UpperArgs.prof): unique
+  // upserts, deletes, staged segments
+  uint64_t* prof_ins = nullptr;
   bool prof_stats = false;
   std::mutex mu;
   // profiling (shm_profile_*)
@@ -808,8 +811,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.stamps = t->stamps;
   u.force_abort = (t->force_flags & 1u) ? 1u : 0u;
   u.no_direct = (t->force_flags & 2u) ? 1u : 0u;
-  u.no_prelock = 0;
-  u.quick = 1;
+  u.prof = t->prof_on ? t->prof_ins : nullptr;
   u.pub_always = t->next_page != t->dir_np ? 1u : 0u;
   // small splits built by the upsert kernel itself; the forced k_upper paths
   // (force flags 1, 2, 4) leave them all to k_upper
@@ -817,7 +819,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   ue.early = (t->force_flags & 7u) ? 0u : 1u;
   // a chunk with no new key and no delete is completed by the segmentation
   // kernel's block 0 (u: k_upper's quick path; k_upper then returns at once).
-  const bool quick_ok = u.quick && !u.force_abort;
+  const bool quick_ok = !u.force_abort;
   // force flag bit 3: every tile counts its predecessors itself (the
   // look-back's fallback, exercised by a test)
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
@@ -957,7 +959,7 @@ void free_all(shm_tree* t) {
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
   F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->dir); F(t->dir_hint); F(t->gcount); F(t->bins);
-  F(t->top_keys); F(t->top_pages); F(t->top_scratch); F(t->idx_stats);
+  F(t->top_keys); F(t->top_pages); F(t->top_scratch); F(t->idx_stats); F(t->prof_ins);
   for (auto& r : t->prof_pending)
     for (hipEvent_t e : r.e)
       if (e) t->event_pool.push_back(e);
@@ -1873,6 +1875,10 @@ int shm_profile_enable(shm_tree* t, int on) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   t->prof_on = (on & 1) != 0;
+  if (t->prof_on && !t->prof_ins) {
+    if (dalloc(&t->prof_ins, 4)) return SHM_ENOMEM;
+    HIP_OK(hipMemset(t->prof_ins, 0, sizeof(uint64_t) * 4));
+  }
   const bool st = (on & 2) != 0;
   if (st && !t->idx_stats) {
     if (dalloc(&t->idx_stats, dev::kIdxStats)) return SHM_ENOMEM;
@@ -1906,6 +1912,15 @@ int shm_profile_read(shm_tree* t, shm_profile_t* out, int reset) {
   std::lock_guard<std::mutex> g(t->mu);
   int rc = drain_profile(t);
   if (rc) return rc;
+  if (t->prof_ins) {
+    HIP_OK(hipDeviceSynchronize());
+    uint64_t c[4];
+    HIP_OK(hipMemcpy(c, t->prof_ins, sizeof(c), hipMemcpyDeviceToHost));
+    t->prof_acc.insert_unique = c[0];
+    t->prof_acc.insert_dels = c[1];
+    t->prof_acc.insert_staged = c[2];
+    if (reset) HIP_OK(hipMemset(t->prof_ins, 0, sizeof(c)));
+  }
   *out = t->prof_acc;
   if (reset) t->prof_acc = shm_profile_t{};
   return SHM_OK;

@@ -60,6 +60,8 @@ __device__ __forceinline__ void seg_complete_unchanged(const UpperArgs& q) {
   if (*q.n_del != 0) return;  // the deletes are k_upper's
   upper_zero_next(q.ctl, q.par, threadIdx.x, blockDim.x);
   if (threadIdx.x == 0) {
+    if (q.prof)  // the chunk's unique upserts (profiling; no delete, nothing staged)
+      atomicAdd(reinterpret_cast<unsigned long long*>(q.prof), (unsigned long long)q.n_del[-1]);
     upper_finish_unchanged(q, __hip_atomic_load(q.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     q.ctl->skip[q.par][0] = q.batch;
   }
