@@ -176,37 +176,31 @@ def cap_fracs(d, keys):
 
 
 class Region:
-    """rocprofv3 --selected-regions: collection only between
-    roctxProfilerResume(0) and roctxProfilerPause(0).  SHM_BENCH_REGION names
-    the window a profiling run wants (tools/roofline_pass.sh): "profile" =
-    the roofline pass whose HIP-event times give roofline.achieved, "timed" =
-    the timed steps; unset = no markers."""
+    """The edges of a profiling window: an empty kernel (shm__mark, tag 1 at
+    the start, 2 at the end) whose dispatches tools/fold_roofline.py finds in
+    a kernel trace or a counter collection, keeping only the dispatches
+    between them.  SHM_BENCH_REGION names the window a profiling run wants
+    (tools/roofline_pass.sh): "profile" = the roofline pass whose HIP-event
+    times give roofline.achieved, "timed" = the timed steps; unset = no
+    markers (the device sees nothing extra)."""
 
     def __init__(self):
         self.want = os.environ.get("SHM_BENCH_REGION")
-        self.lib = None
-        if self.want:
-            import ctypes
-            for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
-                         "libroctx64.so.4"):
-                try:
-                    self.lib = ctypes.CDLL(name)
-                    break
-                except OSError:
-                    pass
-            assert self.lib is not None, "SHM_BENCH_REGION set but no roctx library"
-            for f in (self.lib.roctxProfilerResume, self.lib.roctxProfilerPause):
-                f.argtypes, f.restype = [ctypes.c_uint64], None
+
+    def _mark(self, tag):
+        import torch
+        import sherman_amd as shm
+        torch.cuda.synchronize()
+        assert shm._hooks().shm__mark(tag, None) == 0
+        torch.cuda.synchronize()
 
     def begin(self, name):
-        if self.lib is not None and name == self.want:
-            self.lib.roctxProfilerResume(0)
+        if name == self.want:
+            self._mark(1)
 
     def end(self, name):
-        if self.lib is not None and name == self.want:
-            import torch
-            torch.cuda.synchronize()
-            self.lib.roctxProfilerPause(0)
+        if name == self.want:
+            self._mark(2)
 
 
 def log(*a):

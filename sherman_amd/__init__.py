@@ -609,6 +609,7 @@ _HOOKS = [
     ("shm__shard_create_local", ctypes.c_int, [vp, vp, u32, ctypes.POINTER(vp)]),
     ("shm__upper_force", ctypes.c_int, [vp, u32]),
     ("shm__hog", ctypes.c_int, [u32, u64, vp]),
+    ("shm__mark", ctypes.c_int, [u32, vp]),
     ("shm__early_pages", ctypes.c_int, [vp, ctypes.POINTER(u64)]),
 ]
 

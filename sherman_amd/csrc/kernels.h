@@ -299,6 +299,8 @@ void launch_upper(const UpperArgs& a, hipStream_t s);
 // diagnostics (shm__hog): n blocks that each hold a whole CU's LDS and spin
 // until `ticks` of the 100 MHz wall clock have passed since they started
 void launch_hog(uint32_t n, uint64_t ticks, hipStream_t s);
+// diagnostics (shm__mark): an empty kernel marking a profile window's edge
+void launch_mark(uint32_t tag, hipStream_t s);
 
 void launch_empty_leaf(uint8_t* arena, uint64_t page_off, uint8_t* sum, hipStream_t s);
 void launch_write_superblock(uint8_t* arena, const Superblock& sb, hipStream_t s);
@@ -418,18 +420,29 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
 // An overflowed key goes to ovk / ovi (its input position) for the second
 // round; with ovk == nullptr it finds nothing and kErrOverflow goes to *err.
 // The results are gathered back to input order.
+// Own run (own_out non-null): the run of peer `own` (this rank) is written to
+// own_out[0, cap) instead of out[own * cap, ...), i.e. straight into the
+// receive buffer the local get reads, so it never enters the collective
+// (VERDICT r4 #2); spos still names slot own * cap + pos.
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
                         uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
-                        uint32_t* ovi, uint32_t* err, hipStream_t s);
+                        uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own = 0,
+                        uint64_t* own_out = nullptr);
+// out[i] = in[spos[i]]; with own_src non-null, slots of run `own` (own * cap
+// .. + cap) are read from own_src (the local get's results, never exchanged)
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
-                         uint8_t* found, hipStream_t s);
+                         uint8_t* found, hipStream_t s, uint32_t own = 0, uint64_t cap = 0,
+                         const uint64_t* own_src = nullptr);
 // out[ovi[perm[j]]] = in[j], found likewise (the overflow round's results)
 void launch_route_ov_scatter(const uint64_t* in, const uint32_t* perm, const uint32_t* ovi,
                              uint64_t m, uint64_t* out, uint8_t* found, hipStream_t s);
 // routed insert: the bucketed runs (cnt[p] keys of peer p, in order) packed
 // into P slot runs of cap (kKeyMax / 0 padding)
+// (own_k / own_v non-null: run `own` goes there, straight into the receive
+// buffers of the local insert, instead of pk / pv)
 void launch_route_pack(const uint64_t* kb, const uint64_t* vb, const uint64_t* cnt, uint32_t P,
-                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s);
+                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s, uint32_t own = 0,
+                       uint64_t* own_k = nullptr, uint64_t* own_v = nullptr);
 // routed range scans: shard p owns [b[p], b[p + 1]) (P <= 16; b[P] unused)
 struct ShardBounds {
   uint64_t b[17];

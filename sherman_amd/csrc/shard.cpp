@@ -10,11 +10,13 @@
 //
 //   search : every key straight into its owner's run of fixed-capacity
 //            slots (cap = 1.25 n / P + 256, kKeyMax padding; a per-peer
-//            cursor places it, spos records where) -> ncclAllToAll of the
-//            slots and of the per-peer key counts -> local batched get over
-//            all received slots (a kKeyMax finds nothing) -> ncclAllToAll of
-//            the results back -> gather to input order through spos (found
-//            = value != 0, Tree.cpp:445-448).  No host wait before the key
+//            cursor places it, spos records where; this rank's own run is
+//            placed straight into its receive slot) -> grouped ncclSend /
+//            ncclRecv of the P - 1 peers' runs and key counts (nothing at
+//            P = 1) -> local batched get over all received slots (a kKeyMax
+//            finds nothing) -> the peers' results back the same way ->
+//            gather to input order through spos, the own run's results
+//            read in place (found = value != 0, Tree.cpp:445-448).  No host wait before the key
 //            exchange.  A run longer than its slot (keys far from uniform
 //            over the shards, e.g. a zipf hot key) puts the rest of its keys
 //            on an overflow list; end() reads the key counts back once (they
@@ -137,6 +139,9 @@ struct Xport {
   // `count` elements of eb (4 or 8) bytes to and from every peer: peer p's
   // part of send / recv at p * count
   virtual int a2a(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) = 0;
+  // a2a without this rank's own part (it never leaves the rank: the callers
+  // place it straight where the local kernel reads it); nothing at P = 1
+  virtual int a2a_peers(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) = 0;
   // grouped point-to-point: scnt[p] elements at send + soff[p] to peer p,
   // rcnt[p] elements from peer p to recv + roff[p] (both sides know both)
   virtual int p2p(const void* send, const uint64_t* scnt, const uint64_t* soff, void* recv,
@@ -155,6 +160,19 @@ struct RcclXport : Xport {
   int group_end() override { return nccl_ok(ncclGroupEnd(), "ncclGroupEnd"); }
   int a2a(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) override {
     return nccl_ok(ncclAllToAll(send, recv, count, nccl_type(eb), comm, s), "ncclAllToAll");
+  }
+  int a2a_peers(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) override {
+    if (P == 1 || count == 0) return SHM_OK;
+    NCCL_OK(ncclGroupStart());
+    for (uint32_t p = 0; p < P; ++p) {
+      if (p == rank) continue;
+      NCCL_OK(ncclSend(static_cast<const char*>(send) + (uint64_t)p * count * eb, count,
+                       nccl_type(eb), (int)p, comm, s));
+      NCCL_OK(ncclRecv(static_cast<char*>(recv) + (uint64_t)p * count * eb, count, nccl_type(eb),
+                       (int)p, comm, s));
+    }
+    NCCL_OK(ncclGroupEnd());
+    return SHM_OK;
   }
   int p2p(const void* send, const uint64_t* scnt, const uint64_t* soff, void* recv,
           const uint64_t* rcnt, const uint64_t* roff, int eb, hipStream_t s) override {
@@ -264,6 +282,17 @@ struct LocalXport : Xport {
     m.count = count;
     return run(m, s, [&](uint32_t p, const LocalGroup::Post& q) {
       if (!count) return 0;
+      return hipMemcpyAsync(static_cast<char*>(recv) + (uint64_t)p * count * eb,
+                            q.send + (uint64_t)rank * count * eb, count * eb,
+                            hipMemcpyDeviceToDevice, s) != hipSuccess ? 1 : 0;
+    });
+  }
+  int a2a_peers(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) override {
+    LocalGroup::Post m;
+    m.send = static_cast<const char*>(send);
+    m.count = count;
+    return run(m, s, [&](uint32_t p, const LocalGroup::Post& q) {
+      if (!count || p == rank) return 0;
       return hipMemcpyAsync(static_cast<char*>(recv) + (uint64_t)p * count * eb,
                             q.send + (uint64_t)rank * count * eb, count * eb,
                             hipMemcpyDeviceToDevice, s) != hipSuccess ? 1 : 0;
@@ -535,7 +564,8 @@ int flush(shm_shard* h) {
     }
     base += c[p];
     ns += scnt[p];
-    if (c[P + p] > e.icap) rcnt[p] = c[P + p] - e.icap;
+    const uint64_t got = p == h->rank ? c[p] : c[P + p];  // own run: never exchanged
+    if (got > e.icap) rcnt[p] = got - e.icap;
     roff[p] = nr;
     nr += rcnt[p];
   }
@@ -561,7 +591,8 @@ int get_overflow(shm_shard* h, GetSlot& s, uint64_t* vals_out, uint8_t* found_ou
     scnt[p] = w[p] > s.ncap ? w[p] - s.ncap : 0;
     soff[p] = m;
     m += scnt[p];
-    rcnt[p] = w[P + 1 + p] > s.ncap ? w[P + 1 + p] - s.ncap : 0;
+    const uint32_t got = p == h->rank ? w[p] : w[P + 1 + p];  // own run: never exchanged
+    rcnt[p] = got > s.ncap ? got - s.ncap : 0;
     roff[p] = mr;
     mr += rcnt[p];
   }
@@ -654,12 +685,16 @@ int shm_shard_search_begin(shm_shard* h, const uint64_t* keys, uint64_t n, void*
   *ticket = (uint32_t)i;
   const uint32_t P = h->world;
   s.ncap = P == 1 ? n : std::min<uint64_t>(s.pcap, (n + n / 4) / P + 256);
+  // this rank's own run goes straight into its receive slot (s.pr), so only
+  // the P - 1 peers' runs cross the collective (none at P = 1)
+  const uint32_t me = h->rank;
   shm::dev::launch_route_slots(s.keys, s.n, P, s.ncap, s.cw, s.pk, s.spos, s.ovk, s.ovi,
-                               shm__error_word(h->local), s.stream);
+                               shm__error_word(h->local), s.stream, me,
+                               s.pr + (uint64_t)me * s.ncap);
   HIP_OK2(hipGetLastError());
   RC_OK(s.x->group_start());
-  RC_OK(s.x->a2a(s.pk, s.pr, s.ncap, 8, s.stream));
-  RC_OK(s.x->a2a(s.cw, s.cw + P + 1, 1, 4, s.stream));  // keys routed to each peer
+  RC_OK(s.x->a2a_peers(s.pk, s.pr, s.ncap, 8, s.stream));
+  RC_OK(s.x->a2a_peers(s.cw, s.cw + P + 1, 1, 4, s.stream));  // keys routed to each peer
   RC_OK(s.x->group_end());
   HIP_OK2(hipEventRecord(s.ev_keys, s.stream));
   s.busy = true;
@@ -673,9 +708,11 @@ int shm_shard_search_end(shm_shard* h, uint32_t ticket, uint64_t* vals_out, uint
   s.busy = false;
   const uint32_t P = h->world;
   RC_OK(shm_search_batch(h->local, s.pr, (uint64_t)P * s.ncap, s.pv, nullptr, s.stream));
-  // the results go back the way the keys came, slot for slot
-  RC_OK(s.x->a2a(s.pv, s.pb, s.ncap, 8, s.stream));
-  shm::dev::launch_route_gather(s.pb, s.spos, s.n, vals_out, found_out, s.stream);
+  // the results go back the way the keys came, slot for slot; the own run's
+  // are gathered straight from the local results
+  RC_OK(s.x->a2a_peers(s.pv, s.pb, s.ncap, 8, s.stream));
+  shm::dev::launch_route_gather(s.pb, s.spos, s.n, vals_out, found_out, s.stream, h->rank, s.ncap,
+                                s.pv);
   HIP_OK2(hipGetLastError());
   return P == 1 ? SHM_OK : get_overflow(h, s, vals_out, found_out);
 }
@@ -699,12 +736,15 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   // synchronising call), as a local insert rejects its chunk
   RC_OK(shm__route_bucket_insert(h->local, keys, n, P, e.icnt, e.kb, e.perm, s));
   RC_OK(shm_route_permute(h->local, vals, e.perm, n, e.vb, s));
-  shm::dev::launch_route_pack(e.kb, e.vb, e.icnt, P, e.icap, e.pk, e.pv, s);
+  // this rank's own run is packed straight into its receive slot
+  const uint64_t mine = (uint64_t)h->rank * e.icap;
+  shm::dev::launch_route_pack(e.kb, e.vb, e.icnt, P, e.icap, e.pk, e.pv, s, h->rank, e.rk + mine,
+                              e.rv + mine);
   HIP_OK2(hipGetLastError());
   RC_OK(e.x->group_start());
-  RC_OK(e.x->a2a(e.pk, e.rk, e.icap, 8, s));
-  RC_OK(e.x->a2a(e.pv, e.rv, e.icap, 8, s));
-  RC_OK(e.x->a2a(e.icnt, e.icnt + P, 1, 8, s));
+  RC_OK(e.x->a2a_peers(e.pk, e.rk, e.icap, 8, s));
+  RC_OK(e.x->a2a_peers(e.pv, e.rv, e.icap, 8, s));
+  RC_OK(e.x->a2a_peers(e.icnt, e.icnt + P, 1, 8, s));
   RC_OK(e.x->group_end());
   HIP_OK2(hipEventRecord(e.ev_ins, s));
   e.pending = P > 1;

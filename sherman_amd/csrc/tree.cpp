@@ -1736,6 +1736,15 @@ int shm__hog(uint32_t blocks, uint64_t ticks, void* stream) {
   return SHM_OK;
 }
 
+// Diagnostics, not part of include/sherman_amd.h: an empty kernel on
+// `stream` whose dispatch marks the edge of a profiling window (bench.py
+// Region, tools/fold_roofline.py)
+int shm__mark(uint32_t tag, void* stream) {
+  dev::launch_mark(tag, pick(stream));
+  HIP_OK(hipGetLastError());
+  return SHM_OK;
+}
+
 // Diagnostics, not part of include/sherman_amd.h: enable = 1 turns k_upper's
 // phase clock on, 0 off; out (nullable, kUpperStamps words) receives the last
 // chunk's stamps (out[0] = count, then 100 MHz wall-clock values).

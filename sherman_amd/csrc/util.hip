@@ -386,16 +386,19 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
 // results are gathered back from the same places.  cursor[p] ends as the
 // number of keys routed to peer p (a run's overflow included), cursor[P] as
 // the number of overflowed keys.
-__global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t n, uint32_t* cursor,
-                                                   uint32_t P) {
+// kKeyMax padding of the P runs of cap slots (run `own` in own_out when
+// non-null) and the cursors zeroed
+__global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t cap, uint32_t* cursor,
+                                                   uint32_t P, uint32_t own, uint64_t* own_out) {
   const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (i == 0)
     for (uint32_t p = 0; p <= P; ++p) cursor[p] = 0;
-  if (2 * i + 1 < n) {
-    *reinterpret_cast<u32x4*>(out + 2 * i) = u32x4{~0u, ~0u, ~0u, ~0u};
-  } else if (2 * i < n) {
-    out[2 * i] = kKeyMax;
-  }
+  if (i >= (uint64_t)P * cap) return;
+  const uint32_t p = (uint32_t)(i / cap);
+  if (own_out && p == own)
+    own_out[i - (uint64_t)p * cap] = kKeyMax;
+  else
+    out[i] = kKeyMax;
 }
 
 // A block places 4096 keys (16 per thread): per round and wave, ranks among
@@ -414,7 +417,8 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ cursor,
                                                     uint64_t* __restrict__ out,
                                                     uint32_t* __restrict__ spos, uint64_t* ovk,
-                                                    uint32_t* ovi, uint32_t* err) {
+                                                    uint32_t* ovi, uint32_t* err, uint32_t own_p,
+                                                    uint64_t* own_out) {
   constexpr int kW = kT / kWave;
   __shared__ uint32_t wc[kSlotPer][kW][kRouteMaxShards];
   const int t = threadIdx.x, w = t >> 6, lane = lane_id();
@@ -462,7 +466,10 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
       const uint32_t pos = wc[r][w][own[r]] + rank[r];
       if (pos < cap) {
         const uint64_t x = (uint64_t)own[r] * cap + pos;
-        out[x] = kk[r];
+        if (own_out && own[r] == own_p)
+          own_out[pos] = kk[r];  // this rank's run: straight to the local get
+        else
+          out[x] = kk[r];
         spos[i] = (uint32_t)x;
       } else {  // this peer's run is full
         spos[i] = ~0u;
@@ -487,29 +494,35 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
 
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
                         uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
-                        uint32_t* ovi, uint32_t* err, hipStream_t s) {
+                        uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own,
+                        uint64_t* own_out) {
   const uint64_t slots = (uint64_t)P * cap;
-  hipLaunchKernelGGL(k_route_fill, grid1((slots + 1) / 2 + 1), dim3(kT), 0, s, out, slots, cursor,
-                     P);
+  hipLaunchKernelGGL(k_route_fill, grid1(slots + 1), dim3(kT), 0, s, out, cap, cursor, P, own,
+                     own_out);
   if (n)
     hipLaunchKernelGGL(k_route_slots, grid1(n, kSlotTile), dim3(kT), 0, s, keys, n, P, cap, cursor,
-                       out, spos, ovk, ovi, err);
+                       out, spos, ovk, ovi, err, own, own_out);
 }
 
 // out[i] = in[spos[i]] (0 for a key cut by a full run: the overflow round
 // fills it afterwards), found[i] = out[i] != 0 (Tree.cpp:445-448)
 __global__ void k_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n,
-                               uint64_t* out, uint8_t* found) {
+                               uint64_t* out, uint8_t* found, uint64_t own_lo, uint64_t cap,
+                               const uint64_t* own_src) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t x = spos[i];
-  const uint64_t v = x != ~0u ? in[x] : kValueNull;
+  uint64_t v = kValueNull;
+  if (x != ~0u) v = own_src && x - own_lo < cap ? own_src[x] : in[x];
   out[i] = v;
   if (found) found[i] = v != kValueNull ? 1 : 0;
 }
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
-                         uint8_t* found, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_route_gather, grid1(n), dim3(kT), 0, s, in, spos, n, out, found);
+                         uint8_t* found, hipStream_t s, uint32_t own, uint64_t cap,
+                         const uint64_t* own_src) {
+  if (n)
+    hipLaunchKernelGGL(k_route_gather, grid1(n), dim3(kT), 0, s, in, spos, n, out, found,
+                       (uint64_t)own * cap, cap, own_src);
 }
 
 // the overflow round's results: out[ovi[perm[j]]] = in[j] (perm: the
@@ -536,7 +549,8 @@ void launch_route_ov_scatter(const uint64_t* in, const uint32_t* perm, const uin
 // stays in kb / vb for the shard's second round.
 __global__ __launch_bounds__(kT) void k_route_pack(const uint64_t* kb, const uint64_t* vb,
                                                    const uint64_t* cnt, uint32_t P, uint64_t cap,
-                                                   uint64_t* pk, uint64_t* pv) {
+                                                   uint64_t* pk, uint64_t* pv, uint32_t own,
+                                                   uint64_t* own_k, uint64_t* own_v) {
   const uint64_t x = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (x >= (uint64_t)P * cap) return;
   const uint32_t p = (uint32_t)(x / cap);
@@ -544,13 +558,17 @@ __global__ __launch_bounds__(kT) void k_route_pack(const uint64_t* kb, const uin
   uint64_t off = 0;
   for (uint32_t q = 0; q < p; ++q) off += cnt[q];
   const bool real = j < cnt[p];
-  pk[x] = real ? kb[off + j] : kKeyMax;
-  pv[x] = real ? vb[off + j] : kValueNull;
+  const bool mine = own_k && p == own;  // this rank's run: straight to the local insert
+  (mine ? own_k + j : pk + x)[0] = real ? kb[off + j] : kKeyMax;
+  (mine ? own_v + j : pv + x)[0] = real ? vb[off + j] : kValueNull;
 }
 void launch_route_pack(const uint64_t* kb, const uint64_t* vb, const uint64_t* cnt, uint32_t P,
-                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s) {
+                       uint64_t cap, uint64_t* pk, uint64_t* pv, hipStream_t s, uint32_t own,
+                       uint64_t* own_k, uint64_t* own_v) {
   const uint64_t slots = (uint64_t)P * cap;
-  if (slots) hipLaunchKernelGGL(k_route_pack, grid1(slots), dim3(kT), 0, s, kb, vb, cnt, P, cap, pk, pv);
+  if (slots)
+    hipLaunchKernelGGL(k_route_pack, grid1(slots), dim3(kT), 0, s, kb, vb, cnt, P, cap, pk, pv,
+                       own, own_k, own_v);
 }
 
 // ---- routed range scans (shard.cpp shm_shard_range_query) -------------------
@@ -677,6 +695,15 @@ __global__ __launch_bounds__(kT) void k_lock_bench(const uint64_t* keys, uint64_
 void launch_lock_bench(const uint64_t* keys, uint64_t n, uint64_t* locks, uint32_t num_locks,
                        uint64_t tag, uint32_t* err, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_lock_bench, grid1(n), dim3(kT), 0, s, keys, n, locks, num_locks, tag, err);
+}
+
+// ---- diagnostics: a window marker for profiles (shm__mark) -------------------
+// One empty wave whose dispatch names a window's edge in a kernel trace or a
+// counter collection (tools/fold_roofline.py keeps the dispatches between
+// tag 1 and tag 2).
+__global__ void k_mark(uint32_t tag) { (void)tag; }
+void launch_mark(uint32_t tag, hipStream_t s) {
+  hipLaunchKernelGGL(k_mark, dim3(1), dim3(kWave), 0, s, tag);
 }
 
 // ---- diagnostics: a kernel that holds CUs (shm__hog) -----------------------------

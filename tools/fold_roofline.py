@@ -35,10 +35,19 @@ def kname(n):
     return n[5:] if n.startswith("void ") else n
 
 
+def window(rows):
+    """The rows dispatched between the bench's two k_mark dispatches (its
+    Region edges, tag 1 then tag 2), in dispatch order."""
+    rows = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
+    marks = [i for i, r in enumerate(rows) if "k_mark" in r["Kernel_Name"]]
+    assert len(marks) >= 2, "no marked window (SHM_BENCH_REGION unset?)"
+    return rows[marks[0] + 1:marks[1]]
+
+
 def trace(d):
     p = os.path.join(d, "run_kernel_trace.csv")
     agg = collections.defaultdict(lambda: [0, 0])
-    for r in csv.DictReader(open(p)):
+    for r in window(list(csv.DictReader(open(p)))):
         a = agg[kname(r["Kernel_Name"])]
         a[0] += 1
         a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -48,9 +57,9 @@ def trace(d):
 def counter(d, name):
     p = os.path.join(d, "run_counter_collection.csv")
     v = collections.defaultdict(list)
-    for r in csv.DictReader(open(p)):
-        if r["Counter_Name"] == name:
-            v[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    rows = [r for r in csv.DictReader(open(p)) if r["Counter_Name"] == name]
+    for r in window(rows):
+        v[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: (sum(x) / len(x), len(x)) for k, x in v.items()}
 
 
@@ -88,7 +97,7 @@ def main(out, tag, wls):
         ks = kernels(out, w)
         batch = bl["config"]["batch_per_gpu"]
         keys_log2 = bl["config"]["keys_per_gpu"].bit_length() - 1
-        src = "tools/roofline_pass.sh %s (rocprofv3 --selected-regions, bench profile window)" % tag
+        src = "tools/roofline_pass.sh %s (rocprofv3, the bench's marked profile window)" % tag
         if w == "c2":
             k = next(n for n in ks if "k_get_sum" in n)
             e = ks[k]
