@@ -280,6 +280,8 @@ typedef struct shm_profile_t {
   uint64_t insert_unique;/* unique upserts after the batch's last-writer fold */
   uint64_t insert_dels;  /* unique deletes */
   uint64_t insert_staged;/* staged segments: leaves read whole (they get a new key) */
+  double walk_kernel_ms; /* sum of the summary walk's device-clock spans (first block
+                            start to last wave end: the kernel alone, no launch gap) */
 } shm_profile_t;
 /* on: bit 0 = the event timing above, bit 1 = the index statistics below */
 int shm_profile_enable(shm_tree *t, int on);

@@ -104,6 +104,7 @@ class ShmProfile(ctypes.Structure):
         ("insert_unique", u64),
         ("insert_dels", u64),
         ("insert_staged", u64),
+        ("walk_kernel_ms", ctypes.c_double),
     ]
 
 

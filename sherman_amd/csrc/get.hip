@@ -342,6 +342,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
     __syncthreads();
   }
+  if (a.clk && threadIdx.x == 0) a.clk[blockIdx.x] = wall_clock64();
   const bool act = i < a.n;
   const uint64_t k = act ? a.keys[i] : kKeyMax;
   uint64_t val = 0;
@@ -504,14 +505,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
         if (v[j]) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + j), v[j]);
   }
   if (err) atomicOr(a.err, err);
-  if (!act) return;
-  a.out_val[i] = val;
-  if (a.out_found) a.out_found[i] = val != kValueNull ? 1 : 0;
+  if (act) {
+    a.out_val[i] = val;
+    if (a.out_found) a.out_found[i] = val != kValueNull ? 1 : 0;
+  }
+  if (a.clk && lane_id() == 0)
+    a.clk[gridDim.x + blockIdx.x * (TPB / kWave) + (threadIdx.x / kWave)] = wall_clock64();
 }
+
+uint64_t get_sum_blocks(uint64_t n) { return (n + kGetSumTPB - 1) / kGetSumTPB; }
 
 void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s) {
   if (n == 0) return;
-  constexpr int TPB = 256;
+  constexpr int TPB = kGetSumTPB;
   const size_t lds = (size_t)a.top_n * 12;
   hipLaunchKernelGGL(k_get_sum<TPB>, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds, s, a);
 }

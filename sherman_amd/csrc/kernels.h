@@ -64,6 +64,10 @@ struct WalkArgs {
   // GET (k_get_sum), nullable: index statistics (kIdxStats words, added per
   // wave): see IdxStat
   uint64_t* stats;
+  // GET (k_get_sum), nullable (profiling): the launch's device wall clock,
+  // clk[b] = block b's start, clk[gridDim.x + w] = wave w's end (after its
+  // result stores are issued); the host takes last end - first start
+  uint64_t* clk;
 };
 // k_get_sum's index statistics (shm_index_stats)
 enum IdxStat {
@@ -86,6 +90,10 @@ constexpr uint32_t kTopMax = 4096;  // 48 KB of LDS per block
 
 // batched get walk with grouped page resolution (get.hip)
 void launch_get(const WalkArgs& a, uint64_t n, hipStream_t s);
+// k_get_sum's block size, and its blocks for n queries (the profile's clock
+// words: one per block + one per wave, WalkArgs.clk)
+constexpr int kGetSumTPB = 256;
+uint64_t get_sum_blocks(uint64_t n);
 // batched get over the leaf summaries, lane = query (get.hip): directory
 // entry, summary line, matching entries; results in input order
 void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s);

@@ -155,7 +155,16 @@ struct shm_tree {
     hipEvent_t e[4];
     uint64_t n;
     int kind;
+    int clk = -1;         // a get walk's clock slot in prof_clk (k_get_sum), or -1
+    uint64_t blocks = 0;  // its grid
   };
+  // the summary walk's device clock words while profiling (WalkArgs.clk):
+  // kClkSlots launches of (blocks + 4 blocks) words, reused round robin
+  static constexpr int kClkSlots = 16;
+  uint64_t* prof_clk = nullptr;
+  uint64_t clk_words = 0;  // per slot
+  int clk_next = 0, clk_live = 0;
+  double clk_khz = 0.0;
   std::vector<ProfRec> prof_pending;
   std::vector<hipEvent_t> event_pool;
   shm_profile_t prof_acc{};
@@ -608,7 +617,7 @@ hipEvent_t take_event(shm_tree* t) {
 // start a ProfRec with `ne` events, e[0] recorded now on s
 int prof_begin(shm_tree* t, hipStream_t s, int kind, uint64_t n, int ne,
                shm_tree::ProfRec& r) {
-  r = shm_tree::ProfRec{{nullptr, nullptr, nullptr, nullptr}, n, kind};
+  r = shm_tree::ProfRec{{nullptr, nullptr, nullptr, nullptr}, n, kind, -1, 0};
   for (int i = 0; i < ne; ++i) {
     r.e[i] = take_event(t);
     if (!r.e[i]) return SHM_EIO;
@@ -630,6 +639,18 @@ int drain_profile(shm_tree* t) {
       a.queries += r.n;
       a.order_ms += d[0];
       a.walk_ms += d[1];
+      if (r.clk >= 0) {
+        // the walk's own span on the device clock: first block start to last
+        // wave end (what a kernel trace reports, without the launch gap the
+        // events include)
+        std::vector<uint64_t> c(r.blocks * 5);
+        HIP_OK(hipMemcpy(c.data(), t->prof_clk + (uint64_t)r.clk * t->clk_words,
+                         c.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        const uint64_t t0 = *std::min_element(c.begin(), c.begin() + r.blocks);
+        const uint64_t t1 = *std::max_element(c.begin() + r.blocks, c.end());
+        a.walk_kernel_ms += t1 > t0 ? (double)(t1 - t0) / t->clk_khz : 0.0;
+        --t->clk_live;
+      }
     } else if (r.kind == shm_tree::kProfInsert) {
       a.insert_calls += 1;
       a.insert_ops += r.n;
@@ -959,7 +980,7 @@ void free_all(shm_tree* t) {
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
   F(t->part_hist); F(t->part_S); F(t->part_chunks); F(t->dir); F(t->dir_hint); F(t->gcount); F(t->bins);
-  F(t->top_keys); F(t->top_pages); F(t->top_scratch); F(t->idx_stats); F(t->prof_ins);
+  F(t->top_keys); F(t->top_pages); F(t->top_scratch); F(t->idx_stats); F(t->prof_ins); F(t->prof_clk);
   for (auto& r : t->prof_pending)
     for (hipEvent_t e : r.e)
       if (e) t->event_pool.push_back(e);
@@ -1364,6 +1385,10 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     bool gathered = false;
     shm_tree::ProfRec pr{};
     if (t->prof_on) {
+      if (t->clk_live >= shm_tree::kClkSlots) {  // every clock slot holds a record
+        const int rc = drain_profile(t);
+        if (rc) return rc;
+      }
       const int rc = prof_begin(t, s, shm_tree::kProfGet, m, 3, pr);
       if (rc) return rc;
     }
@@ -1396,6 +1421,13 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
     // ordered: the page walk (k_get); unordered: the summary walk (k_get_sum,
     // three lines per get)
+    if (t->prof_on && !gathered && t->prof_clk) {
+      pr.clk = t->clk_next;
+      pr.blocks = dev::get_sum_blocks(m);
+      t->clk_next = (t->clk_next + 1) % shm_tree::kClkSlots;
+      ++t->clk_live;
+      a.clk = t->prof_clk + (uint64_t)pr.clk * t->clk_words;
+    }
     if (gathered)
       dev::launch_get(a, m, s);
     else
@@ -1887,6 +1919,14 @@ int shm_profile_enable(shm_tree* t, int on) {
   if (t->prof_on && !t->prof_ins) {
     if (dalloc(&t->prof_ins, 4)) return SHM_ENOMEM;
     HIP_OK(hipMemset(t->prof_ins, 0, sizeof(uint64_t) * 4));
+  }
+  if (t->prof_on && !t->prof_clk) {
+    t->clk_words = dev::get_sum_blocks(t->nmax) * 5;
+    if (dalloc(&t->prof_clk, t->clk_words * shm_tree::kClkSlots)) return SHM_ENOMEM;
+    int khz = 0, dev_id = 0;
+    HIP_OK(hipGetDevice(&dev_id));
+    HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_id));
+    t->clk_khz = khz > 0 ? (double)khz : 1e5;  // 100 MHz on gfx950
   }
   const bool st = (on & 2) != 0;
   if (st && !t->idx_stats) {
