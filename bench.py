@@ -112,9 +112,9 @@ def parse():
     p.add_argument("--dir-extra-bits", type=int, default=None,
                    help="leaf directory with 2^x entries per tree page (SHM_DIR_EXTRA_BITS)")
     p.add_argument("--order-first", type=int, default=0, choices=(0, 1),
-                   help="c5 slotted scans: 1 = each batch's insert ordering is queued "
-                        "(shm_insert_order) before its scans, its tree changes "
-                        "(shm_insert_apply) after them")
+                   help="c5 slotted scans: 1 = the insert ordering is queued "
+                        "(shm_insert_order) before the step's scans (pipelined: the next "
+                        "batch's), the tree changes (shm_insert_apply) after them")
     p.add_argument("--slot-cap", type=int, default=256,
                    help="c5 slotted scans: values per scan buffer (every timed step is "
                         "checked to have no scan past it)")
@@ -452,13 +452,19 @@ def main():
             if pipe:
                 if ticket[0] is None:  # the first batch of the run
                     ticket[0] = tree.insert_order(pk, pv, stream=s_ord)
+                _, _, nk, nv = mixed[applied[0] % n_c5]  # the next step's batch
+                nxt = None
+                if args.order_first:
+                    # the next batch's ordering queued before this step's scans,
+                    # so it starts with them instead of a host call later
+                    nxt = tree.insert_order(nk, nv, stream=s_ord)
                 sv, sc = sbuf[applied[0] % 2]
                 pr = tree.range_query_slots(lo, hi, args.slot_cap, stream=s_main, vals=sv,
                                             counts=sc, status=slot_status)
                 scan_out["r"] = SlotsResult(pr)
                 scan_out["slots"] = slot_status
-                _, _, nk, nv = mixed[applied[0] % n_c5]  # the next step's batch
-                nxt = tree.insert_order(nk, nv, stream=s_ord)
+                if nxt is None:
+                    nxt = tree.insert_order(nk, nv, stream=s_ord)
                 tree.insert_apply(ticket[0], stream=s_main)
                 ticket[0] = nxt
             elif slots:
