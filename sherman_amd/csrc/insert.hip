@@ -120,23 +120,6 @@ __device__ __forceinline__ void upper_chunk(const UpperArgs& a, WaveLds& L, LvlL
   }
 }
 
-// The quick path's completion: block 0 finishes the chunk alone,
-// but the op buffers (and the ordering's delete count, which each block
-// reads at entry) are free for chunk tag + 2's ordering only once EVERY
-// block has read that count -- a block that started late would otherwise
-// read the next chunk's count and take the full path over its deletes.  So
-// every block arrives on the parity's `done` counter (zeroed by the
-// previous chunk, upper_zero_next) and the last arrival publishes
-// kPubApplied.  Thread 0, after the block's shared read of the count.
-__device__ __forceinline__ uint32_t quick_arrival(const UpperArgs& a) {
-  return __hip_atomic_fetch_add(&a.ctl->done[a.par][0], 1u, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void quick_arrive(const UpperArgs& a, uint32_t nb) {
-  if (threadIdx.x == 0 && quick_arrival(a) == nb - 1 && a.pub)
-    __hip_atomic_store(a.pub + kPubApplied, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // ---------------------------------------------------------------------------
 // k_upper: one launch per insert chunk, one 512-thread block per CU at most;
 // no phase needs the blocks to be resident together (tickets and hand-offs
@@ -212,14 +195,11 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   const uint32_t v_np = (uint32_t)t < nb ? ctl->leaf_np[par][t] : 0u;
   const uint32_t v_ns = (uint32_t)t < nb ? ctl->leaf_ns[par][t] : 0u;
   const uint32_t v_nb = (uint32_t)t < nb ? ctl->leaf_nb[par][t] : 0u;
-  // The delete count is the ordering's (another stream), which may rewrite
-  // it for chunk tag + 2 once the op buffers are published free: one load
-  // per block, shared through LDS, so every wave of the block decides alike
-  // and the block's arrival (quick_arrive) follows the load
-  __shared__ uint64_t s_ndel;
-  if (t == 0) s_ndel = *a.n_del;
-  __syncthreads();
-  const uint64_t n_del = s_ndel;
+  // the delete count: the segmentation kernel's copy in UpperCtl, not the
+  // ordering's count, which chunk tag + 2's ordering (another stream) may
+  // rewrite as soon as block 0 below publishes the op buffers free while
+  // another block of this launch has not started
+  const uint64_t n_del = ctl->ndel[par][0];
   if (a.prof && b == 0 && t == 0) {  // the chunk's counts (profiling)
     atomicAdd(reinterpret_cast<unsigned long long*>(a.prof), (unsigned long long)a.n_del[-1]);
     atomicAdd(reinterpret_cast<unsigned long long*>(a.prof) + 1, (unsigned long long)n_del);
@@ -238,8 +218,8 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
     err0 = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // no split left to k_upper and no delete (C5's chunks once their splits
-  // are early): the blocks skip the count scans, block 0 writes the
-  // superblock below, and every block only arrives (quick_arrive)
+  // are early): the blocks skip the count scans and block 0 alone writes the
+  // superblock below
   const bool quick = late == 0 && n_del == 0 && !a.force_abort;
   upper_zero_next(ctl, par, tid, T);
   // leaf level: the upsert kernel left per-range new-page / split counts
@@ -265,13 +245,10 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
   // early splits' pages and root growth change, so block 0 writes the
   // superblock and no block waits for the others (no fan-in on `done`)
   if (total == 0 && n_del == 0 && !a.force_abort) {
-    if (b != 0) quick_arrive(a, nb);
     if (b == 0 && t == 0) {
-      // the error attribution and the arrival first: no load or returning
-      // atomic after the host mirror's stores (each would wait for their
-      // PCIe writes)
+      // the error attribution first: no load or returning atomic after the
+      // host mirror's stores (each would wait for their PCIe writes)
       if (err0 & ~kErrKeyMax) atomicCAS(a.err + 1, 0u, (uint32_t)a.batch);
-      const bool last_in = quick_arrival(a) == nb - 1;
       if (cursor0e != cursor0) {
         if (rn0 > root_level) root_level = rn0;
         sb->next_page = cursor0e;
@@ -290,9 +267,9 @@ __global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void 
       if (a.pub && (cursor0e != cursor0 || a.pub_always))
         __hip_atomic_store(a.pub + 0, a.batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       sb->batches = a.batch;
-      // no block reads the op buffers on this path; they are free once every
-      // block has read the chunk's counts (the last arrival says so)
-      if (a.pub && last_in)
+      // no block of this launch reads the op buffers or the ordering's
+      // counts on this path
+      if (a.pub)
         __hip_atomic_store(a.pub + kPubApplied, a.batch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }

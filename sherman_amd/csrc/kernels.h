@@ -161,6 +161,12 @@ struct UpperCtl {
   // the tag of a chunk the segmentation kernel completed (no new key, no
   // delete: upper_quick.h); its k_upper returns at once
   uint64_t skip[2][16];
+  // the chunk's delete count, copied from the ordering's counts by the
+  // segmentation kernel's block 0 (k_seg_fill), which runs before anything
+  // publishes the op buffers free; k_upper reads this copy, so no block of
+  // it reads the ordering's count, which chunk tag + 2's ordering may rewrite
+  // once the buffers are published
+  uint64_t ndel[2][16];
 };
 // UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
 // the chunk's op buffers (tree.cpp insert_order's flow control)
@@ -397,7 +403,8 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after);
+                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after,
+                    const uint64_t* ndel_src, uint64_t* ndel_dst);
 // exclusive scan of u64 in one launch (lbw: seg_tiles(n) tagged words, zero
 // at creation; tag: a fresh 16-bit value per call, lbw zeroed again when it
 // wraps); tot = {total, *err} for the range scan's one read-back

@@ -846,7 +846,8 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
                       t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
                       quick_ok ? &u : nullptr, lb_ctr(t, dev::kLbSeg),
-                      (t->force_flags & 8u) ? 0u : kSegSelfAfter);
+                      (t->force_flags & 8u) ? 0u : kSegSelfAfter, cnt + 1,
+                      &t->ctl->ndel[tag & 1u][0]);
   DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};

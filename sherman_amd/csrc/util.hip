@@ -71,7 +71,11 @@ __global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t 
                                                  const uint8_t* pnew, uint32_t tag,
                                                  const uint32_t* any_new, uint32_t* err,
                                                  UpperArgs q, int has_q, uint32_t* ids,
-                                                 uint32_t self_after) {
+                                                 uint32_t self_after, const uint64_t* ndel_src,
+                                                 uint64_t* ndel_dst) {
+  // the chunk's delete count into UpperCtl (k_upper's copy), before anything
+  // of this chunk publishes its op buffers free (below, or k_upper)
+  if (ndel_dst && blockIdx.x == 0 && threadIdx.x == 0) *ndel_dst = *ndel_src;
   if (any_new && *any_new != tag) {  // no op of this chunk marked a page (every block)
     if (blockIdx.x == 0) {
       if (threadIdx.x == 0) *num_seg = 0;
@@ -93,13 +97,15 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
                     uint32_t* seg_start, uint32_t* seg_end, uint64_t* seg_page,
                     uint32_t* num_seg, const uint8_t* pnew, uint32_t tag,
                     const uint32_t* any_new, uint32_t* err, hipStream_t s,
-                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after) {
-  if (!n) return;
+                    const UpperArgs* quick, uint32_t* ids, uint32_t self_after,
+                    const uint64_t* ndel_src, uint64_t* ndel_dst) {
   const UpperArgs q = quick ? *quick : UpperArgs{};
   const int has_q = quick && any_new ? 1 : 0;
-  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)seg_tiles(n)), dim3(kT), 0, s, page, n, n_dev,
-                     lbw, seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q,
-                     has_q, ids, self_after);
+  // at least one block: block 0 copies the delete count even for no ops
+  const uint64_t tiles = n ? seg_tiles(n) : 1;
+  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)tiles), dim3(kT), 0, s, page, n, n_dev, lbw,
+                     seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q, has_q, ids,
+                     self_after, ndel_src, ndel_dst);
 }
 
 // Exclusive scan of u64 counts in one launch: every 1024-element tile

@@ -7,10 +7,11 @@
   must be the same: oracle contents;
 * a C5-shaped chunk stream (new keys with small splits, deletes, range scans
   between) while another process holds 240 of the 256 CUs;
-* k_upper's quick path (no split left to it, no delete): the op buffers are
-  published free only after every block has read the ordering's delete
-  count, so a pipelined ordering of chunk tag + 2 with
-  deletes cannot be read by a late block of chunk tag.
+* k_upper's quick path (no split left to it, no delete): block 0 publishes
+  the op buffers free while other blocks may not have started, so no block
+  reads the ordering's delete count -- they read the segmentation kernel's
+  copy (UpperCtl.ndel) -- and a pipelined ordering of chunk tag + 2 with
+  deletes cannot be read by a late block of chunk tag (ADVICE r4 high).
 
 Reference: every wait in the reference is on a lock a running thread holds
 (src/Tree.cpp:205-242); batch semantics as in SURVEY §8a.
@@ -164,7 +165,7 @@ def test_c5_chunks_beside_cu_hog(lib_ok):
     t.close()
 
 
-def test_quick_path_publishes_after_every_block_read_its_counts(lib_ok):
+def test_quick_path_late_blocks_read_their_own_delete_count(lib_ok):
     """Pipelined chunks (shm_insert_order on one stream, shm_insert_apply on
     another) that alternate quick-path chunks -- new keys into leaves with
     room or small early splits, no delete, so k_upper only completes them --
