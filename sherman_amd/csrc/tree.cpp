@@ -388,7 +388,6 @@ void publish_host(shm_tree* t) {
 // (C2) then runs on an exact directory, with no B-link right moves left
 // from the pages the last 1/32 of growth split (0.039 per get at C2 before
 // this rule: each one a header and a summary read)
-// (SHM_DIR_READ_PHASE=0: only the growth rule, the A/B)
 constexpr uint32_t kReadPhase = 4;
 // ... and likewise once the tree has gone quiet: the mirror showed
 // kQuietChunks newer chunk tags in a row with the same page count (updates
@@ -399,25 +398,39 @@ constexpr uint32_t kReadPhase = 4;
 // load's last rebuild fell early).  A mirror that merely lags (the host ahead
 // of the device) shows no newer tag, so it never looks quiet
 constexpr uint32_t kQuietChunks = 2;
+
+// Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS
+// overrides both): four 64 B entries per page while the tree is written, so
+// ~76 % of C2's gets find their prefix inside one leaf and are answered from
+// the entry's fingerprints (DESIGN §3 "Fingerprints in the directory";
+// round 4: C2 17803 -> 17978 Mops/s against two per page, C3 / C5
+// unchanged), and eight in a read phase (86 % from the fingerprints, 1 GB at
+// C2's 2^26 keys): round-5 same-box A/B C2 19168 / 19182 -> 19416 / 19379
+// Mops/s, while C3 / C5 (written every step, never in a read phase) measured
+// -7 % to +1 % with eight, so they keep four
+uint32_t dir_extra_bits(bool read_phase) {
+  static const int env = [] {
+    const char* e = getenv("SHM_DIR_EXTRA_BITS");
+    return e ? atoi(e) : -1;
+  }();
+  const int v = env >= 0 ? env : read_phase ? 3 : 2;
+  return (uint32_t)(v > 3 ? 3 : v);
+}
+bool read_phase(const shm_tree* t) { return t->reads_since_write >= kReadPhase; }
+uint32_t dir_bits_for(const shm_tree* t, bool rp) {
+  uint32_t bits = 10;
+  while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
+  bits += dir_extra_bits(rp);
+  if (bits > 25) bits = 25;  // 2 GB of entries at most
+  if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
+  return bits;
+}
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
-  return t->next_page != t->dir_np &&
-         (t->reads_since_write >= kReadPhase || t->quiet_chunks >= kQuietChunks);
-}
-
-// Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS,
-// default 2: four 64 B entries per page, so ~76 % of C2's gets find their
-// prefix inside one leaf and are answered from the entry's fingerprints;
-// DESIGN §3 "Fingerprints in the directory".  Round 4, once ties no longer
-// started left: C2 17803 -> 17978 Mops/s over four paired runs against two
-// entries per page, C3 / C5 unchanged; 512 MB at C2's 2^26 keys)
-uint32_t dir_extra_bits() {
-  static const uint32_t x = [] {
-    const char* e = getenv("SHM_DIR_EXTRA_BITS");
-    const int v = e ? atoi(e) : 2;
-    return (uint32_t)(v < 0 ? 0 : v > 3 ? 3 : v);
-  }();
-  return x;
+  const bool rp = read_phase(t);
+  // a read phase also wants its denser directory, once
+  if (rp && t->dir_bits < dir_bits_for(t, true)) return true;
+  return t->next_page != t->dir_np && (rp || t->quiet_chunks >= kQuietChunks);
 }
 
 // The look-back kernels' block-index counters (lookback_index): the
@@ -442,11 +455,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
     fprintf(stderr, "sherman_amd: leaf directory rebuild: pages %llu (last build %llu), %u reads "
             "since the last insert\n", (unsigned long long)t->next_page,
             (unsigned long long)t->dir_np, t->reads_since_write);
-  uint32_t bits = 10;
-  while (bits < 24 && (1ull << bits) < t->next_page) ++bits;
-  bits += dir_extra_bits();
-  if (bits > 25) bits = 25;  // 2 GB of entries at most
-  if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
+  const uint32_t bits = dir_bits_for(t, read_phase(t));
   if (!t->dir || bits != t->dir_bits) {
     if (t->dir) {
       HIP_OK(hipStreamSynchronize(s));
