@@ -115,6 +115,13 @@ def parse():
                    help="c5 slotted scans: 1 = the insert ordering is queued "
                         "(shm_insert_order) before the step's scans (pipelined: the next "
                         "batch's), the tree changes (shm_insert_apply) after them")
+    p.add_argument("--order-cus", type=int, default=0,
+                   help="c3 / c5 pipelined: the insert ordering's stream is confined to "
+                        "this many CUs (hipExtStreamCreateWithCUMask; 0 = all), so the "
+                        "ordering of the next chunk leaves the rest to the step's chain")
+    p.add_argument("--order-cu-mode", choices=("low", "spread"), default="spread",
+                   help="which CUs --order-cus takes: the lowest mask bits, or every "
+                        "(total / n)-th bit")
     p.add_argument("--slot-cap", type=int, default=256,
                    help="c5 slotted scans: values per scan buffer (every timed step is "
                         "checked to have no scan past it)")
@@ -201,6 +208,26 @@ class Region:
     def end(self, name):
         if name == self.want:
             self._mark(2)
+
+
+def cu_masked_stream(n, mode, dev):
+    """A torch stream on its own HIP queue restricted to n CUs (the insert
+    ordering beside the step's chain, --order-cus)."""
+    import ctypes
+    import torch
+    props = torch.cuda.get_device_properties(dev)
+    total = props.multi_processor_count
+    n = max(1, min(n, total))
+    bits = list(range(n)) if mode == "low" else [int(i * total / n) for i in range(n)]
+    words = [0] * ((total + 31) // 32)
+    for b in bits:
+        words[b // 32] |= 1 << (b % 32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    h = ctypes.c_void_p()
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
+    assert rc == 0, f"hipExtStreamCreateWithCUMask failed ({rc})"
+    return torch.cuda.ExternalStream(h.value, device=dev)
 
 
 def log(*a):
@@ -424,7 +451,8 @@ def main():
             # tree changes when pipelined) at high priority, so the ordering
             # beside it takes the CUs it leaves
             s_scan = torch.cuda.Stream(priority=-1 if args.prio else 0)
-            s_ins = torch.cuda.Stream()
+            s_ins = (cu_masked_stream(args.order_cus, args.order_cu_mode, dev) if args.order_cus
+                     else torch.cuda.Stream())
             s_scan.wait_stream(torch.cuda.current_stream())
             s_ins.wait_stream(torch.cuda.current_stream())
 
@@ -528,7 +556,8 @@ def main():
             # gets and tree changes on one stream, the orderings on their own:
             # batch i + 1 is ordered while batch i's gets and inserts run
             c3_main = torch.cuda.Stream(priority=-1 if args.prio else 0)
-            c3_ord = torch.cuda.Stream()
+            c3_ord = (cu_masked_stream(args.order_cus, args.order_cu_mode, dev) if args.order_cus
+                      else torch.cuda.Stream())
             c3_main.wait_stream(torch.cuda.current_stream())
             c3_ord.wait_stream(torch.cuda.current_stream())
 
