@@ -64,8 +64,10 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
   if (a.dir && a.target_level == 0) {
     u32x4 e[4];
     bool fpform;
-    ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform,
-                      match ? &alt : nullptr);
+    // (alt's address is always passed: a pointer chosen at run time kept it
+    // in scratch memory, a store and a load on every op's path)
+    ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform, &alt);
+    if (!match) alt = 0;
     if (match && fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
       // the prefix lies in one leaf and the entry holds its fingerprints: an
       // op whose key that leaf holds updates it without the summary line (a
