@@ -2,6 +2,9 @@
 // segments: runs of ops on one page that gets a new key): k_seg_fill's body
 // (util.hip, one tile per block), kept apart for a kernel that lists its own
 // segments (fusing the segmentation into the upsert kernel).
+// (Round 5 measured a one-wave tile, 16 ops per lane at 32 VGPRs: 23.6
+// against 13.5 us alone in C5's profile window, and no better beside the
+// ordering, 32-33 us either way; the 256-thread tile stays.)
 #pragma once
 #include "device_common.h"
 #include "kernels.h"
@@ -10,16 +13,37 @@ namespace shm {
 namespace dev {
 namespace segt {
 
-// One tile = one wave (round 5): 1024 ops, 16 consecutive ops per lane,
-// streamed in two passes at 32 VGPRs.  A 256-thread block per tile made
-// k_seg_fill 4096 waves per C5 chunk; beside the next chunk's k_bin_unique
-// (one 16-wave block per CU, 152 KB of LDS, 111 VGPRs: 448 of a SIMD's 512
-// VGPRs) one 40-VGPR wave per SIMD fit, so the tiles ran in four rounds
-// (30 us in the timed steps against 13.5 alone).  1024 one-wave tiles of 32
-// VGPRs fit two per SIMD beside it, and a wave needs no block barrier.
-constexpr int kT = kWave;                     // threads per block: one wave
-constexpr int kPer = (int)kSegTile / kT;      // consecutive ops per lane
+constexpr int kT = 256;                       // threads per block
+constexpr int kPer = (int)kSegTile / kT;      // consecutive ops per thread
 static_assert(kPer * kT == (int)kSegTile, "tile shape");
+
+// exclusive scan of v over the block's 256 threads; *total = the block sum
+template <class T>
+__device__ __forceinline__ T block_scan(T v, T* total) {
+  __shared__ T ws[kT / kWave];
+  T incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const T y = __shfl_up(incl, off);
+    if (lane_id() >= off) incl += y;
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == kWave - 1) ws[w] = incl;
+  __syncthreads();
+  T base = 0, sum = 0;
+#pragma unroll
+  for (int i = 0; i < kT / kWave; ++i) {
+    base += i < w ? ws[i] : T(0);
+    sum += ws[i];
+  }
+  __syncthreads();
+  *total = sum;
+  return base + incl - v;
+}
+
+__device__ __forceinline__ uint32_t seg_head(const uint64_t* page, uint64_t i, uint64_t nv) {
+  return i < nv && (i == 0 || page[i] != page[i - 1]) ? 1u : 0u;
+}
 
 // Only segments whose page gets a new key (pnew[page] == new_mark(tag), set by
 // k_locate) need the upsert and split kernels: the others were applied in
@@ -28,8 +52,9 @@ __device__ __forceinline__ bool page_new(const uint8_t* pnew, uint64_t pg, uint3
   return pnew[ga_offset(pg) >> 10] == new_mark(tag);
 }
 
-// The staged heads of tile x, counted by one lane (seg_tile's fallback):
-// the same count tile x publishes, from the same ops and page marks.
+// The staged heads of tile x, counted by one thread (seg_tile's fallback):
+// the same count tile x publishes, from the same ops and page marks.  A
+// plain loop: an unrolled or non-inlined form cost the tile kernel 20 VGPRs.
 __device__ __forceinline__ uint32_t tile_heads(const uint64_t* page, uint64_t nv, uint64_t x,
                                                const uint8_t* pnew, uint32_t tag) {
   const uint64_t s0 = x * kSegTile;
@@ -45,12 +70,11 @@ __device__ __forceinline__ uint32_t tile_heads(const uint64_t* page, uint64_t nv
   return c;
 }
 
-// Tile b (one wave): count its staged heads (a staged head is an op whose
-// page differs from the previous op's and is marked new), publish the count
-// in its tagged word (chunk tag << 32 | count), sum the words of the tiles
-// before it, and fill its segments: seg_start / seg_page at each staged
-// head, seg_end at its run's last op + 1 (the run may end in the next tile:
-// read, not waited for), and the total at the lane holding the last op.
+// Tile b (whole block): count its staged heads, publish the count in its
+// tagged word (chunk tag << 32 | count), sum the words of the tiles before it,
+// and fill its segments: seg_start / seg_page at each staged head, seg_end at
+// its run's last op + 1 (the run may end in the next tile: read, not waited
+// for), and the total at the thread holding the last op.
 // Forward progress: a tile waits for an earlier
 // tile's word at most `self_after` polls and then counts that tile's staged
 // heads itself (tile_heads), so a tile whose block is not placed -- other
@@ -61,36 +85,23 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
                                          uint64_t* lbw, uint32_t* seg_start, uint32_t* seg_end,
                                          uint64_t* seg_page, uint32_t* num_seg,
                                          const uint8_t* pnew, uint32_t tag, uint32_t self_after) {
-  const int lane = lane_id();
-  const uint64_t t0 = b * kSegTile;
-  const uint64_t i0 = t0 + (uint64_t)lane * kPer;
-  // pass 1: this lane's 16 ops, streamed (few registers: the tile must fit
-  // beside the ordering's blocks, see kT): staged heads as bits of hm
-  uint64_t prev = i0 > 0 && i0 - 1 < nv ? page[i0 - 1] : ~0ull;
-  uint32_t hm = 0, c = 0;
-#pragma unroll 2
-  for (int j = 0; j < kPer; ++j) {
-    const uint64_t i = i0 + j;
-    const uint64_t cur = i < nv ? page[i] : ~0ull;
-    if (i < nv && (i == 0 || cur != prev) && page_new(pnew, cur, tag)) {
-      hm |= 1u << j;
-      ++c;
-    }
-    prev = cur;
-  }
-  // the wave's exclusive scan of the lanes' counts
-  uint32_t incl = c;
+  __shared__ uint32_t s_pre[kT / kWave];
+  const uint64_t i0 = b * kSegTile + (uint64_t)threadIdx.x * kPer;
+  uint32_t h[kPer], c = 0;
 #pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
-    if (lane >= off) incl += y;
+  for (int j = 0; j < kPer; ++j) {
+    h[j] = seg_head(page, i0 + j, nv);
+    if (h[j]) h[j] = page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
+    c += h[j];
   }
-  const uint32_t total = (uint32_t)__shfl((int)incl, kWave - 1);
+  uint32_t total;
+  const uint32_t local = block_scan<uint32_t>(c, &total);
   const uint64_t tg = (uint64_t)tag << 32;
-  if (lane == 0) __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the counts of the tiles before this one
   uint32_t v = 0;
-  for (uint64_t x = (uint64_t)lane; x < b; x += kWave) {
+  for (uint64_t x = threadIdx.x; x < b; x += kT) {
     uint64_t w = 0;
     for (uint32_t spin = 0;; ++spin) {
       if (spin >= self_after) {
@@ -105,26 +116,26 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   }
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  // pass 2: the lane's segments (its pages again, from the cache): seg_start
-  // / seg_page at each staged head, seg_end at each run end whose page is new
-  uint32_t pos = v + incl - c;
-  uint64_t cur = i0 < nv ? page[i0] : ~0ull;
-#pragma unroll 2
+  if (lane_id() == 0) s_pre[threadIdx.x / kWave] = v;
+  __syncthreads();
+  uint32_t pos = local;
+#pragma unroll
+  for (int w = 0; w < kT / kWave; ++w) pos += s_pre[w];
+#pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint64_t i = i0 + j;
     if (i >= nv) break;
-    const uint64_t nx = i + 1 < nv ? page[i + 1] : ~0ull;
-    const bool h = (hm >> j) & 1u;
-    if (h) {
+    const uint64_t pg = page[i];
+    if (h[j]) {
       seg_start[pos] = (uint32_t)i;
-      seg_page[pos] = cur;
+      seg_page[pos] = pg;
     }
-    pos += h ? 1u : 0u;
-    const bool tail = i + 1 == nv || nx != cur;
-    if (tail && (h || page_new(pnew, cur, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
+    pos += h[j];
+    const bool tail = i + 1 == nv || page[i + 1] != pg;
+    if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
     if (i + 1 == nv) *num_seg = pos;
-    cur = nx;
   }
+  __syncthreads();  // s_pre and the scan's words are reused by the next tile
 }
 
 }  // namespace segt

@@ -64,7 +64,7 @@ __device__ __forceinline__ T block_scan(T v, T* total) {
 // last op (the count of staged heads up to and including that op is the
 // segment's position + 1).
 
-__global__ __launch_bounds__(segt::kT) void k_seg_fill(const uint64_t* page, uint64_t n,
+__global__ __launch_bounds__(kT) void k_seg_fill(const uint64_t* page, uint64_t n,
                                                  const uint64_t* n_dev, uint64_t* lbw,
                                                  uint32_t* seg_start, uint32_t* seg_end,
                                                  uint64_t* seg_page, uint32_t* num_seg,
@@ -103,7 +103,7 @@ void launch_segment(const uint64_t* page, uint64_t n, const uint64_t* n_dev, uin
   const int has_q = quick && any_new ? 1 : 0;
   // at least one block: block 0 copies the delete count even for no ops
   const uint64_t tiles = n ? seg_tiles(n) : 1;
-  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)tiles), dim3(segt::kT), 0, s, page, n, n_dev, lbw,
+  hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)tiles), dim3(kT), 0, s, page, n, n_dev, lbw,
                      seg_start, seg_end, seg_page, num_seg, pnew, tag, any_new, err, q, has_q, ids,
                      self_after, ndel_src, ndel_dst);
 }

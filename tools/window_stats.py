@@ -14,7 +14,8 @@ agg = collections.defaultdict(list)
 for r in w:
     agg[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(
         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-steps = max((len(v) for k, v in agg.items() if "k_upper" in k), default=1)
+steps = max((len(v) for k, v in agg.items() if "k_upper" in k),
+            default=max(len(v) for v in agg.values()))
 print(f"window {span:.1f} us, {steps} steps, {span / steps:.1f} us/step")
 for k, v in sorted(agg.items(), key=lambda x: -sum(x[1])):
     print(f"{k[:44]:44s} {len(v):5d} {sum(v) / len(v):8.2f} us  {sum(v) / steps:8.2f} us/step")
