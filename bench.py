@@ -115,6 +115,9 @@ def parse():
                    help="c5 slotted scans: 1 = the insert ordering is queued "
                         "(shm_insert_order) before the step's scans (pipelined: the next "
                         "batch's), the tree changes (shm_insert_apply) after them")
+    p.add_argument("--order-sync", type=int, default=0, choices=(0, 1),
+                   help="c5 pipelined: 1 = the step's tree phase waits for the next chunk's "
+                        "ordering (an event), so the ordering overlaps the scans only")
     p.add_argument("--order-cus", type=int, default=0,
                    help="c3 / c5 pipelined: the insert ordering's stream is confined to "
                         "this many CUs (hipExtStreamCreateWithCUMask; 0 = all), so the "
@@ -493,6 +496,12 @@ def main():
                 scan_out["slots"] = slot_status
                 if nxt is None:
                     nxt = tree.insert_order(nk, nv, stream=s_ord)
+                if args.order_sync:
+                    # the tree phase waits for the next chunk's ordering, so the
+                    # ordering runs beside the scans only, not beside the chain
+                    ev = torch.cuda.Event()
+                    ev.record(s_ord)
+                    s_main.wait_event(ev)
                 tree.insert_apply(ticket[0], stream=s_main)
                 ticket[0] = nxt
             elif slots:
