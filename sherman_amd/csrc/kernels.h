@@ -513,10 +513,6 @@ struct RangeArgs {
   // slotted scans (shm_range_query_slots, nullable): += scans whose count
   // passed stage_cap, |= this launch's error bits (the caller zeroes them)
   uint64_t* status;
-  // leaves a scan warms in L2 ahead of its sibling chain (range.hip, with a
-  // directory): the leaves the directory names for `hints` keys spread over
-  // (lo, hi]; 0 = none, at most 3
-  uint32_t hints;
 };
 void launch_range(const RangeArgs& a, hipStream_t s);
 // x[i] += c for i < n

@@ -32,7 +32,6 @@ constexpr int kRL = kWave / kRG;              // lanes per scan
 constexpr int kRE = 4;                        // leaf entries per lane
 constexpr int kRCD = kLeafEntry * kRE / 4;    // dwords of a lane's entry chunk
 constexpr int kRChunks = kPageSize / 16 / kRL;  // 16 B page chunks per lane
-constexpr int kMaxHints = 3;                  // RangeArgs.hints <= 3
 static_assert(kRL * kRE >= kLeafCardinality, "entries per group");
 
 struct RPage {
@@ -103,16 +102,6 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
   uint64_t p = 0;
   int hops = 0;
   uint32_t hw = kLeafCardinality;  // slots of the current leaf that may be valid
-  // L2 warm-up hints: lanes 1..hints of the group ask the directory for the
-  // leaf holding key lo + (hi - lo) * li / (hints + 1) (requested together
-  // with lo's entry, so no round trip is added)
-  const bool hinting = act && a.dir && a.hints && hi > lo;
-  uint64_t hp = 0;
-  if (hinting && li >= 1 && li <= (int)a.hints) {
-    const uint64_t hk = lo + (uint64_t)(((unsigned __int128)(hi - lo) * (unsigned)li) /
-                                        (a.hints + 1u));
-    hp = dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, hk, 0);
-  }
   if (act) {
     p = a.dir ? dir_start(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, lo, a.root) : a.root;
     if (!ptr_ok(p, a.node, a.arena_bytes)) {
@@ -127,33 +116,6 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
       hw = h < (uint32_t)kLeafCardinality ? h : (uint32_t)kLeafCardinality;
     } else {
       rload(a.arena, p, li, w);
-    }
-  }
-  // ... then the first 768 B (six 128 B lines) of each hinted leaf are
-  // touched, issued after lo's leaf: they complete beside it, and the
-  // sibling chain below finds those lines in L2 (the chain stays the
-  // authority: a stale, repeated or wrong hint costs only its loads).  The
-  // touched words are folded into `sink`, consumed at the end, so the loads
-  // stay in flight meanwhile.
-  uint32_t sink = 0;
-  {
-    // every lane: its group's hinted pages (shuffles with the whole wave
-    // active; lane li takes touches li and li + 16 of the 6 x kMaxHints)
-    const int g0 = lane_id() - li;
-    uint64_t hpg[kMaxHints];
-#pragma unroll
-    for (int h = 0; h < kMaxHints; ++h) hpg[h] = shfl64(hp, g0 + 1 + h);
-    if (hinting) {
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const uint32_t j = (uint32_t)li + (uint32_t)(r * kRL);
-        if (j < 6u * a.hints) {
-          const uint32_t h = j / 6;
-          const uint64_t pg = h == 0 ? hpg[0] : h == 1 ? hpg[1] : hpg[2];
-          if (pg != p && ptr_ok(pg, a.node, a.arena_bytes))
-            sink ^= *reinterpret_cast<const uint32_t*>(a.arena + ga_offset(pg) + 128 * (j % 6));
-        }
-      }
     }
   }
   bool desc = act;
@@ -269,7 +231,6 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
       }
     }
   }
-  if (a.n == 0) err |= sink;  // never (a launch has scans): keeps the touches
   return cnt;
 }
 

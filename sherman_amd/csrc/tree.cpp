@@ -1109,11 +1109,6 @@ dev::RangeArgs range_args(shm_tree* t, const uint64_t* from, const uint64_t* to,
   a.vals_cap = ~0ull;
   a.leaf_hw = t->leaf_hw;
   set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
-  static const uint32_t hints = [] {  // A/B (round 5), to be fixed once measured
-    const char* e = getenv("SHM_RANGE_HINTS");
-    return e ? (uint32_t)atoi(e) : 3u;
-  }();
-  a.hints = hints > 3 ? 3 : hints;
   return a;
 }
 
