@@ -33,6 +33,8 @@
 #include "lds_dma.h"
 #include "leaf_chunk.h"
 #include "split_wave.h"
+#include "seg_tile.h"
+#include "upper_quick.h"
 
 namespace shm {
 namespace dev {
@@ -408,6 +410,72 @@ __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperA
   return err;
 }
 
+// Fused segmentation (a.fused, round 5): the chunk's staged segments listed
+// by this kernel before it applies them, so the chain has no k_seg_fill
+// launch (one dependent launch, ~3-4 us per chunk).  Every block first
+// claims 1024-op tiles by ticket (seg_tile.h: count, publish, look back,
+// fill; a tile waits only on tiles of smaller index, all claimed earlier by
+// running blocks, and recounts a late one itself), counts each finished tile
+// once its records are written back, and, with no tile left to claim, waits
+// until every tile is counted -- every tile is held by a running block, so
+// the wait ends (bounded: kErrSegSpin).  A chunk with no new key is
+// completed by block 0 (upper_quick.h) and every block returns.
+constexpr uint32_t kFusedSpins = 1u << 20;
+__device__ __forceinline__ uint32_t fused_segments(const SegArgs& a, const UpperArgs& u) {
+  __shared__ uint32_t s_tile, s_ns;
+  // the chunk's delete count for k_upper, before anything publishes the op
+  // buffers free (upper_quick.h below, or k_upper)
+  if (a.ndel_dst && blockIdx.x == 0 && threadIdx.x == 0) *a.ndel_dst = *a.ndel_src;
+  if (a.any_new && *a.any_new != a.seg_tag) {  // no op of the chunk is new: nothing staged
+    if (blockIdx.x == 0) {
+      if (threadIdx.x == 0) *a.num_seg_w = 0;
+      if (a.quick_ok) seg_complete_unchanged(u);
+    }
+    return 0;
+  }
+  const uint64_t nv = a.n_dev ? *a.n_dev : a.n_ops;
+  const uint64_t ntiles = (nv + kSegTile - 1) / kSegTile;
+  uint32_t* tk = &a.ctl->seg_tk[a.par][0];
+  uint32_t* dn = &a.ctl->seg_dn[a.par][0];
+  for (;;) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(tk, 1u);
+    __syncthreads();
+    const uint64_t tt = s_tile;
+    __syncthreads();
+    if (tt >= ntiles) break;
+    segt::seg_tile(a.op_page, nv, tt, a.lbw, a.seg_start_w, a.seg_end_w, a.seg_page_w,
+                   a.num_seg_w, a.pnew, a.seg_tag, a.self_after);
+    // every thread's records performed, then the tile counts as finished
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // the write-back performed before the count (the compiler may drop the
+      // fence's own wait: MI355X_MICROARCH.md "Compiler hazard")
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint32_t spin = 0;
+    while (__hip_atomic_load(dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
+      if (++spin > kFusedSpins) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    uint32_t ns = 0;
+    if (spin > kFusedSpins)
+      atomicOr(a.err, kErrSegSpin);
+    else if (ntiles)
+      ns = __hip_atomic_load(a.num_seg_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (blockIdx.x == 0)
+      *a.num_seg_w = 0;  // no op: k_upper reads the count
+    s_ns = ns;
+  }
+  __syncthreads();
+  return s_ns;
+}
+
 // Early splits (u.early): a segment that would split into at most
 // kSmallSplit pages is queued in the block's LDS queue instead of being left
 // to k_upper, and a wave of the same block builds it and takes its separators
@@ -426,7 +494,12 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t num_seg = *a.num_seg_dev;
+  uint32_t num_seg;
+  if (a.fused) {
+    num_seg = fused_segments(a, u);
+  } else {
+    num_seg = *a.num_seg_dev;
+  }
   if (num_seg == 0) return;  // every op applied in place (C3's chunks): the block's only load
   const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
   // early splits need a root above the leaves (a leaf root grows the tree:
@@ -489,7 +562,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a, UpperArg
 
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
   constexpr int G = 4;
-  if (!a.num_seg) return;
+  if (!a.num_seg && !a.fused) return;
   static unsigned nb = 0;
   if (!nb) {
     int per_cu = 0, cus = 0, dev = 0;
@@ -499,7 +572,8 @@ void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
     nb = (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
   }
   const uint64_t groups = (a.num_seg + G - 1) / G;
-  const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+  uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (a.fused && need == 0) need = 1;  // block 0 copies the delete count
   hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, nb)), dim3(kBlock),
                      0, s, a, u);
 }
