@@ -5,6 +5,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+assert torch.cuda.is_available()
 import sherman_amd as shm  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
