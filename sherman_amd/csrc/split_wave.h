@@ -386,7 +386,7 @@ __device__ __forceinline__ uint32_t block_claim(uint32_t* tk, uint32_t* slot) {
   __syncthreads();  // every thread has read the previous ticket
   if (threadIdx.x == 0) *slot = atomicAdd(tk, 1u);
   __syncthreads();
-  return *slot;
+  return __builtin_amdgcn_readfirstlane(*slot);  // uniform: loops over it stay single loops
 }
 
 constexpr uint32_t kHandoffSpins = 1u << 22;

@@ -433,14 +433,21 @@ __device__ __forceinline__ uint32_t fused_segments(const SegArgs& a, const Upper
     }
     return 0;
   }
-  const uint64_t nv = a.n_dev ? *a.n_dev : a.n_ops;
+  // uniform (SGPR) loop bounds and tickets: with the exit read as a VGPR
+  // the exit looked divergent, and the compiler merged the count of a
+  // finished tile with the next claim (both "if thread 0") into a second
+  // latch -- lanes 1..63 of wave 0 ran the next iteration's barriers while
+  // lane 0 still claimed, so the block's barriers paired wrongly and it hung
+  // (the fused hang of rounds 4 and 5; a device printf changed the shape).
+  // One claim site, at the end of the body with the count, and readfirstlane.
+  const uint64_t nv = __builtin_amdgcn_readfirstlane(a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_ops);
   const uint64_t ntiles = (nv + kSegTile - 1) / kSegTile;
   uint32_t* tk = &a.ctl->seg_tk[a.par][0];
   uint32_t* dn = &a.ctl->seg_dn[a.par][0];
+  if (threadIdx.x == 0) s_tile = atomicAdd(tk, 1u);
   for (;;) {
-    if (threadIdx.x == 0) s_tile = atomicAdd(tk, 1u);
     __syncthreads();
-    const uint64_t tt = s_tile;
+    const uint64_t tt = __builtin_amdgcn_readfirstlane(s_tile);
     __syncthreads();
     if (tt >= ntiles) break;
     segt::seg_tile(a.op_page, nv, tt, a.lbw, a.seg_start_w, a.seg_end_w, a.seg_page_w,
@@ -454,6 +461,7 @@ __device__ __forceinline__ uint32_t fused_segments(const SegArgs& a, const Upper
       // fence's own wait: MI355X_MICROARCH.md "Compiler hazard")
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_tile = atomicAdd(tk, 1u);
     }
   }
   if (threadIdx.x == 0) {
@@ -473,7 +481,7 @@ __device__ __forceinline__ uint32_t fused_segments(const SegArgs& a, const Upper
     s_ns = ns;
   }
   __syncthreads();
-  return s_ns;
+  return __builtin_amdgcn_readfirstlane(s_ns);
 }
 
 // Early splits (u.early): a segment that would split into at most
