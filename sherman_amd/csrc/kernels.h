@@ -167,10 +167,6 @@ struct UpperCtl {
   // it reads the ordering's count, which chunk tag + 2's ordering may rewrite
   // once the buffers are published
   uint64_t ndel[2][16];
-  // the fused segmentation's tile tickets and finished tiles (per parity,
-  // zeroed by the previous chunk: upper_zero_next)
-  uint32_t seg_tk[2][32];
-  uint32_t seg_dn[2][32];
 };
 // UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
 // the chunk's op buffers (tree.cpp insert_order's flow control)
@@ -220,26 +216,6 @@ struct SegArgs {
   UpperCtl* ctl;
   uint32_t par;
   uint32_t up_nb;
-  // fused segmentation (round 5, upsert.hip): the kernel lists the chunk's
-  // staged segments itself (seg_tile.h tiles claimed by ticket, every block
-  // then waits until all are listed) instead of a k_seg_fill launch before
-  // it; the lists are written through the *_w views of the arrays above
-  uint32_t fused;
-  const uint64_t* op_page;    // the locate's page per op
-  uint64_t n_ops;             // host bound of the op count
-  const uint64_t* n_dev;      // device op count
-  uint64_t* lbw;              // the tiles' tagged look-back words
-  const uint8_t* pnew;        // the locate's page marks
-  uint32_t seg_tag;           // the chunk's tag (marks, words)
-  const uint32_t* any_new;    // the locate's any-page-marked word
-  uint32_t self_after;        // seg_tile's wait bound before it recounts
-  const uint64_t* ndel_src;   // the ordering's delete count ...
-  uint64_t* ndel_dst;         // ... copied for k_upper (UpperCtl.ndel)
-  uint32_t quick_ok;          // a chunk with no new key and no delete is completed here
-  uint32_t* seg_start_w;
-  uint32_t* seg_end_w;
-  uint64_t* seg_page_w;
-  uint32_t* num_seg_w;
 };
 struct UpperArgs;
 // u: the split arguments of the chunk with u.early = 1 (small splits taken

@@ -133,7 +133,7 @@ constexpr uint32_t kErrOverflow = 1u << 6;     // page overfull at apply
 constexpr uint32_t kErrNoMem = 1u << 7;        // page arena exhausted (splits left unapplied)
 constexpr uint32_t kErrHandoff = 1u << 8;      // k_upper: a phase hand-off wait timed out
                                                // (the chunk's levels / deletes resume later)
-constexpr uint32_t kErrSegSpin = 1u << 9;      // fused segmentation: the all-tiles wait bound
+constexpr uint32_t kErrSegSpin = 1u << 9;      // retired (k_seg_fill counts a late tile itself)
 constexpr uint32_t kErrScanSpin = 1u << 10;    // k_scan_u64: look-back spin bound
 constexpr uint32_t kErrBinSpin = 1u << 11;     // k_bin_unique: look-back spin bound
 constexpr uint32_t kErrGetHops = 1u << 12;     // a get walk (k_get / k_get_sum) hop bound

@@ -1,10 +1,12 @@
 // seg_tile.h — one 1024-op tile of the insert segmentation (the staged
 // segments: runs of ops on one page that gets a new key): k_seg_fill's body
-// (util.hip, one tile per block), kept apart for a kernel that lists its own
-// segments (fusing the segmentation into the upsert kernel).
+// (util.hip, one tile per block).
 // (Round 5 measured a one-wave tile, 16 ops per lane at 32 VGPRs: 23.6
 // against 13.5 us alone in C5's profile window, and no better beside the
-// ordering, 32-33 us either way; the 256-thread tile stays.)
+// ordering, 32-33 us either way; the 256-thread tile stays.  Holding the
+// pages in registers and loading the look-back words together took C5's
+// step 196.9 -> 191.4 us.  The tile inside the upsert kernel, round 5's
+// second attempt at the fusion, lost 17 % on C5: DESIGN §8.)
 #pragma once
 #include "device_common.h"
 #include "kernels.h"
@@ -87,11 +89,21 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
                                          const uint8_t* pnew, uint32_t tag, uint32_t self_after) {
   __shared__ uint32_t s_pre[kT / kWave];
   const uint64_t i0 = b * kSegTile + (uint64_t)threadIdx.x * kPer;
-  uint32_t h[kPer], c = 0;
+  // the thread's ops' pages, the one before and the one after, held for the
+  // fill below (one round of independent loads), then every op's page mark
+  // (a second round): the fill re-reads nothing
+  uint64_t pg[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) pg[j] = i0 + j < nv ? page[i0 + j] : ~0ull;
+  const uint64_t before = i0 > 0 && i0 - 1 < nv ? page[i0 - 1] : ~0ull;
+  const uint64_t after = i0 + kPer < nv ? page[i0 + kPer] : ~0ull;
+  uint32_t h[kPer], pn[kPer], c = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) pn[j] = i0 + j < nv && page_new(pnew, pg[j], tag) ? 1u : 0u;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
-    h[j] = seg_head(page, i0 + j, nv);
-    if (h[j]) h[j] = page_new(pnew, page[i0 + j], tag) ? 1u : 0u;
+    const uint64_t prv = j ? pg[j - 1] : before;
+    h[j] = i0 + j < nv && (i0 + j == 0 || pg[j] != prv) ? pn[j] : 0u;
     c += h[j];
   }
   uint32_t total;
@@ -99,20 +111,33 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   const uint64_t tg = (uint64_t)tag << 32;
   if (threadIdx.x == 0)
     __hip_atomic_store(lbw + b, tg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the counts of the tiles before this one
+  // the counts of the tiles before this one: the first kLb words of each
+  // thread loaded together (2^20 ops = 1024 tiles: one round), a word not yet
+  // published polled after
+  constexpr int kLb = 4;
   uint32_t v = 0;
-  for (uint64_t x = threadIdx.x; x < b; x += kT) {
-    uint64_t w = 0;
-    for (uint32_t spin = 0;; ++spin) {
-      if (spin >= self_after) {
-        w = tg | tile_heads(page, nv, x, pnew, tag);
-        break;
-      }
-      w = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((w & ~0xFFFFFFFFull) == tg) break;
-      __builtin_amdgcn_s_sleep(1);
+  for (uint64_t x0 = threadIdx.x; x0 < b; x0 += (uint64_t)kLb * kT) {
+    uint64_t w[kLb];
+#pragma unroll
+    for (int k = 0; k < kLb; ++k) {
+      const uint64_t x = x0 + (uint64_t)k * kT;
+      w[k] = x < b ? __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tg;
     }
-    v += (uint32_t)w;
+#pragma unroll
+    for (int k = 0; k < kLb; ++k) {
+      const uint64_t x = x0 + (uint64_t)k * kT;
+      if (x >= b) break;
+      if (!self_after) w[k] = tg | tile_heads(page, nv, x, pnew, tag);  // forced (tests)
+      for (uint32_t spin = 0; (w[k] & ~0xFFFFFFFFull) != tg; ++spin) {
+        if (spin >= self_after) {
+          w[k] = tg | tile_heads(page, nv, x, pnew, tag);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        w[k] = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      v += (uint32_t)w[k];
+    }
   }
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
@@ -125,14 +150,13 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   for (int j = 0; j < kPer; ++j) {
     const uint64_t i = i0 + j;
     if (i >= nv) break;
-    const uint64_t pg = page[i];
     if (h[j]) {
       seg_start[pos] = (uint32_t)i;
-      seg_page[pos] = pg;
+      seg_page[pos] = pg[j];
     }
     pos += h[j];
-    const bool tail = i + 1 == nv || page[i + 1] != pg;
-    if (tail && (h[j] || page_new(pnew, pg, tag))) seg_end[pos - 1] = (uint32_t)(i + 1);
+    const uint64_t nxt = j + 1 < kPer ? pg[j + 1] : after;  // ~0 past nv
+    if (nxt != pg[j] && pn[j]) seg_end[pos - 1] = (uint32_t)(i + 1);
     if (i + 1 == nv) *num_seg = pos;
   }
   __syncthreads();  // s_pre and the scan's words are reused by the next tile

@@ -758,16 +758,6 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
 }
 
 // steps 2-5 on the ordered chunk of tag (the leaf directory is current)
-// the segmentation inside the upsert kernel (SHM_FUSED_SEG=1; A/B while
-// measured, round 5)
-bool fused_seg() {
-  static const bool on = [] {
-    const char* e = getenv("SHM_FUSED_SEG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
@@ -862,35 +852,14 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   const bool quick_ok = !u.force_abort;
   // force flag bit 3: every tile counts its predecessors itself (the
   // look-back's fallback, exercised by a test)
-  const uint32_t self_after = (t->force_flags & 8u) ? 0u : kSegSelfAfter;
-  const bool fused = fused_seg();
-  if (!fused) {
-    dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
-                        t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
-                        quick_ok ? &u : nullptr, lb_ctr(t, dev::kLbSeg), self_after, cnt + 1,
-                        &t->ctl->ndel[tag & 1u][0]);
-    DBG(s, "segment");
-  }
+  dev::launch_segment(t->pages, n, cnt + 0, t->seg_lb, t->seg_start, t->seg_end,
+                      t->seg_page, d_ns, t->pnew, tag, w.any_new, t->d_err, s,
+                      quick_ok ? &u : nullptr, lb_ctr(t, dev::kLbSeg),
+                      (t->force_flags & 8u) ? 0u : kSegSelfAfter, cnt + 1,
+                      &t->ctl->ndel[tag & 1u][0]);
+  DBG(s, "segment");
   if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
   dev::SegArgs a{};
-  if (fused) {  // the upsert kernel lists the segments itself (upsert.hip)
-    a.fused = 1;
-    a.op_page = t->pages;
-    a.n_ops = n;
-    a.n_dev = cnt + 0;
-    a.lbw = t->seg_lb;
-    a.pnew = t->pnew;
-    a.seg_tag = tag;
-    a.any_new = w.any_new;
-    a.self_after = self_after;
-    a.ndel_src = cnt + 1;
-    a.ndel_dst = &t->ctl->ndel[tag & 1u][0];
-    a.quick_ok = quick_ok ? 1u : 0u;
-    a.seg_start_w = t->seg_start;
-    a.seg_end_w = t->seg_end;
-    a.seg_page_w = t->seg_page;
-    a.num_seg_w = d_ns;
-  }
   a.arena = t->arena;
   a.arena_bytes = t->arena_bytes;
   a.node = t->cfg.node_id;

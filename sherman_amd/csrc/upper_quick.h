@@ -33,8 +33,6 @@ __device__ __forceinline__ void upper_zero_next(UpperCtl* ctl, uint32_t par, uin
     ctl->root_new[par ^ 1][0] = 0;
     ctl->done[par ^ 1][0] = 0;
     ctl->ualloc[par ^ 1][0] = 0;
-    ctl->seg_tk[par ^ 1][0] = 0;
-    ctl->seg_dn[par ^ 1][0] = 0;
   }
 }
 

@@ -33,8 +33,6 @@
 #include "lds_dma.h"
 #include "leaf_chunk.h"
 #include "split_wave.h"
-#include "seg_tile.h"
-#include "upper_quick.h"
 
 namespace shm {
 namespace dev {
@@ -410,80 +408,6 @@ __device__ __forceinline__ uint32_t upsert_groups(const SegArgs& a, const UpperA
   return err;
 }
 
-// Fused segmentation (a.fused, round 5): the chunk's staged segments listed
-// by this kernel before it applies them, so the chain has no k_seg_fill
-// launch (one dependent launch, ~3-4 us per chunk).  Every block first
-// claims 1024-op tiles by ticket (seg_tile.h: count, publish, look back,
-// fill; a tile waits only on tiles of smaller index, all claimed earlier by
-// running blocks, and recounts a late one itself), counts each finished tile
-// once its records are written back, and, with no tile left to claim, waits
-// until every tile is counted -- every tile is held by a running block, so
-// the wait ends (bounded: kErrSegSpin).  A chunk with no new key is
-// completed by block 0 (upper_quick.h) and every block returns.
-constexpr uint32_t kFusedSpins = 1u << 20;
-__device__ __forceinline__ uint32_t fused_segments(const SegArgs& a, const UpperArgs& u) {
-  __shared__ uint32_t s_tile, s_ns;
-  // the chunk's delete count for k_upper, before anything publishes the op
-  // buffers free (upper_quick.h below, or k_upper)
-  if (a.ndel_dst && blockIdx.x == 0 && threadIdx.x == 0) *a.ndel_dst = *a.ndel_src;
-  if (a.any_new && *a.any_new != a.seg_tag) {  // no op of the chunk is new: nothing staged
-    if (blockIdx.x == 0) {
-      if (threadIdx.x == 0) *a.num_seg_w = 0;
-      if (a.quick_ok) seg_complete_unchanged(u);
-    }
-    return 0;
-  }
-  // uniform (SGPR) loop bounds and tickets: with the exit read as a VGPR
-  // the exit looked divergent, and the compiler merged the count of a
-  // finished tile with the next claim (both "if thread 0") into a second
-  // latch -- lanes 1..63 of wave 0 ran the next iteration's barriers while
-  // lane 0 still claimed, so the block's barriers paired wrongly and it hung
-  // (the fused hang of rounds 4 and 5; a device printf changed the shape).
-  // One claim site, at the end of the body with the count, and readfirstlane.
-  const uint64_t nv = __builtin_amdgcn_readfirstlane(a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_ops);
-  const uint64_t ntiles = (nv + kSegTile - 1) / kSegTile;
-  uint32_t* tk = &a.ctl->seg_tk[a.par][0];
-  uint32_t* dn = &a.ctl->seg_dn[a.par][0];
-  if (threadIdx.x == 0) s_tile = atomicAdd(tk, 1u);
-  for (;;) {
-    __syncthreads();
-    const uint64_t tt = __builtin_amdgcn_readfirstlane(s_tile);
-    __syncthreads();
-    if (tt >= ntiles) break;
-    segt::seg_tile(a.op_page, nv, tt, a.lbw, a.seg_start_w, a.seg_end_w, a.seg_page_w,
-                   a.num_seg_w, a.pnew, a.seg_tag, a.self_after);
-    // every thread's records performed, then the tile counts as finished
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      // the write-back performed before the count (the compiler may drop the
-      // fence's own wait: MI355X_MICROARCH.md "Compiler hazard")
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_tile = atomicAdd(tk, 1u);
-    }
-  }
-  if (threadIdx.x == 0) {
-    uint32_t spin = 0;
-    while (__hip_atomic_load(dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
-      if (++spin > kFusedSpins) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    uint32_t ns = 0;
-    if (spin > kFusedSpins)
-      atomicOr(a.err, kErrSegSpin);
-    else if (ntiles)
-      ns = __hip_atomic_load(a.num_seg_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if (blockIdx.x == 0)
-      *a.num_seg_w = 0;  // no op: k_upper reads the count
-    s_ns = ns;
-  }
-  __syncthreads();
-  return __builtin_amdgcn_readfirstlane(s_ns);
-}
-
 // Early splits (u.early): a segment that would split into at most
 // kSmallSplit pages is queued in the block's LDS queue instead of being left
 // to k_upper, and a wave of the same block builds it and takes its separators
@@ -502,12 +426,7 @@ __device__ __forceinline__ void upsert_body(const SegArgs& a, const UpperArgs& u
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint32_t num_seg;
-  if (a.fused) {
-    num_seg = fused_segments(a, u);
-  } else {
-    num_seg = *a.num_seg_dev;
-  }
+  const uint32_t num_seg = *a.num_seg_dev;
   if (num_seg == 0) return;  // every op applied in place (C3's chunks): the block's only load
   const uint64_t ngroups = ((uint64_t)num_seg + G - 1) / G;
   // early splits need a root above the leaves (a leaf root grows the tree:
@@ -570,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_upsert_pipe(SegArgs a, UpperArg
 
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
   constexpr int G = 4;
-  if (!a.num_seg && !a.fused) return;
+  if (!a.num_seg) return;
   static unsigned nb = 0;
   if (!nb) {
     int per_cu = 0, cus = 0, dev = 0;
@@ -580,8 +499,7 @@ void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s) {
     nb = (unsigned)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256));
   }
   const uint64_t groups = (a.num_seg + G - 1) / G;
-  uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (a.fused && need == 0) need = 1;  // block 0 copies the delete count
+  const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(k_leaf_upsert_pipe<G>, dim3((unsigned)std::min<uint64_t>(need, nb)), dim3(kBlock),
                      0, s, a, u);
 }

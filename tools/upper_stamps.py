@@ -1,5 +1,5 @@
 """k_upper phase clock (diagnostic; run on the GPU box):
-    python tools/upper_stamps.py [keys_log2] [batches]
+    python tools/upper_stamps.py [keys_log2] [batches] [pipe]
 Builds a tree of 2^keys_log2 keys, then applies C5-like insert batches
 (1 Mi ops, key = to_key(1 + zipf(0.99) over twice the key set)) and C3-like
 ones (zipf over the stored keys: updates only) and prints, per batch, the
@@ -20,6 +20,8 @@ from sherman_amd.workload import Zipf  # noqa: E402
 def main():
     kl = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    pipe = len(sys.argv) > 3 and sys.argv[3] == "pipe"
+    s_ord, s_app = torch.cuda.Stream(), torch.cuda.Stream()
     dev = torch.device("cuda:0")
     n = 1 << kl
     t = shm.Tree(arena_bytes=max(2 << 30, n * 1024 // 20), max_batch=1 << 20, device=0)
@@ -42,8 +44,25 @@ def main():
             k = torch.empty_like(ids)
             t.hash_keys(ids, k)
             v = torch.arange(1, (1 << 20) + 1, dtype=torch.int64, device=dev)
-            t.insert_batch(k, v)
-            fn(t.h, 2, out)
+            if pipe and name == "c5":
+                # bench's C5 shape: the next chunk's ordering on its own
+                # stream beside this chunk's apply (the upsert rows are this
+                # chunk's, the ordering rows the next chunk's)
+                ids2 = z.sample(1 << 20, g) + 1
+                k2 = torch.empty_like(ids2)
+                t.hash_keys(ids2, k2)
+                s_ord.wait_stream(torch.cuda.current_stream())
+                s_app.wait_stream(torch.cuda.current_stream())
+                t0_ = t.insert_order(k, v, stream=s_ord)
+                t1_ = t.insert_order(k2, v, stream=s_ord)
+                t.insert_apply(t0_, stream=s_app)
+                torch.cuda.synchronize()
+                fn(t.h, 2, out)
+                t.insert_apply(t1_, stream=s_app)
+                torch.cuda.synchronize()
+            else:
+                t.insert_batch(k, v)
+                fn(t.h, 2, out)
             cnt = int(out[0])
             ts = [int(out[i]) for i in range(1, cnt)]
             d = [round((ts[i] - ts[i - 1]) / 100.0, 1) for i in range(1, len(ts))]  # 100 MHz
