@@ -168,7 +168,11 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
     bool more = false;
     uint64_t sibling = 0;
     uint32_t hwn = kLeafHwFull;
-    RPage wn = w;
+    // w is staged: its registers take the sibling's bytes (one page of
+    // registers per lane, not two: 88 -> 77 VGPRs, 5 -> 6 waves per SIMD,
+    // k_range 63.4 -> 62.7 us in the bench's profile pass.  Pages by LDS-DMA
+    // instead, one slot per scan, measured 66.3: the slot refills only after
+    // the page's compare, and the entry unpack still held 86 VGPRs)
     bool hit[kRE];
     uint64_t ev[kRE];
 #pragma unroll
@@ -188,7 +192,7 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
           // in flight: the sibling's bound (a 1.8 MB array, L2-resident) and
           // its first 768 bytes
           if (a.leaf_hw) hwn = a.leaf_hw[ga_offset(sibling) >> 10];
-          rload3(a.arena, sibling, li, wn);
+          rload3(a.arena, sibling, li, w);
         }
       }
       uint32_t D[kRCD];
@@ -222,10 +226,9 @@ __device__ __forceinline__ uint64_t range_walk(const RangeArgs& a, bool act, uin
     wave_lds_sync();  // LDS reads done before the next stage
     if (act) {
       if (more) {
-        if (hwn >= kChunk3Hw) rload_last(a.arena, sibling, li, wn);
+        if (hwn >= kChunk3Hw) rload_last(a.arena, sibling, li, w);
         hw = hwn < (uint32_t)kLeafCardinality ? hwn : (uint32_t)kLeafCardinality;
         p = sibling;
-        w = wn;
       } else {
         act = false;
       }
