@@ -5,7 +5,9 @@
 // against 13.5 us alone in C5's profile window, and no better beside the
 // ordering, 32-33 us either way; the 256-thread tile stays.  Holding the
 // pages in registers and loading the look-back words together took C5's
-// step 196.9 -> 191.4 us.  The tile inside the upsert kernel, round 5's
+// step 196.9 -> 191.4 us; one copy of the late-word path (not one per
+// batched word) took the kernel 74 -> 61 VGPRs, so its blocks fit beside
+// k_bin_unique's (112 VGPRs x 4 waves per SIMD): 190.6 -> 188.5 us.  The tile inside the upsert kernel, round 5's
 // second attempt at the fusion, lost 17 % on C5: DESIGN §8.)
 #pragma once
 #include "device_common.h"
@@ -97,15 +99,16 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   for (int j = 0; j < kPer; ++j) pg[j] = i0 + j < nv ? page[i0 + j] : ~0ull;
   const uint64_t before = i0 > 0 && i0 - 1 < nv ? page[i0 - 1] : ~0ull;
   const uint64_t after = i0 + kPer < nv ? page[i0 + kPer] : ~0ull;
-  uint32_t h[kPer], pn[kPer], c = 0;
+  // page marks and staged heads as bit masks (bit j: op i0 + j)
+  uint32_t pn = 0, h = 0;
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) pn[j] = i0 + j < nv && page_new(pnew, pg[j], tag) ? 1u : 0u;
+  for (int j = 0; j < kPer; ++j) pn |= (i0 + j < nv && page_new(pnew, pg[j], tag) ? 1u : 0u) << j;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint64_t prv = j ? pg[j - 1] : before;
-    h[j] = i0 + j < nv && (i0 + j == 0 || pg[j] != prv) ? pn[j] : 0u;
-    c += h[j];
+    h |= (i0 + j < nv && (i0 + j == 0 || pg[j] != prv) ? (pn >> j) & 1u : 0u) << j;
   }
+  const uint32_t c = __builtin_popcount(h);
   uint32_t total;
   const uint32_t local = block_scan<uint32_t>(c, &total);
   const uint64_t tg = (uint64_t)tag << 32;
@@ -123,20 +126,32 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
       const uint64_t x = x0 + (uint64_t)k * kT;
       w[k] = x < b ? __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tg;
     }
+    // bit k: tile x0 + k kT (< b) not yet published, or the forced recount;
+    // a slot past b adds nothing (w = tg | 0)
+    uint32_t late = 0;
 #pragma unroll
     for (int k = 0; k < kLb; ++k) {
-      const uint64_t x = x0 + (uint64_t)k * kT;
-      if (x >= b) break;
-      if (!self_after) w[k] = tg | tile_heads(page, nv, x, pnew, tag);  // forced (tests)
-      for (uint32_t spin = 0; (w[k] & ~0xFFFFFFFFull) != tg; ++spin) {
-        if (spin >= self_after) {
-          w[k] = tg | tile_heads(page, nv, x, pnew, tag);
+      const bool past = x0 + (uint64_t)k * kT >= b;
+      if (past || ((w[k] & ~0xFFFFFFFFull) == tg && self_after))
+        v += (uint32_t)w[k];
+      else
+        late |= 1u << k;
+    }
+    // the rare path, one copy: poll each late word, then count it ourselves
+#pragma unroll 1
+    for (; late; late &= late - 1) {
+      const uint64_t x = x0 + (uint64_t)__builtin_ctz(late) * kT;
+      uint64_t y = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (spin >= self_after) {  // self_after 0: forced (tests)
+          y = tile_heads(page, nv, x, pnew, tag);
           break;
         }
+        y = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((y & ~0xFFFFFFFFull) == tg) break;
         __builtin_amdgcn_s_sleep(1);
-        w[k] = __hip_atomic_load(lbw + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      v += (uint32_t)w[k];
+      v += (uint32_t)y;
     }
   }
 #pragma unroll
@@ -150,13 +165,14 @@ __device__ __forceinline__ void seg_tile(const uint64_t* page, uint64_t nv, uint
   for (int j = 0; j < kPer; ++j) {
     const uint64_t i = i0 + j;
     if (i >= nv) break;
-    if (h[j]) {
+    const uint32_t hj = (h >> j) & 1u;
+    if (hj) {
       seg_start[pos] = (uint32_t)i;
       seg_page[pos] = pg[j];
     }
-    pos += h[j];
+    pos += hj;
     const uint64_t nxt = j + 1 < kPer ? pg[j + 1] : after;  // ~0 past nv
-    if (nxt != pg[j] && pn[j]) seg_end[pos - 1] = (uint32_t)(i + 1);
+    if (nxt != pg[j] && ((pn >> j) & 1u)) seg_end[pos - 1] = (uint32_t)(i + 1);
     if (i + 1 == nv) *num_seg = pos;
   }
   __syncthreads();  // s_pre and the scan's words are reused by the next tile
