@@ -362,7 +362,9 @@ int shm_shard_search(shm_shard *s, const uint64_t *keys, uint64_t n, uint64_t *v
 /* the same in two halves for pipelining: begin = bucketing + the keys'
  * exchange, end = local get + the results' exchange + unpack (neither waits
  * for the device).  Two batches may be begun at once (two slots, each with
- * its own communicator); end them in order. */
+ * its own communicator); end them in order.  At world 1 begin does nothing
+ * and end is the local get over keys[], so keys[] stays unchanged until
+ * end's work has run on the stream. */
 int shm_shard_search_begin(shm_shard *s, const uint64_t *keys, uint64_t n, void *stream,
                            uint32_t *ticket);
 int shm_shard_search_end(shm_shard *s, uint32_t ticket, uint64_t *vals_out, uint8_t *found_out);
