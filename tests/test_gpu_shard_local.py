@@ -22,7 +22,7 @@ Checked against ONE unsharded CPU oracle tree (test infrastructure):
     rank 3's next synchronising call) while the other ranks' batches apply,
     as a local insert rejects the chunk holding kKeyMax;
   * routed gets of a uniform batch, of a zipf(0.99) batch (the hot key's
-    shard passes its slot of 1.25 n / P + 256) and of a batch whose every key
+    shard passes its slot of n / P + 6 sqrt(n / P) + 256) and of a batch whose every key
     belongs to shard 0 (7/8 of it overflows): every value returned, no key
     dropped; two batches in flight (begin, begin, end, end);
   * routed range scans across shard boundaries (whole key space, empty,
