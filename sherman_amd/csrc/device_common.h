@@ -432,6 +432,32 @@ __device__ __forceinline__ void lane_entry(const uint8_t* page, int s, uint64_t&
   r = (q4 >> 8) & 0xFF;
 }
 
+// lane_entry in two halves, so several entries (and a summary line) can be
+// requested before any is decoded: the raw dwords of entry s, then its fields
+struct RawEntry {
+  uint32_t d[5];
+  uint32_t sh;
+};
+__device__ __forceinline__ void entry_load(const uint8_t* page, int s, RawEntry& r) {
+  const uint32_t off = (uint32_t)(kOffRecords + kLeafEntry * s);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(page + (off & ~3u));
+#pragma unroll
+  for (int j = 0; j < 5; ++j) r.d[j] = d[j];
+  r.sh = off & 3u;
+}
+__device__ __forceinline__ void entry_decode(const RawEntry& e, uint64_t& key, uint64_t& val,
+                                             uint32_t& f, uint32_t& r) {
+  const uint32_t q0 = __builtin_amdgcn_alignbyte(e.d[1], e.d[0], e.sh);
+  const uint32_t q1 = __builtin_amdgcn_alignbyte(e.d[2], e.d[1], e.sh);
+  const uint32_t q2 = __builtin_amdgcn_alignbyte(e.d[3], e.d[2], e.sh);
+  const uint32_t q3 = __builtin_amdgcn_alignbyte(e.d[4], e.d[3], e.sh);
+  const uint32_t q4 = e.d[4] >> (8 * e.sh);
+  f = q0 & 0xFF;
+  key = (uint64_t)((q0 >> 8) | (q1 << 24)) | ((uint64_t)((q1 >> 8) | (q2 << 24)) << 32);
+  val = (uint64_t)((q2 >> 8) | (q3 << 24)) | ((uint64_t)((q3 >> 8) | (q4 << 24)) << 32);
+  r = (q4 >> 8) & 0xFF;
+}
+
 __device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f, uint32_t r,
                                           uint64_t k) {
   return key == k && val != kValueNull && ((f ^ r) & 0xF) == 0;
@@ -443,12 +469,12 @@ __device__ __forceinline__ bool entry_hit(uint64_t key, uint64_t val, uint32_t f
 struct SumLine {
   uint64_t highest, cand;
 };
-__device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, uint64_t k,
-                                         SumLine& o) {
+__device__ __forceinline__ void sum_load(const uint8_t* sum, uint64_t page_off, u32x4 (&l)[4]) {
   const u32x4* line = reinterpret_cast<const u32x4*>(sum + (page_off >> 10) * kSumBytes);
-  u32x4 l[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) l[j] = line[j];
+}
+__device__ __forceinline__ bool sum_decode(const u32x4 (&l)[4], uint64_t k, SumLine& o) {
   if ((l[0].z & 0xFF) != kSumLeaf) return false;
   o.highest = (uint64_t)l[0].x | ((uint64_t)l[0].y << 32);
   const uint32_t fq = key_fp(k);
@@ -463,6 +489,12 @@ __device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, 
   }
   o.cand = cand;
   return true;
+}
+__device__ __forceinline__ bool sum_read(const uint8_t* sum, uint64_t page_off, uint64_t k,
+                                         SumLine& o) {
+  u32x4 l[4];
+  sum_load(sum, page_off, l);
+  return sum_decode(l, k, o);
 }
 // a page's sibling pointer from its header (bytes 17..24, Tree.h:130-160):
 // the right turn of a summary walk

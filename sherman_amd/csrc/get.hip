@@ -352,28 +352,111 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
   if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
     uint64_t ptr = a.root;
     uint64_t alt = 0;  // a tie's safe start (dir_start_e)
+    bool done = false;  // val is the answer
     if (a.dir) {
       u32x4 e[4];
       bool fpform;
       ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform, &alt);
-      if (fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
-        // the prefix lies in one leaf and the entry holds its fingerprints:
-        // read the candidate slots straight away (Tree.cpp:687-697's first
-        // valid slot with the key); a key not found this way (absent, or
-        // the copy is stale) takes the summary walk below
-        const uint8_t* page = a.arena + ga_offset(ptr);
-        uint64_t cand = dir_fp_cand(e, k);
-        while (cand) {
-          uint64_t ek, ev;
-          uint32_t ef, er;
+      // A wave's gets take their slowest lane's number of dependent rounds,
+      // so the common cases share a round: after the directory entry, a lane
+      // in fingerprint form reads its lowest candidate entry (the prefix lies
+      // in one leaf and the entry holds its fingerprints: Tree.cpp:687-697's
+      // first valid slot with the key) while a lane that needs the summary
+      // line reads it -- before, the summary lanes waited for the whole
+      // wave's candidate loop -- and then the summary lanes read their
+      // lowest candidate.  Anything else -- a further candidate, a stale
+      // copy, an absent key, a right turn, a tie's safe start, an internal
+      // page -- goes on one request at a time.  C3 +5-7 %, C2 +0.5 %
+      // (same box); also reading the second candidate in the same round
+      // was C2 -2 % (its speculative requests) for about the same C3.
+      const bool pok = ptr_ok(ptr, a.node, a.arena_bytes);
+      const uint64_t off = ga_offset(ptr);
+      const uint8_t* page = a.arena + off;
+      const bool fp = fpform && pok;
+      const uint64_t cand = fp ? dir_fp_cand(e, k) : 0;
+      const uint64_t cand2 = cand & (cand - 1);
+      const int s1 = cand ? (int)ctz64(cand) : -1;
+      const int s2 = -1;  // (a second candidate in the same round: C2 -2 %, C3 +4.5 %)
+      RawEntry r1, r2;
+      if (s1 >= 0) entry_load(page, s1, r1);
+      u32x4 sraw[4];
+      const bool sm = !fpform && pok;
+      if (sm) sum_load(a.sum, off, sraw);
+      c_ent += (s1 >= 0 ? 1u : 0u) + (s2 >= 0 ? 1u : 0u);
+      uint64_t ek, ev;
+      uint32_t ef, er;
+      if (s1 >= 0) {
+        entry_decode(r1, ek, ev, ef, er);
+        if (entry_hit(ek, ev, ef, er, k)) {
+          val = ev;
+          hit = done = true;
+        }
+      }
+      if (!done && s2 >= 0) {
+        entry_decode(r2, ek, ev, ef, er);
+        if (entry_hit(ek, ev, ef, er, k)) {
+          val = ev;
+          hit = done = true;
+        }
+      }
+      if (!done && fp) {
+        // a third candidate and on (rare); then, not found, the summary walk
+        // below (absent key or stale copy)
+        uint64_t rest = cand2;
+        while (rest) {
           ++c_ent;
-          lane_entry(page, ctz64(cand), ek, ev, ef, er);
+          lane_entry(page, ctz64(rest), ek, ev, ef, er);
           if (entry_hit(ek, ev, ef, er, k)) {
             val = ev;
-            hit = true;
+            hit = done = true;
             break;
           }
-          cand &= cand - 1;
+          rest &= rest - 1;
+        }
+      }
+      SumLine sl;
+      if (sm && sum_decode(sraw, k, sl) && k < sl.highest) {
+        // k's leaf (k >= highest turns right below); its two lowest
+        // candidates together, the rest one at a time
+        const uint64_t sc = sl.cand;
+        const uint64_t sc2 = sc & (sc - 1);
+        const int t1 = sc ? (int)ctz64(sc) : -1;
+        const int t2 = -1;
+        if (t1 >= 0) entry_load(page, t1, r1);
+        c_ent += (t1 >= 0 ? 1u : 0u) + (t2 >= 0 ? 1u : 0u);
+        if (t1 >= 0) {
+          entry_decode(r1, ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            done = true;
+          }
+        }
+        if (!done && t2 >= 0) {
+          entry_decode(r2, ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            done = true;
+          }
+        }
+        uint64_t rest = sc2;
+        while (!done && rest) {
+          ++c_ent;
+          lane_entry(page, ctz64(rest), ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            done = true;
+          }
+          rest &= rest - 1;
+        }
+        if (!done) {
+          if (alt) {
+            // a tie's optimistic leaf does not hold k: k may lie below its
+            // lowest fence, so walk again from the safe start
+            ptr = alt;
+            alt = 0;
+          } else {
+            done = true;  // k's leaf does not hold k
+          }
         }
       }
     } else if (tn) {
@@ -389,7 +472,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
       ptr = dir_page_ga(tpg[lo], a.node);
     }
     int retries = 0;
-    for (int hop = 0; !hit; ++hop) {
+    for (int hop = 0; !done; ++hop) {
       if (hop > kMaxRounds) {
         err |= kErrGetHops;
         break;
