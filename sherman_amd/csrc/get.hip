@@ -358,105 +358,64 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
       bool fpform;
       ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform, &alt);
       // A wave's gets take their slowest lane's number of dependent rounds,
-      // so the common cases share a round: after the directory entry, a lane
-      // in fingerprint form reads its lowest candidate entry (the prefix lies
+      // so the lanes share rounds: after the directory entry, a lane in
+      // fingerprint form reads its lowest candidate entry (the prefix lies
       // in one leaf and the entry holds its fingerprints: Tree.cpp:687-697's
       // first valid slot with the key) while a lane that needs the summary
       // line reads it -- before, the summary lanes waited for the whole
-      // wave's candidate loop -- and then the summary lanes read their
-      // lowest candidate.  Anything else -- a further candidate, a stale
-      // copy, an absent key, a right turn, a tie's safe start, an internal
-      // page -- goes on one request at a time.  C3 +5-7 %, C2 +0.5 %
-      // (same box); also reading the second candidate in the same round
-      // was C2 -2 % (its speculative requests) for about the same C3.
+      // wave's candidate loop -- and then every lane reads one candidate per
+      // round, lowest first, the summary lanes' first beside the fingerprint
+      // lanes' second.  A stale copy, an absent key, a right turn, a tie's
+      // safe start, an internal page go on below.  C3 +5-7 %, C2 +0.5 %
+      // (same box, first form); reading two candidates per round was C2
+      // -2 % (speculative requests) for about the same C3.
       const bool pok = ptr_ok(ptr, a.node, a.arena_bytes);
       const uint64_t off = ga_offset(ptr);
       const uint8_t* page = a.arena + off;
       const bool fp = fpform && pok;
-      const uint64_t cand = fp ? dir_fp_cand(e, k) : 0;
-      const uint64_t cand2 = cand & (cand - 1);
-      const int s1 = cand ? (int)ctz64(cand) : -1;
-      const int s2 = -1;  // (a second candidate in the same round: C2 -2 %, C3 +4.5 %)
-      RawEntry r1, r2;
-      if (s1 >= 0) entry_load(page, s1, r1);
-      u32x4 sraw[4];
       const bool sm = !fpform && pok;
+      // pend: the lane's candidate slots still to read, lowest first
+      uint64_t pend = fp ? dir_fp_cand(e, k) : 0;
+      RawEntry r1;
+      if (pend) entry_load(page, (int)ctz64(pend), r1);
+      u32x4 sraw[4];
       if (sm) sum_load(a.sum, off, sraw);
-      c_ent += (s1 >= 0 ? 1u : 0u) + (s2 >= 0 ? 1u : 0u);
       uint64_t ek, ev;
       uint32_t ef, er;
-      if (s1 >= 0) {
+      if (pend) {
+        ++c_ent;
         entry_decode(r1, ek, ev, ef, er);
         if (entry_hit(ek, ev, ef, er, k)) {
           val = ev;
           hit = done = true;
         }
+        pend &= pend - 1;
       }
-      if (!done && s2 >= 0) {
-        entry_decode(r2, ek, ev, ef, er);
+      // a summary lane in k's leaf (k >= highest turns right below) joins
+      // the candidate rounds
+      SumLine sl;
+      const bool inleaf = sm && sum_decode(sraw, k, sl) && k < sl.highest;
+      if (inleaf) pend = sl.cand;
+      while (!done && pend) {  // one candidate per lane and round, lowest first
+        ++c_ent;
+        lane_entry(page, ctz64(pend), ek, ev, ef, er);
         if (entry_hit(ek, ev, ef, er, k)) {
           val = ev;
-          hit = done = true;
+          done = true;
+          hit = fp;
         }
+        pend &= pend - 1;
       }
-      if (!done && fp) {
-        // a third candidate and on (rare); then, not found, the summary walk
-        // below (absent key or stale copy)
-        uint64_t rest = cand2;
-        while (rest) {
-          ++c_ent;
-          lane_entry(page, ctz64(rest), ek, ev, ef, er);
-          if (entry_hit(ek, ev, ef, er, k)) {
-            val = ev;
-            hit = done = true;
-            break;
-          }
-          rest &= rest - 1;
-        }
-      }
-      SumLine sl;
-      if (sm && sum_decode(sraw, k, sl) && k < sl.highest) {
-        // k's leaf (k >= highest turns right below); its two lowest
-        // candidates together, the rest one at a time
-        const uint64_t sc = sl.cand;
-        const uint64_t sc2 = sc & (sc - 1);
-        const int t1 = sc ? (int)ctz64(sc) : -1;
-        const int t2 = -1;
-        if (t1 >= 0) entry_load(page, t1, r1);
-        c_ent += (t1 >= 0 ? 1u : 0u) + (t2 >= 0 ? 1u : 0u);
-        if (t1 >= 0) {
-          entry_decode(r1, ek, ev, ef, er);
-          if (entry_hit(ek, ev, ef, er, k)) {
-            val = ev;
-            done = true;
-          }
-        }
-        if (!done && t2 >= 0) {
-          entry_decode(r2, ek, ev, ef, er);
-          if (entry_hit(ek, ev, ef, er, k)) {
-            val = ev;
-            done = true;
-          }
-        }
-        uint64_t rest = sc2;
-        while (!done && rest) {
-          ++c_ent;
-          lane_entry(page, ctz64(rest), ek, ev, ef, er);
-          if (entry_hit(ek, ev, ef, er, k)) {
-            val = ev;
-            done = true;
-          }
-          rest &= rest - 1;
-        }
-        if (!done) {
-          if (alt) {
-            // a tie's optimistic leaf does not hold k: k may lie below its
-            // lowest fence, so walk again from the safe start
-            ptr = alt;
-            alt = 0;
-          } else {
-            done = true;  // k's leaf does not hold k
-          }
+      // not found: a fingerprint lane takes the summary walk below (absent
+      // key or stale copy); a summary lane's leaf does not hold k, unless
+      // this was a tie's optimistic leaf (k may lie below its lowest fence:
+      // walk again from the safe start)
+      if (!done && inleaf) {
+        if (alt) {
+          ptr = alt;
+          alt = 0;
+        } else {
+          done = true;
         }
       }
     } else if (tn) {
