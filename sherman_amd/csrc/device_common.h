@@ -324,6 +324,36 @@ __device__ __forceinline__ uint64_t dir_fp_cand(const u32x4 (&e)[4], uint64_t k)
   return cand;
 }
 
+// A directory entry in pair form (layout.h kDirPairs): usable when its build
+// finished clean (no kDirPairsBad, at most kDirPairMax pairs); the pairs
+// whose fingerprint equals k's (bit j: pair j), each naming a slot of one of
+// the entry's leaves (dir_pair_slot).  Like the fingerprint form's, a
+// candidate is only a slot to read (a stale pair costs the summary walk).
+__device__ __forceinline__ uint32_t dir_pair_cand(const u32x4 (&e)[4], uint64_t k, bool& usable) {
+  const uint32_t cw = e[1].w;
+  const uint32_t np = (cw >> 16) & 0xFFu;
+  usable = (cw & kDirPairs) && !(cw & kDirPairsBad) && np <= kDirPairMax;
+  if (!usable) return 0;
+  const uint32_t fq = key_fp(k);
+  const uint32_t w[8] = {e[2].x, e[2].y, e[2].z, e[2].w, e[3].x, e[3].y, e[3].z, e[3].w};
+  uint32_t cand = 0;
+#pragma unroll
+  for (int j = 0; j < (int)kDirPairMax; ++j) {
+    const uint32_t pr = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    cand |= (uint32_t)((uint32_t)j < np && (pr & 0xFFu) == fq) << j;
+  }
+  return cand;
+}
+// pair j's leaf (page index from the entry's list) and slot
+__device__ __forceinline__ void dir_pair_slot(const u32x4 (&e)[4], int j, uint32_t& pg, int& slot) {
+  const uint32_t w = (j < 8 ? (j < 4 ? (j < 2 ? e[2].x : e[2].y) : (j < 6 ? e[2].z : e[2].w))
+                            : (j < 12 ? (j < 10 ? e[3].x : e[3].y) : (j < 14 ? e[3].z : e[3].w)));
+  const uint32_t pr = (w >> (16 * (j & 1))) & 0xFFFFu;
+  const uint32_t leaf = (pr >> 14) & 3u;
+  slot = (int)((pr >> 8) & 63u);
+  pg = leaf == 0 ? e[0].x : leaf == 1 ? e[0].y : leaf == 2 ? e[0].z : e[0].w;
+}
+
 __device__ __forceinline__ bool ptr_ok(uint64_t ga, uint16_t node,
                                        uint64_t arena_bytes) {
   const uint64_t off = ga_offset(ga);

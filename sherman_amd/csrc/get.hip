@@ -373,21 +373,47 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
       const uint64_t off = ga_offset(ptr);
       const uint8_t* page = a.arena + off;
       const bool fp = fpform && pok;
-      const bool sm = !fpform && pok;
-      // pend: the lane's candidate slots still to read, lowest first
-      uint64_t pend = fp ? dir_fp_cand(e, k) : 0;
+      // a read phase's pair form: the prefix's own keys, in up to four leaves
+      bool pu = false;
+      const uint32_t pc = !fpform && pok ? dir_pair_cand(e, k, pu) : 0u;
+      const bool sm = !fpform && pok && !pu;
+      // pend: the lane's candidates still to read, lowest first (slots of
+      // its leaf, or pair-form pairs)
+      uint64_t pend = fp ? dir_fp_cand(e, k) : (uint64_t)pc;
+      bool pairs = pu;
+      // candidate bit c -> its page and slot (false: a pair naming a bad page)
+      auto at = [&](int c, const uint8_t*& cp, int& cs) {
+        if (!pairs) {
+          cp = page;
+          cs = c;
+          return true;
+        }
+        uint32_t pgi;
+        dir_pair_slot(e, c, pgi, cs);
+        const uint64_t ga = dir_page_ga(pgi, a.node);
+        cp = a.arena + ga_offset(ga);
+        return ptr_ok(ga, a.node, a.arena_bytes);
+      };
+      const uint8_t* cp = page;
+      int cs = 0;
       RawEntry r1;
-      if (pend) entry_load(page, (int)ctz64(pend), r1);
+      bool l1 = false;
+      if (pend) {
+        l1 = at((int)ctz64(pend), cp, cs);
+        if (l1) entry_load(cp, cs, r1);
+      }
       u32x4 sraw[4];
       if (sm) sum_load(a.sum, off, sraw);
       uint64_t ek, ev;
       uint32_t ef, er;
       if (pend) {
-        ++c_ent;
-        entry_decode(r1, ek, ev, ef, er);
-        if (entry_hit(ek, ev, ef, er, k)) {
-          val = ev;
-          hit = done = true;
+        if (l1) {
+          ++c_ent;
+          entry_decode(r1, ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            hit = done = true;
+          }
         }
         pend &= pend - 1;
       }
@@ -397,19 +423,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
       const bool inleaf = sm && sum_decode(sraw, k, sl) && k < sl.highest;
       if (inleaf) pend = sl.cand;
       while (!done && pend) {  // one candidate per lane and round, lowest first
-        ++c_ent;
-        lane_entry(page, ctz64(pend), ek, ev, ef, er);
-        if (entry_hit(ek, ev, ef, er, k)) {
-          val = ev;
-          done = true;
-          hit = fp;
+        if (at((int)ctz64(pend), cp, cs)) {
+          ++c_ent;
+          lane_entry(cp, cs, ek, ev, ef, er);
+          if (entry_hit(ek, ev, ef, er, k)) {
+            val = ev;
+            done = true;
+            hit = fp || pairs;
+          }
         }
         pend &= pend - 1;
       }
-      // not found: a fingerprint lane takes the summary walk below (absent
-      // key or stale copy); a summary lane's leaf does not hold k, unless
-      // this was a tie's optimistic leaf (k may lie below its lowest fence:
-      // walk again from the safe start)
+      // not found: a fingerprint or pair lane takes the summary walk below
+      // (absent key or stale copy); a summary lane's leaf does not hold k,
+      // unless this was a tie's optimistic leaf (k may lie below its lowest
+      // fence: walk again from the safe start)
       if (!done && inleaf) {
         if (alt) {
           ptr = alt;

@@ -111,10 +111,15 @@ void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s);
 // recorded in hint (same entry count, same tree) instead of the root
 // sum (nullable): the leaf summaries; an entry whose prefix lies inside one
 // leaf then carries that leaf's fingerprints (layout.h kDirFp)
+// pairs: build the pair form (layout.h kDirPairs) instead of the
+// fingerprint form: the leaf lists here, then the pairs by launch_dir_pairs
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
                      uint32_t* hint, int from_hint, const uint8_t* sum, uint32_t* err,
-                     hipStream_t s);
+                     hipStream_t s, int pairs = 0);
+// the pairs of a pair-form directory: one wave per page of [1, n_pages)
+void launch_dir_pairs(const uint8_t* arena, uint64_t n_pages, uint16_t node, uint64_t dir_lo,
+                      uint32_t shift, uint64_t n_ent, uint64_t* dir, hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.

@@ -85,6 +85,14 @@ static_assert(kSumOffFp + kLeafCardinality <= kSumBytes, "summary line");
 // word flag: the entry is in fingerprint form (device_common.h dir_fp_cand)
 constexpr uint64_t kDirWords = 8;
 constexpr uint32_t kDirFp = 0x100u;
+// pair form (a read phase's build, leafdir.hip k_dir_pairs): the leaf list
+// of the first 32 B stays valid, and bytes 32..63 list up to kDirPairMax
+// (fingerprint, slot | leaf << 6) u16 pairs of the keys inside the prefix;
+// the pair count in bits 16..23 of the count word; kDirPairsBad: a key of
+// the prefix was found in a leaf the list does not name (not usable)
+constexpr uint32_t kDirPairs = 0x200u;
+constexpr uint32_t kDirPairsBad = 0x400u;
+constexpr uint32_t kDirPairMax = 16;
 SHM_HD uint32_t key_fp(uint64_t k) {
   const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56);
   return f ? f : 1u;

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
                                                   uint64_t* __restrict__ dir,
                                                   uint32_t* __restrict__ hint, int from_hint,
                                                   const uint8_t* __restrict__ sum,
-                                                  uint32_t* err) {
+                                                  uint32_t* err, int pairs) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_ent) return;
   const uint64_t lo = dir_lo + (p << shift);
@@ -149,6 +149,14 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
   }
   u32x4* e = reinterpret_cast<u32x4*>(dir + kDirWords * p);
   const uint32_t pg0 = dir_page_index(out[0]);
+  if (pairs && out[7] >= 1) {
+    // the leaf list, pair form: k_dir_pairs adds the prefix's keys
+    e[0] = u32x4{pg0, dir_page_index(out[1]), dir_page_index(out[2]), dir_page_index(out[3])};
+    e[1] = u32x4{t[0], t[1], t[2], (uint32_t)out[7] | kDirPairs};
+    e[2] = u32x4{0u, 0u, 0u, 0u};
+    e[3] = u32x4{0u, 0u, 0u, 0u};
+    return;
+  }
   if (sum && out[7] == 1) {
     // one leaf covers the whole prefix: the entry carries its summary's
     // fingerprints (layout.h kDirFp), so a get of a key it holds reads the
@@ -191,11 +199,63 @@ __global__ __launch_bounds__(256) void k_leaf_dir(const uint8_t* __restrict__ ar
 void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
                      uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
                      uint32_t* hint, int from_hint, const uint8_t* sum, uint32_t* err,
-                     hipStream_t s) {
+                     hipStream_t s, int pairs) {
   if (!n_ent) return;
   hipLaunchKernelGGL(k_leaf_dir, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s, arena,
                      arena_bytes, node, root, dir_lo, shift, n_ent, dir, hint, from_hint, sum,
-                     err);
+                     err, pairs);
+}
+
+// The pair form's pairs (round 5): one wave per page; a leaf's valid entries
+// (value != 0, f == r: the entries a get can find, Tree.cpp:687-697) each
+// add (fingerprint, slot | leaf << 6) to the entry of their key's prefix,
+// leaf = the page's place in that entry's leaf list.  A key in a leaf the
+// list does not name marks the entry unusable (kDirPairsBad); more than
+// kDirPairMax keys leave it unusable as well (the count says so).  A get
+// reads the directory entry and then only the slots whose pair matches its
+// fingerprint: 16 B of candidates for the ~4-9 keys of a prefix instead of
+// the fingerprints of every slot of its leaf (fewer false candidates), and
+// prefixes that span up to four leaves are answered the same way.
+__global__ __launch_bounds__(256) void k_dir_pairs(const uint8_t* __restrict__ arena,
+                                                   uint64_t n_pages, uint16_t node,
+                                                   uint64_t dir_lo, uint32_t shift,
+                                                   uint64_t n_ent, uint64_t* __restrict__ dir) {
+  const int lane = lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  for (uint64_t pi = 1 + (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+       pi < n_pages; pi += nw) {
+    const uint8_t* pg = arena + (pi << 10);
+    if (pg[kOffLevel] != 0 || pg64_b1(pg, 2) != 0) continue;  // a leaf (no leftmost)
+    if (lane >= kLeafCardinality) continue;
+    uint64_t k, v;
+    uint32_t f, r;
+    lane_entry(pg, lane, k, v, f, r);
+    if (v == kValueNull || ((f ^ r) & 0xF) != 0) continue;
+    if (k < dir_lo || ((k - dir_lo) >> shift) >= n_ent) continue;
+    uint32_t* w = reinterpret_cast<uint32_t*>(dir + kDirWords * ((k - dir_lo) >> shift));
+    const uint32_t cw = w[7];
+    if (!(cw & kDirPairs)) continue;
+    const uint32_t n = cw & 0xFFu;
+    const uint32_t me = (uint32_t)pi;
+    uint32_t j = 4;
+    for (uint32_t x = 0; x < n && x < 4; ++x)
+      if (w[x] == me) j = x;
+    if (j == 4) {
+      atomicOr(w + 7, kDirPairsBad);
+      continue;
+    }
+    const uint32_t pos = (atomicAdd(w + 7, 1u << 16) >> 16) & 0xFFu;
+    if (pos < kDirPairMax)
+      reinterpret_cast<uint16_t*>(w + 8)[pos] =
+          (uint16_t)(key_fp(k) | (((uint32_t)lane | (j << 6)) << 8));
+  }
+}
+
+void launch_dir_pairs(const uint8_t* arena, uint64_t n_pages, uint16_t node, uint64_t dir_lo,
+                      uint32_t shift, uint64_t n_ent, uint64_t* dir, hipStream_t s) {
+  if (n_pages <= 1 || !n_ent) return;
+  hipLaunchKernelGGL(k_dir_pairs, dim3(2048), dim3(256), 0, s, arena, n_pages, node, dir_lo,
+                     shift, n_ent, dir);
 }
 
 }  // namespace dev

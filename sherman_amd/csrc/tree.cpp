@@ -130,6 +130,7 @@ struct shm_tree {
   uint32_t* dir_hint = nullptr;  // per prefix: the level-1 / level-2 page on its path
   uint64_t dir_np = 0;
   bool dir_valid = false;
+  bool dir_pairs = false;  // the directory is in pair form (a read phase's build)
   bool hint_ok = false;  // dir_hint holds the last build's pages of this tree
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
@@ -429,7 +430,7 @@ bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
   const bool rp = read_phase(t);
   // a read phase also wants its denser directory, once
-  if (rp && t->dir_bits < dir_bits_for(t, true)) return true;
+  if (rp && (t->dir_bits < dir_bits_for(t, true) || !t->dir_pairs)) return true;
   return t->next_page != t->dir_np && (rp || t->quiet_chunks >= kQuietChunks);
 }
 
@@ -469,9 +470,17 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
     t->dir_bits = bits;
     t->hint_ok = false;
   }
+  // a read phase builds the pair form (layout.h kDirPairs): each prefix's
+  // own keys, a get reads fewer false candidates and prefixes that span
+  // several leaves are answered from the entry as well
+  const bool pairs = read_phase(t);
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
                        t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint,
-                       t->hint_ok ? 1 : 0, t->sum, t->d_err, s);
+                       t->hint_ok ? 1 : 0, t->sum, t->d_err, s, pairs ? 1 : 0);
+  if (pairs)
+    dev::launch_dir_pairs(t->arena, t->next_page, t->cfg.node_id, t->cfg.key_lo,
+                          t->cfg.key_bits - bits, 1ull << bits, t->dir, s);
+  t->dir_pairs = pairs;
   t->dir_np = t->next_page;
   t->dir_valid = true;
   t->hint_ok = true;
