@@ -405,17 +405,17 @@ constexpr uint32_t kQuietChunks = 2;
 // ~76 % of C2's gets find their prefix inside one leaf and are answered from
 // the entry's fingerprints (DESIGN §3 "Fingerprints in the directory";
 // round 4: C2 17803 -> 17978 Mops/s against two per page, C3 / C5
-// unchanged), and eight in a read phase (86 % from the fingerprints, 1 GB at
-// C2's 2^26 keys): round-5 same-box A/B C2 19168 / 19182 -> 19416 / 19379
-// Mops/s, while C3 / C5 (written every step, never in a read phase) measured
-// -7 % to +1 % with eight, so they keep four
+// unchanged; C3 / C5 measured -7 % to +1 % with eight), and sixteen in a
+// read phase, in pair form (every C2 get answered from its entry, 2 GB at
+// C2's 2^26 keys): same box, C2 18200 / 18217 at four, 18941 / 18964 at
+// eight, 19651 / 19685 Mops/s at sixteen (DESIGN §3 "The pair form")
 uint32_t dir_extra_bits(bool read_phase) {
   static const int env = [] {
     const char* e = getenv("SHM_DIR_EXTRA_BITS");
     return e ? atoi(e) : -1;
   }();
-  const int v = env >= 0 ? env : read_phase ? 3 : 2;
-  return (uint32_t)(v > 3 ? 3 : v);
+  const int v = env >= 0 ? env : read_phase ? 4 : 2;
+  return (uint32_t)(v > 4 ? 4 : v);
 }
 bool read_phase(const shm_tree* t) { return t->reads_since_write >= kReadPhase; }
 uint32_t dir_bits_for(const shm_tree* t, bool rp) {
