@@ -325,11 +325,13 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   return v;
 }
 
-// 6 waves per SIMD (<= 80 VGPRs): with the directory's fingerprints a get's
-// chain is two requests, and more gets in flight pay (C2 +2 % against 5,
-// 8 no better; a same-box A/B)
+// 5 waves per SIMD (95 VGPRs, no scratch).  Round 4 capped it at 6 waves
+// (80 VGPRs: C2 +2 % against 5 then); with the pair form and the shared
+// rounds the cap spilled 28-48 B per lane into scratch on the candidate
+// rounds: same box C2 18623 / 18631 and C3 12750 / 12903 at 6 waves against
+// 19572 / 19611 and 14828 / 14986 at 5.
 template <int TPB>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k_get_sum(WalkArgs a) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k_get_sum(WalkArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_top[];  // top_n x (8 + 4) B
   const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
   const uint32_t tn = a.top_n;
@@ -377,62 +379,83 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) void k
       bool pu = false;
       const uint32_t pc = !fpform && pok ? dir_pair_cand(e, k, pu) : 0u;
       const bool sm = !fpform && pok && !pu;
-      // pend: the lane's candidates still to read, lowest first (slots of
-      // its leaf, or pair-form pairs)
-      uint64_t pend = fp ? dir_fp_cand(e, k) : (uint64_t)pc;
-      bool pairs = pu;
-      // candidate bit c -> its page and slot (false: a pair naming a bad page)
-      auto at = [&](int c, const uint8_t*& cp, int& cs) {
-        if (!pairs) {
+      // pend: the lane's candidate slots of its leaf still to read, lowest
+      // first; a pair lane's candidates instead as up to 8 packed bytes
+      // (leaf << 6 | slot) in plist, with the leaves' pages in lpg (the
+      // directory entry itself is dead past this point: held through the
+      // rounds it spilled registers, C3 -15 %)
+      uint64_t pend = fp ? dir_fp_cand(e, k) : 0;
+      uint64_t plist = 0;
+      uint32_t pn = 0;
+      const uint32_t lpg[4] = {e[0].x, e[0].y, e[0].z, e[0].w};
+      if (pu) {
+#pragma unroll
+        for (int j = 0; j < (int)kDirPairMax; ++j) {
+          if (((pc >> j) & 1u) && pn < 8) {
+            uint32_t pgi;
+            int sl;
+            dir_pair_slot(e, j, pgi, sl);
+            const uint32_t leaf = pgi == lpg[0] ? 0u : pgi == lpg[1] ? 1u : pgi == lpg[2] ? 2u : 3u;
+            plist |= (uint64_t)((leaf << 6) | (uint32_t)sl) << (8 * pn);
+            ++pn;
+          }
+        }
+      }
+      // the next candidate -> its page and slot (false: a pair naming a bad
+      // page); pops it
+      const uint8_t* cp = page;
+      int cs = 0;
+      auto next = [&]() -> bool {
+        if (pn == 0) {
           cp = page;
-          cs = c;
+          cs = (int)ctz64(pend);
+          pend &= pend - 1;
           return true;
         }
-        uint32_t pgi;
-        dir_pair_slot(e, c, pgi, cs);
-        const uint64_t ga = dir_page_ga(pgi, a.node);
+        const uint32_t b = (uint32_t)plist & 0xFFu;
+        plist >>= 8;
+        --pn;
+        cs = (int)(b & 63u);
+        const uint32_t li = b >> 6;
+        const uint64_t ga = dir_page_ga(li == 0 ? lpg[0] : li == 1 ? lpg[1] : li == 2 ? lpg[2] : lpg[3],
+                                        a.node);
         cp = a.arena + ga_offset(ga);
         return ptr_ok(ga, a.node, a.arena_bytes);
       };
-      const uint8_t* cp = page;
-      int cs = 0;
       RawEntry r1;
       bool l1 = false;
-      if (pend) {
-        l1 = at((int)ctz64(pend), cp, cs);
+      const bool any1 = pend || pn;
+      if (any1) {
+        l1 = next();
         if (l1) entry_load(cp, cs, r1);
       }
       u32x4 sraw[4];
       if (sm) sum_load(a.sum, off, sraw);
       uint64_t ek, ev;
       uint32_t ef, er;
-      if (pend) {
-        if (l1) {
-          ++c_ent;
-          entry_decode(r1, ek, ev, ef, er);
-          if (entry_hit(ek, ev, ef, er, k)) {
-            val = ev;
-            hit = done = true;
-          }
+      if (any1 && l1) {
+        ++c_ent;
+        entry_decode(r1, ek, ev, ef, er);
+        if (entry_hit(ek, ev, ef, er, k)) {
+          val = ev;
+          hit = done = true;
         }
-        pend &= pend - 1;
       }
       // a summary lane in k's leaf (k >= highest turns right below) joins
       // the candidate rounds
       SumLine sl;
       const bool inleaf = sm && sum_decode(sraw, k, sl) && k < sl.highest;
       if (inleaf) pend = sl.cand;
-      while (!done && pend) {  // one candidate per lane and round, lowest first
-        if (at((int)ctz64(pend), cp, cs)) {
+      while (!done && (pend || pn)) {  // one candidate per lane and round, lowest first
+        if (next()) {
           ++c_ent;
           lane_entry(cp, cs, ek, ev, ef, er);
           if (entry_hit(ek, ev, ef, er, k)) {
             val = ev;
             done = true;
-            hit = fp || pairs;
+            hit = fp || pu;
           }
         }
-        pend &= pend - 1;
       }
       // not found: a fingerprint or pair lane takes the summary walk below
       // (absent key or stale copy); a summary lane's leaf does not hold k,
