@@ -152,7 +152,9 @@ __device__ __forceinline__ void upper_chunk(const UpperArgs& a, WaveLds& L, LvlL
 //             levels and the deletes again alone (idempotent); then the
 //             superblock and its host mirror
 // 4 waves per SIMD (<= 128 VGPRs): two blocks fit a CU.
-__global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(4))) void k_upper(
+// (3 waves per SIMD: 144 VGPRs and no scratch; at 4 the cap spilled 68 B
+// per lane.  One 512-thread block per CU either way; C5 / C3 within noise)
+__global__ __launch_bounds__(kUpT) __attribute__((amdgpu_waves_per_eu(3))) void k_upper(
     UpperArgs a) {
   __shared__ __attribute__((aligned(16))) WaveLds s_l[kUpWaves];
   __shared__ uint32_t s_red[kUpWaves];
