@@ -32,6 +32,9 @@ struct WalkArgs {
   uint32_t dir_shift;
   // GET: map blocks to chunks XCD-contiguously (see get.hip)
   int xcd_remap;
+  // LOCATE: the directory is in pair form (layout.h kDirPairs): the
+  // pair-aware kernel (the fingerprint form's kernel stays as it was)
+  int dir_pairs;
   // GET: page DMAs with the non-temporal policy (nt; streamed once per batch)
   int nt;
   // GET: per-page occupancy bound (nullable -> whole pages are read).  For a

@@ -48,6 +48,7 @@ __device__ __forceinline__ uint64_t g_u64(const uint32_t* p, int d) {
 
 }  // namespace
 
+template <bool PAIRS>
 __device__ __forceinline__ void locate_body(const WalkArgs& a) {
   const uint64_t i = (uint64_t)blockIdx.x * kLocBlock + threadIdx.x;
   const uint64_t n = a.n_dev ? *a.n_dev : a.n;
@@ -68,6 +69,29 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
     // in scratch memory, a store and a load on every op's path)
     ptr = dir_start_e(a.dir, a.dir_lo, a.dir_shift, a.dir_n, a.node, k, ptr, e, fpform, &alt);
     if (!match) alt = 0;
+    // a quiet tree's pair form (layout.h kDirPairs): the prefix's own keys'
+    // slots, in up to four leaves -- an update found there is written in
+    // place like one found through the fingerprints
+    bool pu = false;
+    const uint32_t pc = PAIRS && match && !fpform ? dir_pair_cand(e, k, pu) : 0u;
+    for (uint32_t rest = pc; rest && !slot; rest &= rest - 1) {  // lowest pair first
+      uint32_t pgi;
+      int sl;
+      dir_pair_slot(e, (int)__builtin_ctz(rest), pgi, sl);
+      const uint64_t ga = dir_page_ga(pgi, a.node);
+      if (!ptr_ok(ga, a.node, a.arena_bytes)) continue;
+      uint32_t* pg = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(a.arena + ga_offset(ga)));
+      uint64_t ek, ev;
+      uint32_t ef, er;
+      lane_entry(reinterpret_cast<const uint8_t*>(pg), sl, ek, ev, ef, er);
+      if (ek == k && ev != kValueNull) {
+        const uint32_t nf = ((ef & 0xF) + 1) & 0xF;
+        put_leaf_entry(pg, sl, k, v, (ef & 0xF0) | nf, (er & 0xF0) | nf);
+        slot = 0x80000000u | (uint32_t)sl;
+        out = ga;
+      }
+    }
+    // (not found through the pairs: the summary walk below)
     if (match && fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
       // the prefix lies in one leaf and the entry holds its fingerprints: an
       // op whose key that leaf holds updates it without the summary line (a
@@ -203,11 +227,18 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
   }
 }
 
-__global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) { locate_body(a); }
+// PAIRS: the pair-aware form, for a directory in pair form; the other keeps
+// the fingerprint form's code (and its 82 VGPRs: the pair loop in every
+// locate cost C5 2 %, same box)
+template <bool PAIRS>
+__global__ __launch_bounds__(kLocBlock) void k_locate(WalkArgs a) { locate_body<PAIRS>(a); }
 void launch_locate(const WalkArgs& a, uint64_t n_upper, hipStream_t s) {
   if (n_upper == 0) return;
   const dim3 g((unsigned)((n_upper + kLocBlock - 1) / kLocBlock));
-  hipLaunchKernelGGL(k_locate, g, dim3(kLocBlock), 0, s, a);
+  if (a.dir_pairs)
+    hipLaunchKernelGGL(k_locate<true>, g, dim3(kLocBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_locate<false>, g, dim3(kLocBlock), 0, s, a);
 }
 
 }  // namespace dev

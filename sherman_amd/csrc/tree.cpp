@@ -426,15 +426,20 @@ uint32_t dir_bits_for(const shm_tree* t, bool rp) {
   if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
   return bits;
 }
+// The form of the next build: pairs while no page is added (a read phase,
+// or a write phase whose chunks leave the page count as it is: C3's
+// updates), fingerprints while the tree grows (C5: a pair build reads every
+// leaf, and its pairs go stale with every split).  The form only changes at
+// a rebuild the staleness rules call for anyway (and once when a read phase
+// starts), so sporadic splits cause no rebuilds of their own.
+bool want_pairs(const shm_tree* t) {
+  return read_phase(t) || t->quiet_chunks >= kQuietChunks;
+}
 bool dir_stale(const shm_tree* t) {
   if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
   const bool rp = read_phase(t);
   // a read phase also wants its denser directory, once
   if (rp && (t->dir_bits < dir_bits_for(t, true) || !t->dir_pairs)) return true;
-  // and a write phase its own form again (the locate reads the fingerprint
-  // form, not the pairs; C3 / C5 after a read phase measured 12.4 K against
-  // 14.5 K Mops/s on the pair form)
-  if (!rp && t->dir_pairs) return true;
   return t->next_page != t->dir_np && (rp || t->quiet_chunks >= kQuietChunks);
 }
 
@@ -477,7 +482,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   // a read phase builds the pair form (layout.h kDirPairs): each prefix's
   // own keys, a get reads fewer false candidates and prefixes that span
   // several leaves are answered from the entry as well
-  const bool pairs = read_phase(t);
+  const bool pairs = want_pairs(t);
   dev::launch_leaf_dir(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
                        t->cfg.key_bits - bits, 1ull << bits, t->dir, t->dir_hint,
                        t->hint_ok ? 1 : 0, t->sum, t->d_err, s, pairs ? 1 : 0);
@@ -804,6 +809,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.num_locks = t->cfg.num_locks;
   w.lock_tag = lock_tag;
   set_dir(t, &w.dir, &w.dir_lo, &w.dir_shift, &w.dir_n);
+  w.dir_pairs = w.dir && t->dir_pairs ? 1 : 0;
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
