@@ -1559,3 +1559,54 @@ def test_pending_range_waits_for_its_issue_stream(lib_ok):
     assert np.array_equal(ac.cpu().numpy(), sc.cpu().numpy())
     assert np.array_equal(host(av), host(sv))
     t.close()
+
+
+def test_pair_form_directory_reads_through_stale_pairs(lib_ok):
+    """A read phase builds the pair-form directory (layout.h kDirPairs: each
+    prefix lists its own keys' slots): every get of the current tree is then
+    answered from its entry.  Inserts that split leaves, in-place updates and
+    deletes follow without a rebuild (below the 1/32 growth rule), so the
+    next searches read stale pairs -- moved keys, emptied and overwritten
+    slots, keys the pairs never listed -- and must still equal the oracle
+    (a pair is only a slot to read; a miss takes the summary walk).  The
+    next read phase rebuilds the pairs, and the contents stay exact."""
+    n0 = 1 << 18
+    t = shm.Tree(arena_bytes=512 << 20, max_batch=1 << 18)
+    orc = OracleTree(512 << 20)
+    base = hashed_keys(1, n0 + 1)
+    bv = np.arange(1, n0 + 1, dtype=U64) * U64(2)
+    gpu_insert(t, base, bv)
+    orc.apply_batch(base, bv)
+    rng = np.random.default_rng(23)
+    probe = base[rng.integers(0, n0, 1 << 15)]
+    for _ in range(5):  # four searches without an insert: the read phase
+        gv, gf = gpu_search(t, probe)
+    assert_same(probe, *orc.search_batch(probe), gv, gf)
+    t.profile(False, index_stats=True)
+    gv, gf = gpu_search(t, probe)
+    st = t.index_stats()
+    t.profile(False)
+    assert_same(probe, *orc.search_batch(probe), gv, gf)
+    assert st["dir_fp_hits"] == st["gets"] == probe.size, st  # all from the entries
+    # updates, deletes and splitting inserts, no rebuild in between
+    upd = base[rng.integers(0, n0, 5000)]
+    dele = base[rng.integers(0, n0, 3000)]
+    anchors = base[rng.integers(0, n0, 40)]
+    add = np.unique((anchors[:, None] + np.arange(1, 31, dtype=U64)[None, :]).ravel())
+    add = add[~np.isin(add, base)]
+    k = np.concatenate([upd, dele, add])
+    v = np.concatenate([upd ^ U64(0x5A5A), np.zeros(dele.size, dtype=U64),
+                        np.arange(1, add.size + 1, dtype=U64) * U64(11)])
+    pages = t.stats()["pages_used"]
+    gpu_insert(t, k, v)
+    orc.apply_batch(k, v)
+    assert t.stats()["pages_used"] > pages  # leaves split
+    probe2 = np.concatenate([upd, dele, add, add + U64(1 << 20),
+                             base[rng.integers(0, n0, 20000)]])
+    for _ in range(6):  # stale pairs first, then the next read phase's rebuild
+        gv, gf = gpu_search(t, probe2)
+        assert_same(probe2, *orc.search_batch(probe2), gv, gf)
+    rc, oc = orc.check()
+    assert rc == 0 and t.check()["keys"] == oc["keys"]
+    orc.close()
+    t.close()
