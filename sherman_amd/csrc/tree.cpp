@@ -401,11 +401,10 @@ constexpr uint32_t kReadPhase = 4;
 constexpr uint32_t kQuietChunks = 2;
 
 // Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS
-// overrides both): four 64 B entries per page while the tree is written, so
-// ~76 % of C2's gets find their prefix inside one leaf and are answered from
-// the entry's fingerprints (DESIGN §3 "Fingerprints in the directory";
-// round 4: C2 17803 -> 17978 Mops/s against two per page, C3 / C5
-// unchanged; C3 / C5 measured -7 % to +1 % with eight), and sixteen in a
+// overrides both): eight 64 B entries per page while the tree is written
+// (late round 5, with the shared candidate rounds and a quiet phase's pair
+// form: same box C3 15671 / 15171 -> 15994 / 16078 Mops/s against four, C5
+// unchanged; sixteen no better), and sixteen in a
 // read phase, in pair form (every C2 get answered from its entry, 2 GB at
 // C2's 2^26 keys): same box, C2 18200 / 18217 at four, 18941 / 18964 at
 // eight, 19651 / 19685 Mops/s at sixteen (DESIGN §3 "The pair form")
@@ -414,7 +413,7 @@ uint32_t dir_extra_bits(bool read_phase) {
     const char* e = getenv("SHM_DIR_EXTRA_BITS");
     return e ? atoi(e) : -1;
   }();
-  const int v = env >= 0 ? env : read_phase ? 4 : 2;
+  const int v = env >= 0 ? env : read_phase ? 4 : 3;
   return (uint32_t)(v > 4 ? 4 : v);
 }
 bool read_phase(const shm_tree* t) { return t->reads_since_write >= kReadPhase; }
