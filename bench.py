@@ -131,7 +131,10 @@ def parse():
     p.add_argument("--sync-scans", dest="async_scans", action="store_false",
                    help="c5, N=1: range scans read their total back before the "
                         "batch's inserts are queued (default: async, checked after)")
-    p.add_argument("--profile-steps", type=int, default=10)
+    p.add_argument("--profile-steps", type=int, default=None,
+                   help="steps of the profile pass (default 10; c5: 60, so the "
+                        "leaf directory's rebuild, one per ~52 growing chunks, is "
+                        "averaged over about as many chunks as it serves)")
     p.add_argument("--latency-steps", type=int, default=None,
                    help="steps of the per-batch latency pass (default: --steps)")
     p.add_argument("--streams", type=int, default=2, choices=(1, 2),
@@ -276,6 +279,8 @@ def build_shard(tree, n_keys, world, rank, dev):
 
 def main():
     args = parse()
+    if args.profile_steps is None:
+        args.profile_steps = 60 if args.workload == "c5" else 10
     if args.dir_extra_bits is not None:
         os.environ["SHM_DIR_EXTRA_BITS"] = str(args.dir_extra_bits)
     import torch
