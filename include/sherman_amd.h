@@ -300,8 +300,9 @@ typedef struct shm_index_stats_t {
   uint64_t page_hops;       /* pages walked from their own bytes */
   uint64_t entry_reads;     /* leaf entries read (fingerprint matches) */
   uint64_t hits;            /* queries found */
-  uint64_t dir_fp_hits;     /* found through the directory entry's copy of
-                               the leaf's fingerprints (no summary line) */
+  uint64_t dir_fp_hits;     /* found from the directory entry alone (no
+                               summary line): its copy of the leaf's
+                               fingerprints, or its pair form's slots */
 } shm_index_stats_t;
 int shm_index_stats(shm_tree *t, shm_index_stats_t *out, int reset);
 
