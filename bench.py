@@ -160,6 +160,11 @@ def parse():
                    help="N > 1: route gets / inserts through the C-ABI shard (C++ over "
                         "RCCL, shm_shard_*) or the Python exchange; auto = the C-ABI on "
                         "the nccl backend once it matched the Python route on one batch")
+    p.add_argument("--insert-every", type=int, default=0,
+                   help="c2, N=1: one insert chunk of 2^batch-log2 NEW keys (ids past the "
+                        "preload, value 2 id, so leaves split) after every K get batches; "
+                        "the line then also reports the gets' rate beside the chunks "
+                        "against a pure get pass on the same tree (VERDICT r5 #3)")
     a = p.parse_args()
     if a.steps is None:
         a.steps = 20 if a.workload == "c5" else 200
@@ -318,7 +323,12 @@ def main():
     n_keys = 1 << args.keys_log2
     batch = 1 << args.batch_log2
     dev = torch.device(f"cuda:{local}")
+    assert not args.insert_every or (args.workload == "c2" and world == 1), \
+        "--insert-every is a c2, N = 1 option"
     arena = max(2 << 30, n_keys * 48)
+    if args.insert_every:
+        # room for the chunks of new keys the run inserts (every pass's)
+        arena += n_keys * 48 * 2
     from sherman_amd.shard import shard_range
     sim = world == 1 and args.sim_world > 1
     s_rank, s_world = (args.sim_rank, args.sim_world) if sim else (rank, world)
@@ -350,6 +360,7 @@ def main():
     g.manual_seed(0x5EED0000 + rank)
     vals = torch.empty(batch, dtype=torch.int64, device=dev)
     found = torch.empty(batch, dtype=torch.uint8, device=dev)
+    ins = None  # c2 --insert-every: the chunks of new keys (FreshChunks)
     if args.workload == "c2":
         if world == 1:
             # qi: the ids' positions (keys_local[j] = key(j + 1), value 2 (j + 1))
@@ -387,10 +398,16 @@ def main():
             sx = streams[i % nstr]
             return torch.cuda.stream(sx if sx is not None else torch.cuda.current_stream())
 
+        ins = FreshChunks(tree, n_keys, batch, dev) if args.insert_every else None
+
         def step(i):
             if routes[0] is None:
                 v, f = outs[i % nstr]
                 tree.search_batch(qs[i % N_BATCHES], v, f, stream=streams[i % nstr])
+                if ins is not None and (i + 1) % args.insert_every == 0:
+                    # a chunk of new keys, queued without a host wait; the
+                    # library orders it after both streams' searches
+                    ins.insert(stream=streams[i % nstr])
                 return
             c = seq[0]
             seq[0] += 1
@@ -600,6 +617,11 @@ def main():
     cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
+            # the form the timed steps walk: the read phase's pair-form
+            # directory (built after four searches without an insert,
+            # tree.cpp kReadPhase) -- with --insert-every, the form the
+            # chunks keep current
+            rewarm(tree, dev, seconds=0.0)
             parity = parity_get(qs[0], qi[0], vals, found, step, tree, keys_local, n_keys, g)
         elif args.workload == "c5":
             cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step, n_keys)
@@ -650,6 +672,22 @@ def main():
         cluster_sum = float(cs.item())
     st_end = tree.stats()
     total_ops = batch * args.steps * world
+    if ins is not None:
+        total_ops += batch * (args.steps // args.insert_every)  # the chunks' inserts
+    if parity is not None and args.workload == "c2" and world == 1:
+        # the timed steps' own results: the last batch of each stream holds
+        # exactly what the walk wrote in the timed region
+        checked = 0
+        for i in range(max(0, args.steps - len(outs)), args.steps):
+            v, f = outs[i % len(outs)]
+            want = (qi[i % N_BATCHES] + 1) * 2
+            parity["ok"] = parity["ok"] and bool(torch.equal(v, want)) and bool(f.all())
+            checked += 1
+        parity["timed_batches_checked"] = checked
+        if ins is not None:
+            parity["ok"] = parity["ok"] and ins.check_last()
+            parity["inserted_chunk_checked"] = True
+        log(f"C2 parity incl. the last {checked} timed batches: {parity['ok']}")
     mops = total_ops / elapsed / 1e6
     torch.cuda.synchronize()
     if args.workload == "c2":
@@ -732,6 +770,8 @@ def main():
         idx.update({k + "_per_get": round(idx[k] / g_, 4)
                     for k in ("start_internal", "right_moves", "page_hops", "entry_reads",
                               "dir_fp_hits")})
+    brk = insert_every_breakdown(tree, qs, outs, ins, args.insert_every) if ins is not None else None
+    dirst = tree.dir_stats() if args.start == "dir" else None
     if c1 is not None:
         # C1 on the host cores, after every GPU measurement (the oracle's
         # build has run beside them)
@@ -772,6 +812,12 @@ def main():
             if sim:
                 workload += ", shard %d of %d (no exchange)" % (s_rank, s_world)
             data = "synthetic: key(i)=CityHash64(i)+1, value=2i; uniform queries"
+            if ins is not None:
+                metric = "batched get + insert Mops/s (64M uint64 keys, a chunk of new keys " \
+                         "every %d get batches)" % args.insert_every
+                workload += (", + one 2^%d-key insert chunk of new keys (ids past the preload, "
+                             "value 2 id) after every %d get batches" % (args.batch_log2,
+                                                                        args.insert_every))
         else:
             metric = "mixed get/insert Mops/s (64M uint64 keys, zipf %.2f, %d%% get)" % (
                 args.theta, args.read_ratio)
@@ -861,6 +907,16 @@ def main():
         }
         if idx is not None:
             out["index_stats"] = idx
+        if dirst is not None:
+            # the leaf directory the walk starts from: its form, device
+            # memory and rebuild cost (shm_dir_stats)
+            out["directory"] = {"form": dirst["form"], "entries": dirst["entries"],
+                                "bytes": dirst["bytes"], "builds": dirst["builds"],
+                                "last_build_ms": round(dirst["last_build_ms"], 4),
+                                "total_build_ms": round(dirst["total_build_ms"], 4),
+                                "maintained_by_inserts": bool(dirst["maintained"])}
+        if brk is not None:
+            out["insert_every"] = brk
         if args.workload == "c2":
             step_s = elapsed / args.steps
             rf = out["roofline"]
@@ -1292,15 +1348,23 @@ def parity_get(q, qi, vals, found, step, tree, keys_local, n_keys, g, miss_frac=
     build wrote: query j is key(qi[j] + 1), stored with value 2 (qi[j] + 1),
     so every get must be found with exactly that value (what Tree::search
     returns over the same key stream; the expectation is the key stream's,
-    not the tree's own image).  Then the same batch with ~9 % of its queries
-    replaced by keys that were never stored -- key(i) for ids past the key
-    count, as the reference benchmark's C1 read phase misses ~9 % of its
-    gets (kKeySpace with the modulus, test/benchmark.cpp:43-46) -- each of
-    which must come back not found with value 0 (Tree.cpp:445-448), the rest
-    as above."""
+    not the tree's own image).  The batch runs on the directory form the
+    timed steps walk (the caller reached the read phase first) and its
+    index statistics say how many gets that form answered (dir_fp_hits).
+    Then the same batch with ~9 % of its queries replaced by keys that were
+    never stored -- key(i) for ids past the key count, as the reference
+    benchmark's C1 read phase misses ~9 % of its gets (kKeySpace with the
+    modulus, test/benchmark.cpp:43-46) -- each of which must come back not
+    found with value 0 (Tree.cpp:445-448), the rest as above.  Returns
+    {"ok", "dir_form", "dir_fp_hits_per_get", ...}; main() adds the timed
+    steps' own last batches."""
     import torch
+    form = tree.dir_stats()["form"]
+    tree.profile(False, index_stats=True)
     step(0)
     torch.cuda.synchronize()
+    idx = tree.index_stats()
+    tree.profile(False)
     want = (qi + 1) * 2
     ok = bool(torch.equal(vals, want) and bool(found.all()))
     n = q.numel()
@@ -1319,8 +1383,107 @@ def parity_get(q, qi, vals, found, step, tree, keys_local, n_keys, g, miss_frac=
     tree.synchronize()
     want2 = torch.where(miss, torch.zeros_like(want), want)
     ok = ok and bool(torch.equal(v2, want2)) and bool(torch.equal(f2.bool(), ~miss))
-    log(f"C2 parity: {n} hits + a batch with {m} misses ({m / n:.3f}): {ok}")
-    return ok
+    fp = idx["dir_fp_hits"] / max(idx["gets"], 1)
+    log(f"C2 parity on the {form} directory: {n} hits ({fp:.6f} answered from the entry) + a "
+        f"batch with {m} misses ({m / n:.3f}): {ok}")
+    return {"ok": ok, "dir_form": form, "dir_fp_hits": idx["dir_fp_hits"], "gets": idx["gets"],
+            "dir_fp_hits_per_get": round(fp, 6), "hit_batch": n, "miss_batch_misses": m,
+            "expected": "value 2 id for key(id), the key stream's (test/benchmark.cpp:43-46)"}
+
+
+class FreshChunks:
+    """c2 --insert-every: chunks of keys never stored before, key(i) for ids
+    i past the preload in order, value 2 i (as the build), generated on the
+    device ahead of the passes that insert them (none inside a timed
+    region).  insert() queues the next chunk (shm_insert_batch_async);
+    check_last() searches the last chunk inserted: every key found with its
+    value."""
+
+    def __init__(self, tree, n_keys, batch, dev, ahead=64):
+        self.tree, self.batch, self.dev = tree, batch, dev
+        self.next_id = n_keys + 1
+        self.ready = []
+        self.last = None
+        self.inserted = 0
+        self.fill(ahead)
+
+    def fill(self, n):
+        import torch
+        while len(self.ready) < n:
+            k = torch.empty(self.batch, dtype=torch.int64, device=self.dev)
+            self.tree.gen_keys(self.next_id, self.batch, k)
+            v = torch.arange(self.next_id, self.next_id + self.batch, dtype=torch.int64,
+                             device=self.dev) * 2
+            self.ready.append((k, v))
+            self.next_id += self.batch
+        torch.cuda.synchronize()
+
+    def insert(self, stream=None):
+        if not self.ready:
+            self.fill(8)  # (only past the pre-generated chunks)
+        k, v = self.ready.pop(0)
+        self.tree.insert_batch_async(k, v, stream=stream)
+        self.last = (k, v)
+        self.inserted += 1
+
+    def check_last(self):
+        import torch
+        if self.last is None:
+            return True
+        k, v = self.last
+        out = torch.empty_like(k)
+        f = torch.empty(k.numel(), dtype=torch.uint8, device=k.device)
+        self.tree.search_batch(k, out, f)
+        self.tree.synchronize()
+        ok = bool(torch.equal(out, v)) and bool(f.all())
+        log(f"inserted chunk parity ({k.numel()} new keys): {ok}")
+        return ok
+
+
+def insert_every_breakdown(tree, qs, outs, ins, every, cycles=8):
+    """c2 --insert-every: the gets' rate beside the chunks, one stream, HIP
+    events around each cycle's chunk and its `every` get batches (a
+    directory rebuild a search calls for runs inside its batch's interval),
+    then `cycles` x `every` pure get batches on the same tree the same way.
+    Untimed passes after the timed steps."""
+    import torch
+    v, f = outs[0]
+    ins.fill(cycles)
+    st0 = tree.dir_stats()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * cycles)]
+    for c in range(cycles):
+        ev[3 * c].record()
+        ins.insert()
+        ev[3 * c + 1].record()
+        for j in range(every):
+            tree.search_batch(qs[(c * every + j) % N_BATCHES], v, f)
+        ev[3 * c + 2].record()
+    torch.cuda.synchronize()
+    ins_ms = sum(ev[3 * c].elapsed_time(ev[3 * c + 1]) for c in range(cycles))
+    get_ms = sum(ev[3 * c + 1].elapsed_time(ev[3 * c + 2]) for c in range(cycles))
+    st1 = tree.dir_stats()
+    pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    pe[0].record()
+    for j in range(cycles * every):
+        tree.search_batch(qs[j % N_BATCHES], v, f)
+    pe[1].record()
+    torch.cuda.synchronize()
+    pure_ms = pe[0].elapsed_time(pe[1])
+    gets = cycles * every * qs[0].numel()
+    mix = gets / (get_ms * 1e-3) / 1e6
+    pure = gets / (pure_ms * 1e-3) / 1e6
+    return {"every": every, "cycles": cycles,
+            "get_mops_beside_inserts": round(mix, 1), "get_mops_pure": round(pure, 1),
+            "ratio": round(mix / pure, 4),
+            "insert_ms_per_chunk": round(ins_ms / cycles, 4),
+            "get_ms_per_batch_beside_inserts": round(get_ms / (cycles * every), 4),
+            "get_ms_per_batch_pure": round(pure_ms / (cycles * every), 4),
+            "dir_builds_in_cycles": st1["builds"] - st0["builds"],
+            "dir_form": st1["form"],
+            "condition": "one stream; HIP events around each chunk and around its get batches "
+                         "(directory rebuilds the searches call for included); pure = the same "
+                         "number of get batches after the cycles, same tree"}
 
 
 def c5_model(tree, n_keys, dev):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 9
+#define SHM_ABI_VERSION 10
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -305,6 +305,27 @@ typedef struct shm_index_stats_t {
                                fingerprints, or its pair form's slots */
 } shm_index_stats_t;
 int shm_index_stats(shm_tree *t, shm_index_stats_t *out, int reset);
+
+/* The leaf directory the batched get starts from (the role of the
+ * reference's IndexCache, include/IndexCache.h:59-259, whose size and hit
+ * counts Tree::index_cache_statistics reports, include/Tree.h:62): its form,
+ * the device memory it holds and what its rebuilds cost.  Synchronises with
+ * the last rebuild's end (not with other work). */
+typedef struct shm_dir_stats_t {
+  uint32_t form;              /* 0 none, 1 leaf lists + fingerprints, 2 pair form */
+  uint32_t bits;              /* log2 of the entries of the current build */
+  uint64_t entries;           /* 2^bits entries of 64 B */
+  uint64_t bytes;             /* device bytes held: the allocation (never shrunk)
+                                 + the level hints */
+  uint64_t builds;            /* builds so far */
+  uint64_t pages_at_build;    /* tree pages at the last build */
+  uint64_t pages_since_build; /* pages splits added since */
+  double last_build_ms;       /* device time of the last build (-1: none yet) */
+  double total_build_ms;      /* of every build */
+  uint32_t maintained;        /* 1: insert chunks keep the entries current */
+  uint32_t reserved;
+} shm_dir_stats_t;
+int shm_dir_stats(shm_tree *t, shm_dir_stats_t *out);
 
 /* multi-GPU routing helpers (range shards: shard s owns
  * [s * 2^64 / P, (s+1) * 2^64 / P)) ------------------------------------------ */

@@ -88,6 +88,16 @@ class ShmIndexStats(ctypes.Structure):
                                    "entry_reads", "hits", "dir_fp_hits")]
 
 
+class ShmDirStats(ctypes.Structure):
+    _fields_ = [("form", u32), ("bits", u32), ("entries", u64), ("bytes", u64), ("builds", u64),
+                ("pages_at_build", u64), ("pages_since_build", u64),
+                ("last_build_ms", ctypes.c_double), ("total_build_ms", ctypes.c_double),
+                ("maintained", u32), ("reserved", u32)]
+
+
+DIR_FORMS = {0: "none", 1: "fingerprints", 2: "pairs"}
+
+
 class ShmProfile(ctypes.Structure):
     _fields_ = [
         ("calls", u64),
@@ -109,7 +119,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 9  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 10  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -142,6 +152,7 @@ _SIGNATURES = [
     ("shm_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("shm_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ShmProfile), ctypes.c_int]),
     ("shm_index_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmIndexStats), ctypes.c_int]),
+    ("shm_dir_stats", ctypes.c_int, [vp, ctypes.POINTER(ShmDirStats)]),
     ("shm_route_bucket", ctypes.c_int, [vp, vp, u64, u32, vp, vp, vp, vp]),
     ("shm_route_permute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
     ("shm_route_unpermute", ctypes.c_int, [vp, vp, vp, u64, vp, vp]),
@@ -542,6 +553,21 @@ class Tree:
         _check(lib().shm_index_stats(self.h, ctypes.byref(st), 1 if reset else 0), "index_stats")
         return {f: getattr(st, f) for f, _ in ShmIndexStats._fields_}
 
+    def dir_stats(self):
+        """The leaf directory: form ("none" / "fingerprints" / "pairs"),
+        entries, device bytes, builds and their device time (shm_dir_stats)."""
+        st = ShmDirStats()
+        _check(lib().shm_dir_stats(self.h, ctypes.byref(st)), "dir_stats")
+        d = {f: getattr(st, f) for f, _ in ShmDirStats._fields_ if f != "reserved"}
+        d["form"] = DIR_FORMS.get(d["form"], str(d["form"]))
+        return d
+
+    def dir_config(self, maint=None, mem_limit=0):
+        """Test hook (shm__dir_config): directory upkeep by the writers on /
+        off (None: as is) and a byte cap on directory allocations."""
+        _check(_hooks().shm__dir_config(self.h, -1 if maint is None else int(bool(maint)),
+                                        mem_limit), "dir_config")
+
     def profile_read(self, reset=True):
         p = ShmProfile()
         _check(lib().shm_profile_read(self.h, ctypes.byref(p), 1 if reset else 0),
@@ -612,6 +638,7 @@ _HOOKS = [
     ("shm__hog", ctypes.c_int, [u32, u64, vp]),
     ("shm__mark", ctypes.c_int, [u32, vp]),
     ("shm__early_pages", ctypes.c_int, [vp, ctypes.POINTER(u64)]),
+    ("shm__dir_config", ctypes.c_int, [vp, ctypes.c_int, u64]),
 ]
 
 

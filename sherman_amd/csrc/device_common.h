@@ -276,7 +276,13 @@ __device__ __forceinline__ uint64_t dir_start_e(const uint64_t* dir, uint64_t di
   fpform = false;
   if (alt) *alt = 0;
   const uint64_t p = (k - dir_lo) >> dir_shift;
-  if (k < dir_lo || p >= dir_n || k == kKeyMax) return fallback;
+  if (k < dir_lo || p >= dir_n || k == kKeyMax) {
+    // no entry: a zero one (count 0, no form flag), so the callers' pair /
+    // fingerprint decoding of e[] sees no candidates
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = u32x4{0u, 0u, 0u, 0u};
+    return fallback;
+  }
   const u32x4* ep = reinterpret_cast<const u32x4*>(dir + kDirWords * p);
 #pragma unroll
   for (int j = 0; j < 4; ++j) e[j] = ep[j];

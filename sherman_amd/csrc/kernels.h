@@ -230,6 +230,10 @@ struct UpperArgs;
 // by the upsert kernel itself, upsert.hip) or 0 (every split left to k_upper)
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s);
 
+// the directory form an insert chunk's leaf writers keep (UpperArgs.dir_form,
+// dir_upkeep.h)
+constexpr uint32_t kDirFormNone = 0, kDirFormFp = 1, kDirFormPairs = 2;
+
 // the device-driven split propagation (insert.hip)
 struct UpperArgs {
   uint8_t* arena;
@@ -284,6 +288,10 @@ struct UpperArgs {
   // nullable: the directory's level-1 / level-2 path pages (launch_leaf_dir),
   // start pages of parent_of walks
   const uint32_t* dir_hint;
+  // nullable: the same directory, kept current by this chunk's leaf writers
+  // in form dir_form (dir_upkeep.h: 1 fingerprint, 2 pair form)
+  uint64_t* dir_w;
+  uint32_t dir_form;
   // nullable: block 0 records the wall clock (100 MHz) at each phase end,
   // stamps[0] = count (tools/upper_stamps.py)
   uint64_t* stamps;

@@ -132,6 +132,19 @@ struct shm_tree {
   bool dir_valid = false;
   bool dir_pairs = false;  // the directory is in pair form (a read phase's build)
   bool hint_ok = false;  // dir_hint holds the last build's pages of this tree
+  // the allocation: 2^dir_cap_bits entries (a build may use fewer); never
+  // shrunk, so a change of form or phase reallocates nothing
+  uint32_t dir_cap_bits = 0;
+  uint32_t dir_bits_limit = 64;  // an allocation this large failed: not asked again
+  uint64_t dir_mem_limit = 0;    // shm__dir_mem_limit (test hook): bytes, 0 = none
+  // rebuild cost: timing events around each build, read once they completed
+  hipEvent_t dir_ev[2] = {nullptr, nullptr};
+  bool dir_ev_pending = false;
+  uint64_t dir_builds = 0;
+  double dir_last_ms = -1.0, dir_total_ms = 0.0;
+  bool dir_maint = false;    // the writers keep the entries current (dir_maint_enabled)
+  bool dir_off = false;      // no directory could be allocated: walks from the root
+  double dir_debt_ps = 0.0;  // gets' estimated extra cost on shared prefixes since the build
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
   uint64_t* top_keys = nullptr;
@@ -423,24 +436,94 @@ uint32_t dir_bits_for(const shm_tree* t, bool rp) {
   bits += dir_extra_bits(rp);
   if (bits > 25) bits = 25;  // 2 GB of entries at most
   if (bits > t->cfg.key_bits) bits = t->cfg.key_bits;  // one entry per key at most
+  if (bits > t->dir_bits_limit) bits = t->dir_bits_limit;  // a larger allocation failed
   return bits;
 }
 // The form of the next build: pairs while no page is added (a read phase,
 // or a write phase whose chunks leave the page count as it is: C3's
 // updates), fingerprints while the tree grows (C5: a pair build reads every
-// leaf, and its pairs go stale with every split).  The form only changes at
-// a rebuild the staleness rules call for anyway (and once when a read phase
-// starts), so sporadic splits cause no rebuilds of their own.
+// leaf).  The form only changes at a rebuild the staleness rules call for
+// anyway (and once when a read phase starts), so sporadic splits cause no
+// rebuilds of their own.
 bool want_pairs(const shm_tree* t) {
   return read_phase(t) || t->quiet_chunks >= kQuietChunks;
 }
+
+// Directory upkeep by the writers (SHM_DIR_MAINT, default on, VERDICT r5
+// #3): an insert chunk keeps the entries it affects current -- a new key in
+// an empty slot adds its pair (pair form) or its fingerprint (fingerprint
+// form) to its prefix's entry, and every page a split writes rewrites the
+// entries of the prefixes that lie wholly inside its fences (one leaf, its
+// keys' slots) and leaves the one or two prefixes it shares with a
+// neighbour to the summary walk (kDirPairsBad / kDirFp cleared).  The
+// directory then goes stale only by those shared prefixes, about two per
+// page a split adds, and by density (the tree doubling); a rebuild is
+// bought when the gets' estimated extra cost on the shared prefixes has
+// reached the measured cost of one build (ski rental: at most twice the
+// best offline choice).  SHM_DIR_MAINT=0: the writers leave the directory
+// alone and round 5's rules rebuild it (growth by 1/32, every read phase
+// after a change).
+bool dir_maint_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SHM_DIR_MAINT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// a get that starts at a shared prefix reads the leaf's summary line: about
+// one 128 B request more than an exact entry's (2.18 requests per get at
+// C2, 51 ps per get at 19.5 G gets/s: DESIGN §3)
+constexpr double kSharedPrefixGetPs = 25.0;
+// the cost of a build before one was measured: 100 ps per entry (k_leaf_dir
+// + k_dir_pairs at 2^25 entries: 3.1-3.4 ms, profiles/r05)
+constexpr double kBuildPsPerEntry = 100.0;
+
+double dir_build_ps(const shm_tree* t) {
+  return t->dir_last_ms > 0 ? t->dir_last_ms * 1e9 : kBuildPsPerEntry * (double)(1ull << t->dir_bits);
+}
+// the estimated fraction of prefixes left to the summary walk since the
+// last build: two per page added
+double dir_shared_frac(const shm_tree* t) {
+  if (!t->dir_valid || t->next_page <= t->dir_np) return 0.0;
+  const double f = 2.0 * (double)(t->next_page - t->dir_np) / (double)(1ull << t->dir_bits);
+  return f < 1.0 ? f : 1.0;
+}
+
 bool dir_stale(const shm_tree* t) {
-  if (!t->dir_valid || t->next_page > t->dir_np + t->dir_np / 32) return true;
+  if (t->dir_off) return false;
+  if (!t->dir_valid) return true;
   const bool rp = read_phase(t);
+  if (t->dir_maint) {
+    if (want_pairs(t) && !t->dir_pairs) return true;   // the form a read / quiet phase wants
+    if (dir_bits_for(t, rp) > t->dir_bits) return true;  // a read phase's density, or the tree doubled
+    return t->next_page != t->dir_np && t->dir_debt_ps >= dir_build_ps(t);
+  }
+  if (t->next_page > t->dir_np + t->dir_np / 32) return true;
   // a read phase also wants its denser directory, once
   if (rp && (t->dir_bits < dir_bits_for(t, true) || !t->dir_pairs)) return true;
   return t->next_page != t->dir_np && (rp || t->quiet_chunks >= kQuietChunks);
 }
+
+// a search of n keys: its estimated extra cost on the shared prefixes
+void dir_note_gets(shm_tree* t, uint64_t n) {
+  if (t->dir_maint) t->dir_debt_ps += (double)n * dir_shared_frac(t) * kSharedPrefixGetPs;
+}
+
+// the last build's device time once its end event completed (wait: block
+// for it)
+int dir_poll(shm_tree* t, bool wait) {
+  if (!t->dir_ev_pending) return SHM_OK;
+  const hipError_t q = wait ? hipEventSynchronize(t->dir_ev[1]) : hipEventQuery(t->dir_ev[1]);
+  if (q == hipErrorNotReady) return SHM_OK;
+  HIP_OK(q);
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, t->dir_ev[0], t->dir_ev[1]));
+  t->dir_last_ms = ms;
+  t->dir_total_ms += ms;
+  t->dir_ev_pending = false;
+  return SHM_OK;
+}
+
 
 // The look-back kernels' block-index counters (lookback_index): the
 // ordering's bin prefix (k_bin_unique: 256 blocks, one per CU; two ranks on
@@ -454,7 +537,52 @@ uint32_t* lb_ctr(shm_tree* t, int which) {
   return which == dev::kLbSeg ? nullptr : t->ctl->lb_ids[which];
 }
 
+// The directory's allocation holds 2^bits entries (+ the level hints);
+// never shrunk.  A larger one is allocated before the old one is freed, and
+// when it cannot be had the tree keeps the directory it has, at its size
+// (ADVICE r5): dir_bits_limit then caps every later build, so the failed
+// allocation is not tried again.  No directory at all: progressively smaller
+// ones, and at the last the gets walk from the root.
+int dir_alloc(shm_tree* t, uint32_t bits, hipStream_t s) {
+  if (t->dir && bits <= t->dir_cap_bits) return SHM_OK;
+  for (;;) {
+    const uint64_t ent = 1ull << bits;
+    const uint64_t bytes = ent * (8 * kDirWords) + ent * 8;  // entries + 2 u32 hints
+    uint64_t* nd = nullptr;
+    uint32_t* nh = nullptr;
+    bool ok = !(t->dir_mem_limit && bytes > t->dir_mem_limit);
+    if (ok && dalloc(&nd, kDirWords * ent)) ok = false;
+    if (ok && dalloc(&nh, 2 * ent)) {
+      (void)hipFree(nd);
+      ok = false;
+    }
+    if (ok) {
+      if (t->dir) {  // the old directory's last readers are ordered before s
+        HIP_OK(hipStreamSynchronize(s));
+        HIP_OK(hipFree(t->dir));
+        HIP_OK(hipFree(t->dir_hint));
+      }
+      t->dir = nd;
+      t->dir_hint = nh;
+      t->dir_cap_bits = bits;
+      t->hint_ok = false;
+      return SHM_OK;
+    }
+    (void)hipGetLastError();  // clear the failed allocation's sticky status
+    if (t->dir) {
+      t->dir_bits_limit = t->dir_cap_bits;
+      return SHM_OK;  // keep what we have
+    }
+    if (bits <= 10) {
+      t->dir_off = true;  // no directory: the walks start at the root
+      return SHM_OK;
+    }
+    t->dir_bits_limit = --bits;
+  }
+}
+
 int refresh_dir(shm_tree* t, hipStream_t s) {
+  if (const int rc = dir_poll(t, false)) return rc;
   if (!dir_stale(t)) return SHM_OK;
   static const bool trace = [] {
     const char* e = getenv("SHM_TRACE_DIR");
@@ -462,22 +590,22 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   }();
   if (trace)
     fprintf(stderr, "sherman_amd: leaf directory rebuild: pages %llu (last build %llu), %u reads "
-            "since the last insert\n", (unsigned long long)t->next_page,
-            (unsigned long long)t->dir_np, t->reads_since_write);
-  const uint32_t bits = dir_bits_for(t, read_phase(t));
-  if (!t->dir || bits != t->dir_bits) {
-    if (t->dir) {
-      HIP_OK(hipStreamSynchronize(s));
-      HIP_OK(hipFree(t->dir));
-      HIP_OK(hipFree(t->dir_hint));
-      t->dir = nullptr;
-      t->dir_hint = nullptr;
-    }
-    if (dalloc(&t->dir, kDirWords << bits)) return SHM_ENOMEM;  // 64 B per entry
-    if (dalloc(&t->dir_hint, 2ull << bits)) return SHM_ENOMEM;  // levels 1, 2
-    t->dir_bits = bits;
-    t->hint_ok = false;
+            "since the last insert, debt %.1f us\n", (unsigned long long)t->next_page,
+            (unsigned long long)t->dir_np, t->reads_since_write, t->dir_debt_ps * 1e-6);
+  uint32_t bits = dir_bits_for(t, read_phase(t));
+  if (const int rc = dir_alloc(t, bits, s)) return rc;
+  if (t->dir_off) {
+    t->dir_valid = false;
+    return SHM_OK;
   }
+  if (bits > t->dir_cap_bits) bits = t->dir_cap_bits;
+  if (bits != t->dir_bits) t->hint_ok = false;  // the hints are laid out by entry count
+  t->dir_bits = bits;
+  // the previous build's time first (its events are reused)
+  if (const int rc = dir_poll(t, true)) return rc;
+  for (hipEvent_t& e : t->dir_ev)
+    if (!e) HIP_OK(hipEventCreate(&e));  // timing events (a rebuild is rare)
+  HIP_OK(hipEventRecord(t->dir_ev[0], s));
   // a read phase builds the pair form (layout.h kDirPairs): each prefix's
   // own keys, a get reads fewer false candidates and prefixes that span
   // several leaves are answered from the entry as well
@@ -488,10 +616,14 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   if (pairs)
     dev::launch_dir_pairs(t->arena, t->next_page, t->cfg.node_id, t->cfg.key_lo,
                           t->cfg.key_bits - bits, 1ull << bits, t->dir, s);
+  HIP_OK(hipEventRecord(t->dir_ev[1], s));
+  t->dir_ev_pending = true;
+  ++t->dir_builds;
   t->dir_pairs = pairs;
   t->dir_np = t->next_page;
   t->dir_valid = true;
   t->hint_ok = true;
+  t->dir_debt_ps = 0.0;
   return SHM_OK;
 }
 
@@ -856,6 +988,10 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.n_del = cnt + 1;
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
+  if (u.dir && t->dir_maint) {  // the chunk's leaf writers keep the entries (dir_upkeep.h)
+    u.dir_w = t->dir;
+    u.dir_form = t->dir_pairs ? dev::kDirFormPairs : dev::kDirFormFp;
+  }
   u.stamps = t->stamps;
   u.force_abort = (t->force_flags & 1u) ? 1u : 0u;
   u.no_direct = (t->force_flags & 2u) ? 1u : 0u;
@@ -1028,6 +1164,8 @@ void free_all(shm_tree* t) {
     if (pd.ev) (void)hipEventDestroy(pd.ev);
   for (auto& m : t->gws_m)
     if (m.ev) (void)hipEventDestroy(m.ev);
+  for (hipEvent_t e : t->dir_ev)
+    if (e) (void)hipEventDestroy(e);
   if (t->h_pin) (void)hipHostFree(t->h_pin);
   if (t->stream) (void)hipStreamDestroy(t->stream);
 }
@@ -1235,6 +1373,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   if (!t->cfg.sort_bits || t->cfg.sort_bits > 64) t->cfg.sort_bits = kDefaultSortBits;
   if (t->cfg.key_bits == 0) t->cfg.key_bits = 64;
   if (t->cfg.key_bits == 64) t->cfg.key_lo = 0;
+  t->dir_maint = dir_maint_enabled();
   auto fail = [&](int rc) {
     free_all(t);
     delete t;
@@ -1377,6 +1516,7 @@ int shm_search_batch(shm_tree* t, const uint64_t* keys, uint64_t n,
   Order ord(t, s, false);
   if (t->reads_since_write < kReadPhase) ++t->reads_since_write;
   if (use_leaf_dir(t)) {
+    dir_note_gets(t, n);
     if (dir_stale(t)) ord.make_exclusive();  // the rebuild rewrites what searches read
     const int rc = ord.rc ? ord.rc : refresh_dir(t, s);
     if (rc) return rc;
@@ -1488,6 +1628,7 @@ int shm_mixed_batch(shm_tree* t, const uint64_t* get_keys, uint64_t n_get, uint6
   Order ord(t, s, true);
   if (ord.rc) return ord.rc;
   if (use_leaf_dir(t)) {
+    dir_note_gets(t, n_get);
     const int rc = refresh_dir(t, s);
     if (rc) return rc;
   }
@@ -1981,6 +2122,36 @@ int shm_index_stats(shm_tree* t, shm_index_stats_t* out, int reset) {
   out->hits = v[dev::kIdxHits];
   out->dir_fp_hits = v[dev::kIdxDirFp];
   if (reset) HIP_OK(hipMemset(t->idx_stats, 0, sizeof(v)));
+  return SHM_OK;
+}
+
+int shm_dir_stats(shm_tree* t, shm_dir_stats_t* out) {
+  if (!t || !out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  memset(out, 0, sizeof(*out));
+  if (const int rc = dir_poll(t, true)) return rc;
+  mirror(t);
+  out->form = !t->dir_valid ? 0u : t->dir_pairs ? 2u : 1u;
+  out->bits = t->dir_valid ? t->dir_bits : 0u;
+  out->entries = t->dir_valid ? 1ull << t->dir_bits : 0ull;
+  out->bytes = t->dir ? (1ull << t->dir_cap_bits) * (8 * kDirWords + 8) : 0ull;
+  out->builds = t->dir_builds;
+  out->pages_at_build = t->dir_np;
+  out->pages_since_build = t->next_page > t->dir_np ? t->next_page - t->dir_np : 0ull;
+  out->last_build_ms = t->dir_last_ms;
+  out->total_build_ms = t->dir_total_ms;
+  out->maintained = t->dir_maint ? 1u : 0u;
+  return SHM_OK;
+}
+
+// test hook: directory upkeep on / off for this tree (maint < 0: as is) and
+// a cap on the bytes a directory allocation may take (0: none), as a device
+// short of memory would impose
+int shm__dir_config(shm_tree* t, int maint, uint64_t mem_limit) {
+  if (!t) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (maint >= 0) t->dir_maint = maint != 0;
+  t->dir_mem_limit = mem_limit;
   return SHM_OK;
 }
 

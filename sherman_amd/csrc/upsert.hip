@@ -232,7 +232,11 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         // the leaf summary: an overwrite keeps its key's fingerprint; a new
         // key in an empty slot sets it (one partial line write per page
         // that gained keys, none for pure updates)
-        if (fresh[j]) set_leaf_fp(a.sum, ga_offset(qpage), ebase + j, ek[j]);
+        if (fresh[j]) {
+          set_leaf_fp(a.sum, ga_offset(qpage), ebase + j, ek[j]);
+          // and the key's directory entry (dir_upkeep.h)
+          dir_note_new(u, ek[j], (uint32_t)(ga_offset(qpage) >> 10), ebase + j);
+        }
       }
   }
   if (a.leaf_hw) {

@@ -61,8 +61,18 @@ def test_c2_full_size_get_parity(lib_ok):
     q = keys[qi]
     v = torch.empty_like(q)
     f = torch.empty(b, dtype=torch.uint8, device="cuda")
+    # the form the bench's timed steps walk: the read phase's pair-form
+    # directory (four searches without an insert, tree.cpp kReadPhase)
+    for _ in range(4):
+        t.search_batch(q, v, f)
+    t.profile(False, index_stats=True)
     t.search_batch(q, v, f)
     t.synchronize()
+    idx = t.index_stats()
+    t.profile(False)
+    d = t.dir_stats()
+    assert d["form"] == "pairs" and d["entries"] == 1 << 25, d
+    assert idx["gets"] == b and idx["dir_fp_hits"] == b, idx  # every get from its entry
     want = (qi + 1) * 2
     assert bool(f.all()), int((f == 0).sum())
     assert torch.equal(v, want), int((v != want).sum())
@@ -78,6 +88,31 @@ def test_c2_full_size_get_parity(lib_ok):
     want2 = torch.where(miss, torch.zeros_like(want), want)
     assert torch.equal(v, want2), int((v != want2).sum())
     assert torch.equal(f.bool(), ~miss)
+    # split-heavy chunks of new keys at full size (key(i) for ids past 2^26,
+    # value 2i), then gets before any rebuild: the chunks' leaf writers kept
+    # the pair-form entries (dir_upkeep.h), so every stored key is still
+    # answered exactly -- old, new and their moved slots -- with no rebuild
+    builds = d["builds"]
+    pages = t.stats()["pages_used"]
+    nk = torch.empty(4 << 20, dtype=torch.int64, device="cuda")
+    t.gen_keys(n + 1, nk.numel(), nk)
+    nv = torch.arange(n + 1, n + 1 + nk.numel(), device="cuda", dtype=torch.int64) * 2
+    for c in range(0, nk.numel(), 1 << 20):
+        t.insert_batch(nk[c:c + (1 << 20)], nv[c:c + (1 << 20)])
+    assert t.stats()["pages_used"] > pages + 10000  # leaves split
+    t.profile(False, index_stats=True)
+    t.search_batch(q, v, f)  # the old keys
+    t.synchronize()
+    assert torch.equal(v, want) and bool(f.all())
+    sel = torch.randint(0, nk.numel(), (b,), device="cuda", generator=g)
+    t.search_batch(nk[sel], v, f)  # the new ones
+    t.synchronize()
+    idx = t.index_stats()
+    t.profile(False)
+    assert torch.equal(v, nv[sel]) and bool(f.all())
+    d2 = t.dir_stats()
+    assert d2["builds"] == builds and d2["form"] == "pairs", d2
+    assert idx["dir_fp_hits"] >= 0.95 * idx["gets"], idx
     t.close()
 
 
