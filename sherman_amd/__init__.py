@@ -639,6 +639,7 @@ _HOOKS = [
     ("shm__mark", ctypes.c_int, [u32, vp]),
     ("shm__early_pages", ctypes.c_int, [vp, ctypes.POINTER(u64)]),
     ("shm__dir_config", ctypes.c_int, [vp, ctypes.c_int, u64]),
+    ("shm__shard_force_route", ctypes.c_int, [vp, ctypes.c_int]),
 ]
 
 
@@ -708,6 +709,12 @@ class CShard:
             self.close()
         except Exception:
             pass
+
+    def force_route(self, on=True):
+        """Test hook (shm__shard_force_route): every get and insert takes the
+        routed path through the transport even at world 1 (RCCL sends each
+        run to this rank itself)."""
+        _check(_hooks().shm__shard_force_route(self.h, 1 if on else 0), "force_route")
 
     def search(self, keys, vals_out, found_out, stream=None):
         _check(lib().shm_shard_search(self.h, _ptr(keys), keys.numel(), _ptr(vals_out),

@@ -146,6 +146,9 @@ int ensure(T*& p, uint64_t& cap, uint64_t need, hipStream_t s) {
 // ---- transports ---------------------------------------------------------------
 struct Xport {
   uint32_t P = 1, rank = 0;
+  // a2a_peers also exchanges this rank's own part with itself (shm__shard_
+  // force_route: a world-1 shard's routed path through the transport)
+  bool self_too = false;
   virtual ~Xport() = default;
   virtual int group_start() { return SHM_OK; }
   virtual int group_end() { return SHM_OK; }
@@ -175,10 +178,10 @@ struct RcclXport : Xport {
     return nccl_ok(ncclAllToAll(send, recv, count, nccl_type(eb), comm, s), "ncclAllToAll");
   }
   int a2a_peers(const void* send, void* recv, uint64_t count, int eb, hipStream_t s) override {
-    if (P == 1 || count == 0) return SHM_OK;
+    if ((P == 1 && !self_too) || count == 0) return SHM_OK;
     NCCL_OK(ncclGroupStart());
     for (uint32_t p = 0; p < P; ++p) {
-      if (p == rank) continue;
+      if (p == rank && !self_too) continue;
       NCCL_OK(ncclSend(static_cast<const char*>(send) + (uint64_t)p * count * eb, count,
                        nccl_type(eb), (int)p, comm, s));
       NCCL_OK(ncclRecv(static_cast<char*>(recv) + (uint64_t)p * count * eb, count, nccl_type(eb),
@@ -305,7 +308,7 @@ struct LocalXport : Xport {
     m.send = static_cast<const char*>(send);
     m.count = count;
     return run(m, s, [&](uint32_t p, const LocalGroup::Post& q) {
-      if (!count || p == rank) return 0;
+      if (!count || (p == rank && !self_too)) return 0;
       return hipMemcpyAsync(static_cast<char*>(recv) + (uint64_t)p * count * eb,
                             q.send + (uint64_t)rank * count * eb, count * eb,
                             hipMemcpyDeviceToDevice, s) != hipSuccess ? 1 : 0;
@@ -421,6 +424,11 @@ struct shm_shard {
   ExclCtx ex;
   hipStream_t side = nullptr;     // read-backs that wait on an event
   shm::dev::ShardBounds bnd{};
+  // shm__shard_force_route: even at world 1 every get and insert takes the
+  // routed path -- slot placement, the exchange through the transport (each
+  // rank's own run included, so RCCL sends it to itself), the local batch,
+  // the results back, the gather -- as at world > 1
+  bool force_route = false;
 };
 
 namespace {
@@ -702,10 +710,11 @@ int shm_shard_search_begin(shm_shard* h, const uint64_t* keys, uint64_t n, void*
   // the P - 1 peers' runs cross the collective (none at P = 1)
   const uint32_t me = h->rank;
   s.busy = true;
-  if (P == 1) return SHM_OK;  // nothing to route: _end is the local get
+  if (P == 1 && !h->force_route) return SHM_OK;  // nothing to route: _end is the local get
+  // (forced: the own run crosses the transport like the peers')
   shm::dev::launch_route_slots(s.keys, s.n, P, s.ncap, s.cw, s.pk, s.spos, s.ovk, s.ovi,
                                shm__error_word(h->local), s.stream, me,
-                               s.pr + (uint64_t)me * s.ncap);
+                               h->force_route ? nullptr : s.pr + (uint64_t)me * s.ncap);
   HIP_OK2(hipGetLastError());
   RC_OK(s.x->group_start());
   RC_OK(s.x->a2a_peers(s.pk, s.pr, s.ncap, 8, s.stream));
@@ -722,13 +731,14 @@ int shm_shard_search_end(shm_shard* h, uint32_t ticket, uint64_t* vals_out, uint
   s.busy = false;
   const uint32_t P = h->world;
   // one shard: the batch is all this rank's, searched where it lies
-  if (P == 1) return shm_search_batch(h->local, s.keys, s.n, vals_out, found_out, s.stream);
+  if (P == 1 && !h->force_route)
+    return shm_search_batch(h->local, s.keys, s.n, vals_out, found_out, s.stream);
   RC_OK(shm_search_batch(h->local, s.pr, (uint64_t)P * s.ncap, s.pv, nullptr, s.stream));
   // the results go back the way the keys came, slot for slot; the own run's
-  // are gathered straight from the local results
+  // are gathered straight from the local results (forced: exchanged as well)
   RC_OK(s.x->a2a_peers(s.pv, s.pb, s.ncap, 8, s.stream));
   shm::dev::launch_route_gather(s.pb, s.spos, s.n, vals_out, found_out, s.stream, h->rank, s.ncap,
-                                s.pv);
+                                h->force_route ? nullptr : s.pv);
   HIP_OK2(hipGetLastError());
   return get_overflow(h, s, vals_out, found_out);
 }
@@ -752,10 +762,12 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   // synchronising call), as a local insert rejects its chunk
   RC_OK(shm__route_bucket_insert(h->local, keys, n, P, e.icnt, e.kb, e.perm, s));
   RC_OK(shm_route_permute(h->local, vals, e.perm, n, e.vb, s));
-  // this rank's own run is packed straight into its receive slot
+  // this rank's own run is packed straight into its receive slot (forced:
+  // it crosses the transport like the peers')
   const uint64_t mine = (uint64_t)h->rank * e.icap;
-  shm::dev::launch_route_pack(e.kb, e.vb, e.icnt, P, e.icap, e.pk, e.pv, s, h->rank, e.rk + mine,
-                              e.rv + mine);
+  const bool fr = h->force_route;
+  shm::dev::launch_route_pack(e.kb, e.vb, e.icnt, P, e.icap, e.pk, e.pv, s, h->rank,
+                              fr ? nullptr : e.rk + mine, fr ? nullptr : e.rv + mine);
   HIP_OK2(hipGetLastError());
   RC_OK(e.x->group_start());
   RC_OK(e.x->a2a_peers(e.pk, e.rk, e.icap, 8, s));
@@ -763,7 +775,7 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   RC_OK(e.x->a2a_peers(e.icnt, e.icnt + P, 1, 8, s));
   RC_OK(e.x->group_end());
   HIP_OK2(hipEventRecord(e.ev_ins, s));
-  e.pending = P > 1;
+  e.pending = P > 1 || fr;
   e.pstream = s;
   return shm__insert_batch_padded(h->local, e.rk, e.rv, (uint64_t)P * e.icap, s);
 }
@@ -866,6 +878,17 @@ int shm__route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint
   if (n && (!in || !spos || !vals_out)) return SHM_EINVAL;
   shm::dev::launch_route_gather(in, spos, n, vals_out, found_out, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+}
+
+// (3) The routed path at world 1 (force_route above): every call through the
+// transport, RCCL sending each run to this rank itself (tests/test_gpu_shard.py
+// [nccl-1-routed]), so ncclSend / ncclRecv run on a one-GPU box.
+int shm__shard_force_route(shm_shard* h, int on) {
+  if (!h) return SHM_EINVAL;
+  h->force_route = on != 0;
+  for (Xport* x : h->xp)
+    if (x) x->self_too = on != 0;
+  return SHM_OK;
 }
 
 // (2) An in-process group of P shard handles on one device (P trees, one host

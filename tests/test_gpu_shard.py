@@ -10,8 +10,14 @@ routed gets with misses, routed range scans across shard boundaries).
   * world 2 over "gloo" with CUDA tensors: two ranks, two trees sharing the
     GPU, each built with its shard's key-range hint, a real two-way exchange;
   * world 1 through the C-ABI shard (sherman_amd.CShard, shm_shard_* in
-    csrc/shard.cpp): routed get and insert in C++ over its own RCCL
-    communicators, including two batches in flight (begin, begin, end, end).
+    csrc/shard.cpp): at world 1 its get and insert take the local path (no
+    exchange; a one-shard batch is all the rank's own) and its range scan the
+    1-rank exchange; two batches in flight (begin, begin, end, end);
+  * the same with the routed path forced (shm__shard_force_route, "routed"):
+    slot placement, the key / value / count exchange through grouped
+    ncclSend / ncclRecv (each run sent by the rank to itself), the local
+    batch, the results back and the gather -- every RCCL step of a world > 1
+    get and insert, on the box's one GPU.
 
 One GPU is all a gpurun box has, and RCCL refuses two ranks on one device, so
 the RCCL exchange at world > 1 is covered by the driver's 8-GPU run; its
@@ -35,6 +41,7 @@ U64 = np.uint64
 
 
 def gpu_worker(rank, world, port, outdir, backend, cabi=False):
+    routed = cabi == "routed"
     import sherman_amd as shm
     from sherman_amd.shard import ShardRouter, shard_range
 
@@ -47,6 +54,8 @@ def gpu_worker(rank, world, port, outdir, backend, cabi=False):
     tree = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 14, device=0, node_id=rank,
                     key_lo=lo, key_bits=bits)
     cs = shm.CShard(tree, world, rank, dist) if cabi else None
+    if routed:
+        cs.force_route(True)
     router = ShardRouter(tree, world, dist, cshard=cs)
 
     def d(a):
@@ -103,7 +112,7 @@ def tree_contents(tree):
 
 
 @pytest.mark.parametrize("backend,world,cabi", [("nccl", 1, False), ("gloo", 2, False),
-                                                ("nccl", 1, True)])
+                                                ("nccl", 1, True), ("nccl", 1, "routed")])
 def test_routed_gpu_shards_match_unsharded_oracle(backend, world, cabi):
     assert torch.cuda.is_available(), "GPU test without a GPU"
     with tempfile.TemporaryDirectory() as d:
