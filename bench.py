@@ -160,6 +160,9 @@ def parse():
                    help="N > 1: route gets / inserts through the C-ABI shard (C++ over "
                         "RCCL, shm_shard_*) or the Python exchange; auto = the C-ABI on "
                         "the nccl backend once it matched the Python route on one batch")
+    p.add_argument("--page-check", type=int, default=0, choices=(0, 1),
+                   help="1 = SHM_FLAG_PAGE_CHECK: the get walk also checks the page-level "
+                        "version of every page it takes a value from (DESIGN §3.5)")
     p.add_argument("--insert-every", type=int, default=0,
                    help="c2, N=1: one insert chunk of 2^batch-log2 NEW keys (ids past the "
                         "preload, value 2 id, so leaves split) after every K get batches; "
@@ -336,10 +339,11 @@ def main():
     # N > 1: a rank receives ~batch routed keys (+ a few %), keep one chunk
     tree = shm.Tree(arena_bytes=arena, max_batch=max(1 << 20, batch + (batch >> 2 if world > 1 else 0)), device=local,
                     node_id=rank, sort_gets={"on": True, "off": False}.get(args.sort, "auto"), key_lo=key_lo, key_bits=key_bits,
-                    leaf_dir=args.start == "dir", top_lds=args.start == "lds")
+                    leaf_dir=args.start == "dir", top_lds=args.start == "lds",
+                    page_check=bool(args.page_check))
 
     c1 = None
-    if world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
+    if world == 1 and args.workload == "c2" and not args.no_cpu_baseline and not args.insert_every:
         # the reference benchmark's tree, one insert at a time on a host
         # thread while the GPU work runs (cpu_baseline_c1)
         c1 = C1Build()
@@ -614,7 +618,7 @@ def main():
             return [c3_main if c3_pipe else torch.cuda.current_stream()]
 
     # ---- CPU baseline (rank 0, N = 1): oracle on host cores, same tree -----
-    cpu = parity = None
+    cpu = parity = fresh_ms = None
     if world == 1 and not args.no_cpu_baseline:
         if args.workload == "c2":
             # the form the timed steps walk: the read phase's pair-form
@@ -623,6 +627,8 @@ def main():
             # chunks keep current
             rewarm(tree, dev, seconds=0.0)
             parity = parity_get(qs[0], qi[0], vals, found, step, tree, keys_local, n_keys, g)
+            if ins is not None:
+                fresh_ms = pure_get_ms(tree, qs, outs, 64)  # before any chunk of new keys
         elif args.workload == "c5":
             cpu, parity = cpu_baseline_c5(tree, mixed, scan_out, args, step, n_keys)
         else:
@@ -770,7 +776,8 @@ def main():
         idx.update({k + "_per_get": round(idx[k] / g_, 4)
                     for k in ("start_internal", "right_moves", "page_hops", "entry_reads",
                               "dir_fp_hits")})
-    brk = insert_every_breakdown(tree, qs, outs, ins, args.insert_every) if ins is not None else None
+    brk = (insert_every_breakdown(tree, qs, outs, ins, args.insert_every, fresh_ms=fresh_ms)
+           if ins is not None else None)
     dirst = tree.dir_stats() if args.start == "dir" else None
     if c1 is not None:
         # C1 on the host cores, after every GPU measurement (the oracle's
@@ -1447,7 +1454,22 @@ class FreshChunks:
         return ok
 
 
-def insert_every_breakdown(tree, qs, outs, ins, every, cycles=8):
+def pure_get_ms(tree, qs, outs, batches):
+    """ms per get batch of `batches` batches on one stream (HIP events
+    around the run): the pure-get reference of --insert-every."""
+    import torch
+    v, f = outs[0]
+    torch.cuda.synchronize()
+    pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    pe[0].record()
+    for j in range(batches):
+        tree.search_batch(qs[j % N_BATCHES], v, f)
+    pe[1].record()
+    torch.cuda.synchronize()
+    return pe[0].elapsed_time(pe[1]) / batches
+
+
+def insert_every_breakdown(tree, qs, outs, ins, every, cycles=8, fresh_ms=None):
     """c2 --insert-every: the gets' rate beside the chunks, one stream, HIP
     events around each cycle's chunk and its `every` get batches (a
     directory rebuild a search calls for runs inside its batch's interval),
@@ -1470,17 +1492,11 @@ def insert_every_breakdown(tree, qs, outs, ins, every, cycles=8):
     ins_ms = sum(ev[3 * c].elapsed_time(ev[3 * c + 1]) for c in range(cycles))
     get_ms = sum(ev[3 * c + 1].elapsed_time(ev[3 * c + 2]) for c in range(cycles))
     st1 = tree.dir_stats()
-    pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    pe[0].record()
-    for j in range(cycles * every):
-        tree.search_batch(qs[j % N_BATCHES], v, f)
-    pe[1].record()
-    torch.cuda.synchronize()
-    pure_ms = pe[0].elapsed_time(pe[1])
+    pure_ms = pure_get_ms(tree, qs, outs, cycles * every) * cycles * every
     gets = cycles * every * qs[0].numel()
     mix = gets / (get_ms * 1e-3) / 1e6
     pure = gets / (pure_ms * 1e-3) / 1e6
-    return {"every": every, "cycles": cycles,
+    out = {"every": every, "cycles": cycles,
             "get_mops_beside_inserts": round(mix, 1), "get_mops_pure": round(pure, 1),
             "ratio": round(mix / pure, 4),
             "insert_ms_per_chunk": round(ins_ms / cycles, 4),
@@ -1490,7 +1506,13 @@ def insert_every_breakdown(tree, qs, outs, ins, every, cycles=8):
             "dir_form": st1["form"],
             "condition": "one stream; HIP events around each chunk and around its get batches "
                          "(directory rebuilds the searches call for included); pure = the same "
-                         "number of get batches after the cycles, same tree"}
+                         "number of get batches after the cycles, same tree; pure_fresh = the "
+                         "same measure on the C2 tree before any chunk (the pure C2 rate)"}
+    if fresh_ms:
+        fresh = qs[0].numel() / (fresh_ms * 1e-3) / 1e6
+        out["get_mops_pure_fresh"] = round(fresh, 1)
+        out["ratio_vs_fresh"] = round(mix / fresh, 4)
+    return out
 
 
 def c5_model(tree, n_keys, dev):

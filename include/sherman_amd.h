@@ -63,6 +63,13 @@ extern "C" {
                                     reordered unless SHM_FLAG_SORT_GETS: the
                                     leaf-summary walk reads ~3 lines per get
                                     and ordering never pays */
+#define SHM_FLAG_PAGE_CHECK 0x10u /* the batched get also checks the page-level
+                                    version (front == rear, Tree.h:241-261) of
+                                    every page it takes a value from, and
+                                    reports a torn page as SHM_EIO; off by
+                                    default: gets never overlap writers
+                                    (exclusive calls), and it costs two lines
+                                    per get */
 #define SHM_FLAG_TOP_LDS 0x8u    /* without SHM_FLAG_LEAF_DIR: gets start from
                                     an LDS replica of the top of the tree (the
                                     pages of the deepest upper level that fits

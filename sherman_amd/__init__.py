@@ -29,6 +29,7 @@ SHM_FLAG_SORT_GETS = 0x1
 SHM_FLAG_LEAF_DIR = 0x2
 SHM_FLAG_AUTO_SORT_GETS = 0x4
 SHM_FLAG_TOP_LDS = 0x8
+SHM_FLAG_PAGE_CHECK = 0x10
 
 KEY_MAX = (1 << 64) - 1
 PAGE_SIZE = 1024
@@ -319,7 +320,7 @@ class Tree:
 
     def __init__(self, arena_bytes=1 << 30, max_batch=1 << 20, device=0,
                  node_id=0, sort_gets="auto", num_locks=None, sort_bits=16,
-                 key_lo=0, key_bits=64, leaf_dir=True, top_lds=False):
+                 key_lo=0, key_bits=64, leaf_dir=True, top_lds=False, page_check=False):
         L = lib()
         cfg = ShmConfig()
         _check(L.shm_config_init(ctypes.byref(cfg)), "config")
@@ -337,7 +338,8 @@ class Tree:
         cfg.flags = ((SHM_FLAG_SORT_GETS if sort_gets is True else 0) |
                      (SHM_FLAG_AUTO_SORT_GETS if sort_gets == "auto" else 0) |
                      (SHM_FLAG_LEAF_DIR if leaf_dir else 0) |
-                     (SHM_FLAG_TOP_LDS if top_lds else 0))
+                     (SHM_FLAG_TOP_LDS if top_lds else 0) |
+                     (SHM_FLAG_PAGE_CHECK if page_check else 0))
         h = vp()
         _check(L.shm_tree_create(ctypes.byref(cfg), ctypes.byref(h)), "shm_tree_create")
         self.h = h
@@ -568,6 +570,14 @@ class Tree:
         _check(_hooks().shm__dir_config(self.h, -1 if maint is None else int(bool(maint)),
                                         mem_limit), "dir_config")
 
+    def dir_verify(self):
+        """Diagnostics (shm__dir_verify): every directory entry the walks
+        trust checked against the tree as it is now."""
+        out = (u64 * 8)()
+        _check(_hooks().shm__dir_verify(self.h, out), "dir_verify")
+        return {"checked": out[0], "bad_lists": out[1], "bad_pairs": out[2], "bad_fps": out[3],
+                "first_bad": [x - 1 for x in out[4:8] if x]}
+
     def profile_read(self, reset=True):
         p = ShmProfile()
         _check(lib().shm_profile_read(self.h, ctypes.byref(p), 1 if reset else 0),
@@ -640,6 +650,7 @@ _HOOKS = [
     ("shm__early_pages", ctypes.c_int, [vp, ctypes.POINTER(u64)]),
     ("shm__dir_config", ctypes.c_int, [vp, ctypes.c_int, u64]),
     ("shm__shard_force_route", ctypes.c_int, [vp, ctypes.c_int]),
+    ("shm__dir_verify", ctypes.c_int, [vp, ctypes.POINTER(u64)]),
 ]
 
 

@@ -12,7 +12,10 @@
 //     914-950) rewrites the entries of the prefixes holding its keys that lie
 //     wholly inside its fences -- one leaf, its keys' slots -- and hands the
 //     one or two prefixes it shares with a neighbour to the summary walk
-//     (kDirPairsBad, or kDirFp cleared) (dir_note_split_page).
+//     (kDirPairsBad, or kDirFp cleared) (dir_note_split_page);
+//   * an entry neither rule keeps exact (a shared prefix, a new key whose
+//     leaf its list does not name) is marked kDirFix and listed, and after
+//     the chunk k_dir_repair (leafdir.hip) rebuilds it from the tree.
 // Every entry a get trusts still only names slots to read: a get that does
 // not find its key there walks the summary path (get.hip), so the upkeep is
 // about cost, never about results.  Prefixes of a split page without keys
@@ -36,6 +39,28 @@ __device__ __forceinline__ uint32_t* dir_entry_w(uint64_t* dir, uint64_t lo, uin
 // (dir_fp_cand's placement: 24 at bytes 4..27, 30 at 32..61)
 __device__ __forceinline__ int dir_fp_byte(int s) { return s < 24 ? 4 + s : 8 + s; }
 
+// prefix p for k_dir_repair after the chunk (once: the caller saw kDirFix
+// clear in the count word its atomic returned)
+__device__ __forceinline__ void dir_fix_later(const UpperArgs& u, uint64_t p) {
+  if (!u.dir_fix) return;
+  const uint32_t i = atomicAdd(u.dir_fix_n + u.par, 1u);
+  if (i < u.dir_fix_cap) u.dir_fix[i] = (uint32_t)p;
+}
+
+// an entry this chunk cannot keep exact: left to the summary walk until the
+// repair after the chunk rewrites it (bad pairs, fingerprints off, listed)
+__device__ __forceinline__ void dir_note_stale(const UpperArgs& u, uint32_t* w, uint64_t p) {
+  const uint32_t cw = w[7];
+  if (cw & kDirFix) return;  // listed already
+  const uint32_t old = atomicOr(w + 7, kDirFix | ((cw & kDirPairs) ? kDirPairsBad : 0u));
+  if (old & kDirFp) atomicAnd(w + 7, ~kDirFp);
+  if (!(old & kDirFix)) dir_fix_later(u, p);
+}
+
+__device__ __forceinline__ uint64_t dir_prefix(const UpperArgs& u, const uint32_t* w) {
+  return (uint64_t)(reinterpret_cast<const uint64_t*>(w) - u.dir_w) / kDirWords;
+}
+
 // key k was stored in the empty slot s of leaf page index pg (one lane)
 __device__ __forceinline__ void dir_note_new(const UpperArgs& u, uint64_t k, uint32_t pg, int s) {
   uint32_t* w = u.dir_w ? dir_entry_w(u.dir_w, u.dir_lo, u.dir_shift, u.dir_n, k) : nullptr;
@@ -48,8 +73,8 @@ __device__ __forceinline__ void dir_note_new(const UpperArgs& u, uint64_t k, uin
     int j = -1;
     for (uint32_t x = 0; x < nl && x < 4; ++x)
       if (w[x] == pg) j = (int)x;
-    if (j < 0) {  // a leaf the list does not name (k_dir_pairs' rule)
-      atomicOr(w + 7, kDirPairsBad);
+    if (j < 0) {  // a leaf the list does not name (k_dir_pairs' rule): repair
+      dir_note_stale(u, w, dir_prefix(u, w));
       return;
     }
     const uint32_t pos = (atomicAdd(w + 7, 1u << 16) >> 16) & 0xFFu;
@@ -57,24 +82,15 @@ __device__ __forceinline__ void dir_note_new(const UpperArgs& u, uint64_t k, uin
       reinterpret_cast<uint16_t*>(w + 8)[pos] =
           (uint16_t)(key_fp(k) | (((uint32_t)s | ((uint32_t)j << 6)) << 8));
     else
-      atomicOr(w + 7, kDirPairsBad);  // past the list: unusable for good
+      atomicOr(w + 7, kDirPairsBad);  // more keys than pairs: unusable (as a build leaves it)
   } else if (u.dir_form == kDirFormFp && (cw & kDirFp)) {
     if (w[0] == pg)
       reinterpret_cast<uint8_t*>(w)[dir_fp_byte(s)] = (uint8_t)key_fp(k);
     else
-      atomicAnd(w + 7, ~kDirFp);  // the prefix reached another leaf
+      dir_note_stale(u, w, dir_prefix(u, w));  // the prefix reached another leaf
   }
 }
 
-// a prefix shared with a neighbour page: left to the summary walk
-__device__ __forceinline__ void dir_note_shared(const UpperArgs& u, uint32_t* w) {
-  const uint32_t cw = w[7];
-  if (cw & kDirPairs) {
-    if (!(cw & kDirPairsBad)) atomicOr(w + 7, kDirPairsBad);
-  } else if (cw & kDirFp) {
-    atomicAnd(w + 7, ~kDirFp);
-  }
-}
 
 // One wave: the split wrote leaf page index pg with fences [lowest, highest)
 // and c keys, key (sorted) in lane = slot < c.  Rewrites every entry of a
@@ -113,8 +129,8 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
     uint32_t* w = reinterpret_cast<uint32_t*>(u.dir_w + kDirWords * p);
     const uint64_t a = lo + (p << sh);
     const bool inside = lowest <= a && highest - 1 >= a + span;
-    if (!inside) {
-      if (lane == 0) dir_note_shared(u, w);
+    if (!inside) {  // shared with a neighbour: repaired after the chunk
+      if (lane == 0) dir_note_stale(u, w, p);
       continue;
     }
     const uint32_t cnt = (uint32_t)popc64(m);
@@ -140,6 +156,76 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
       if (lane == 7) v = 1u | kDirFp;
     }
     if (lane < 16) w[lane] = v;
+  }
+  // the prefixes inside the fences that hold none of the page's keys: their
+  // entries may still name the page the split took them from, so they are
+  // written too (one leaf, no pairs / the page's fingerprints), one prefix
+  // per lane -- an exact entry must never place a new key in the wrong leaf
+  // (locate.hip's exact shortcut)
+  const uint64_t lo_k = lowest > lo ? lowest : lo;
+  if (highest - 1 < lo || ((lo_k - lo) >> sh) >= u.dir_n) return;
+  const uint64_t pf = (lo_k - lo) >> sh;
+  uint64_t pe = ((highest - 1) - lo) >> sh;
+  if (pe >= u.dir_n) pe = u.dir_n - 1;
+  // the two prefixes at the fences, when they reach past them, even without
+  // a key of the page: their leaf lists may name the page the split took
+  // the range from (the last page's right end was the old page's), and an
+  // exact entry's list must name the leaf of every key of its prefix
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint64_t q = e == 0 ? pf : pe;
+      const uint64_t a = lo + (q << sh);
+      if (!(lowest <= a && highest - 1 >= a + span))
+        dir_note_stale(u, reinterpret_cast<uint32_t*>(u.dir_w + kDirWords * q), q);
+    }
+  }
+  // the keys inside the directory's range: lanes [k0, k0 + nk), sorted
+  const uint64_t km = ballot(mine);
+  const uint32_t nk = (uint32_t)popc64(km);
+  const uint32_t k0 = km ? (uint32_t)ctz64(km) : 0u;
+  // the entry body every such prefix gets, words 0..15 from lanes 0..15
+  uint32_t body[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) body[x] = shfl32(fpw, x);
+  body[0] = pg;
+  if (u.dir_form == kDirFormPairs) {
+#pragma unroll
+    for (int x = 1; x < 16; ++x) body[x] = 0u;
+    body[7] = 1u | kDirPairs;
+  } else {
+    body[7] = 1u | kDirFp;
+  }
+  for (uint64_t base = pf; base <= pe; base += kWave) {
+    const uint64_t p = base + (uint64_t)lane;
+    bool todo_p = p <= pe;
+    if (todo_p) {
+      const uint64_t a = lo + (p << sh);
+      todo_p = lowest <= a && highest - 1 >= a + span;
+    }
+    // does a key of the page lie in prefix p?  (binary search over the
+    // sorted prefixes of lanes [k0, k0 + nk); every lane takes part in the
+    // exchanges)
+    uint32_t l = k0, h = k0 + nk;
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      const uint32_t mid = (l + h) >> 1;
+      const uint64_t pm = shfl64(pk, (int)(mid < 63 ? mid : 63));
+      if (l < h) {
+        if (pm < p)
+          l = mid + 1;
+        else
+          h = mid;
+      }
+    }
+    const uint64_t pl = shfl64(pk, (int)(l < 63 ? l : 63));
+    const bool has = l < k0 + nk && pl == p;
+    if (todo_p && !has) {
+      uint32_t* w = reinterpret_cast<uint32_t*>(u.dir_w + kDirWords * p);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) w[x] = body[x];
+    }
+    if (base + kWave < base) break;  // (no wrap)
   }
 }
 

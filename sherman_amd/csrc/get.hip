@@ -330,7 +330,12 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 // rounds the cap spilled 28-48 B per lane into scratch on the candidate
 // rounds: same box C2 18623 / 18631 and C3 12750 / 12903 at 6 waves against
 // 19572 / 19611 and 14828 / 14986 at 5.
-template <int TPB>
+// PCHK (SHM_FLAG_PAGE_CHECK): the page-level version check on the fast
+// path too -- a hit read from a page's entry also reads that page's
+// front_version (byte 8) and rear_version (byte 1016) and reports a
+// mismatch (kErrInconsistent: check_consistent, Tree.h:241-261, Tree.cpp:
+// 616-618); two more lines per get (DESIGN §3.5 measures it)
+template <int TPB, bool PCHK>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k_get_sum(WalkArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_top[];  // top_n x (8 + 4) B
   const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
@@ -351,6 +356,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
   uint32_t err = 0;
   uint32_t c_int = 0, c_right = 0, c_hops = 0, c_ent = 0;
   bool hit = false;
+  uint32_t pv_f = 0, pv_r = 0;  // PCHK: the hit page's front / rear versions
   if (k != kKeyMax) {  // never stored (root highest is exclusive, Tree.h:150)
     uint64_t ptr = a.root;
     uint64_t alt = 0;  // a tie's safe start (dir_start_e)
@@ -379,6 +385,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
       bool pu = false;
       const uint32_t pc = !fpform && pok ? dir_pair_cand(e, k, pu) : 0u;
       const bool sm = !fpform && pok && !pu;
+      // an exact directory (built, then kept by every insert chunk since):
+      // a usable entry names every key of its prefix, so a key it does not
+      // lead to is absent -- no summary walk for a miss (a tie at a split
+      // point, or more matching pairs than the lane queues, walks anyway)
+      const bool exact_miss = a.dir_exact && ((fpform && pok) || (pu && alt == 0 &&
+                                                                  __builtin_popcount(pc) <= 8));
       // pend: the lane's candidate slots of its leaf still to read, lowest
       // first; a pair lane's candidates instead as up to 8 packed bytes
       // (leaf << 6 | slot) in plist, with the leaves' pages in lpg (the
@@ -439,6 +451,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (entry_hit(ek, ev, ef, er, k)) {
           val = ev;
           hit = done = true;
+          if (PCHK) {
+            pv_f = cp[kOffFrontVer];
+            pv_r = cp[kOffLeafRear];
+          }
         }
       }
       // a summary lane in k's leaf (k >= highest turns right below) joins
@@ -454,9 +470,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
             val = ev;
             done = true;
             hit = fp || pu;
+            if (PCHK) {
+              pv_f = cp[kOffFrontVer];
+              pv_r = cp[kOffLeafRear];
+            }
           }
         }
       }
+      if (!done && exact_miss) done = true;  // absent (val stays 0)
       // not found: a fingerprint or pair lane takes the summary walk below
       // (absent key or stale copy); a summary lane's leaf does not hold k,
       // unless this was a tie's optimistic leaf (k may lie below its lowest
@@ -513,6 +534,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
           lane_entry(page, ctz64(cand), ek, ev, ef, er);
           if (entry_hit(ek, ev, ef, er, k)) {
             val = ev;
+            if (PCHK) {
+              pv_f = page[kOffFrontVer];
+              pv_r = page[kOffLeafRear];
+            }
             break;
           }
           cand &= cand - 1;
@@ -597,6 +622,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
       for (int j = 0; j < kIdxStats; ++j)
         if (v[j]) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + j), v[j]);
   }
+  if (PCHK && pv_f != pv_r) err |= kErrInconsistent;  // a torn page under a get
   if (err) atomicOr(a.err, err);
   if (act) {
     a.out_val[i] = val;
@@ -612,7 +638,12 @@ void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s) {
   if (n == 0) return;
   constexpr int TPB = kGetSumTPB;
   const size_t lds = (size_t)a.top_n * 12;
-  hipLaunchKernelGGL(k_get_sum<TPB>, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds, s, a);
+  if (a.page_check)
+    hipLaunchKernelGGL((k_get_sum<TPB, true>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds,
+                       s, a);
+  else
+    hipLaunchKernelGGL((k_get_sum<TPB, false>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB),
+                       lds, s, a);
 }
 
 // ---- the top of the tree for the LDS replica ---------------------------------

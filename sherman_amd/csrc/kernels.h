@@ -35,6 +35,14 @@ struct WalkArgs {
   // LOCATE: the directory is in pair form (layout.h kDirPairs): the
   // pair-aware kernel (the fingerprint form's kernel stays as it was)
   int dir_pairs;
+  // the directory is exact (built, then kept by every insert chunk since:
+  // dir_upkeep.h): a usable entry's fingerprints / pairs name every key of
+  // its prefix, so a key they do not lead to is absent, and its leaf is the
+  // entry's (LOCATE: a new key needs no summary walk)
+  int dir_exact;
+  // GET (k_get_sum): the page-level version check on every hit
+  // (SHM_FLAG_PAGE_CHECK)
+  int page_check;
   // GET: page DMAs with the non-temporal policy (nt; streamed once per batch)
   int nt;
   // GET: per-page occupancy bound (nullable -> whole pages are read).  For a
@@ -123,6 +131,18 @@ void launch_leaf_dir(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, 
 // the pairs of a pair-form directory: one wave per page of [1, n_pages)
 void launch_dir_pairs(const uint8_t* arena, uint64_t n_pages, uint16_t node, uint64_t dir_lo,
                       uint32_t shift, uint64_t n_ent, uint64_t* dir, hipStream_t s);
+// rebuild the entries an insert chunk listed (fix[0 .. fix_n[par]), at most
+// cap) from the tree, in form `form` (kDirForm*); zeroes fix_n[par ^ 1]; the
+// repairs past cap are added to *lost (host memory, nullable)
+void launch_dir_repair(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                       uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
+                       const uint32_t* hint, int form, const uint32_t* fix, uint32_t* fix_n,
+                       uint32_t par, uint32_t cap, uint64_t* lost, uint32_t* err, hipStream_t s);
+// diagnostics: the trusted entries against the tree (k_dir_verify): out = 8
+// words, zeroed by the caller
+void launch_dir_verify(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                       uint64_t dir_lo, uint32_t shift, uint64_t n_ent, const uint64_t* dir,
+                       const uint32_t* hint, unsigned long long* out, hipStream_t s);
 
 // ---- insert pipeline -------------------------------------------------------
 // k_upper runs one block per CU (at most kMaxUpper); its control block.
@@ -179,6 +199,8 @@ struct UpperCtl {
 // UpperArgs.pub word 4: the tag of the last chunk whose k_upper is done with
 // the chunk's op buffers (tree.cpp insert_order's flow control)
 constexpr int kPubApplied = 4;
+// UpperArgs.pub word 6: directory repairs lost so far (k_dir_repair, cumulative)
+constexpr int kPubDirLost = 6;
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
 constexpr uint32_t kSmallSplit = 4;
@@ -292,6 +314,12 @@ struct UpperArgs {
   // in form dir_form (dir_upkeep.h: 1 fingerprint, 2 pair form)
   uint64_t* dir_w;
   uint32_t dir_form;
+  // the chunk's repair list (nullable): prefixes whose entries its writers
+  // could not keep exact, for k_dir_repair after the chunk; dir_fix_n[par]
+  // counts them (past dir_fix_cap they are lost: the entry stays marked)
+  uint32_t* dir_fix;
+  uint32_t* dir_fix_n;
+  uint32_t dir_fix_cap;
   // nullable: block 0 records the wall clock (100 MHz) at each phase end,
   // stamps[0] = count (tools/upper_stamps.py)
   uint64_t* stamps;

@@ -93,6 +93,9 @@ constexpr uint32_t kDirFp = 0x100u;
 constexpr uint32_t kDirPairs = 0x200u;
 constexpr uint32_t kDirPairsBad = 0x400u;
 constexpr uint32_t kDirPairMax = 16;
+// count word flag: an insert chunk's writer listed the entry for repair
+// after the chunk (dir_upkeep.h, leafdir.hip k_dir_repair); the walks ignore it
+constexpr uint32_t kDirFix = 0x800u;
 SHM_HD uint32_t key_fp(uint64_t k) {
   const uint32_t f = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56);
   return f ? f : 1u;

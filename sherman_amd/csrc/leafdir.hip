@@ -258,5 +258,324 @@ void launch_dir_pairs(const uint8_t* arena, uint64_t n_pages, uint16_t node, uin
                      shift, n_ent, dir);
 }
 
+// The entries an insert chunk's writers could not keep exact (dir_upkeep.h:
+// prefixes a split page shares with a neighbour, a new key whose prefix's
+// list does not name its leaf) were marked for the summary walk and listed;
+// after the chunk, one wave per listed prefix rebuilds its entry from the
+// tree exactly as k_leaf_dir (+ k_dir_pairs) would: the leaf holding the
+// prefix's first key (walked from the prefix's level-1 hint, a B-link start
+// that stays valid), the up to four leaves covering the prefix, and in the
+// pair form the (fingerprint, slot | leaf << 6) pairs of their valid entries
+// inside the prefix, in leaf then slot order; in the fingerprint form an
+// entry whose prefix lies in one leaf carries that leaf's fingerprints.
+// fix_n[par] holds the chunk's count (past cap: lost repairs, added to *lost
+// in host memory, which the host reads as staleness); the launch zeroes the
+// next chunk's counter.
+// The exact entry of prefix p as a build would write it (one wave): word
+// `lane` of the 64 B entry in *v for lanes < 16; false when the walk failed
+// (a bad pointer).  In the pair form *np_out = the pair count.
+__device__ __forceinline__ bool dir_exact_entry(const uint8_t* __restrict__ arena,
+                                                uint64_t arena_bytes, uint16_t node, uint64_t root,
+                                                uint64_t dir_lo, uint32_t shift, uint64_t p,
+                                                const uint32_t* __restrict__ hint, int form,
+                                                uint32_t* v_out, uint32_t* np_out,
+                                                bool prefix_fps = false) {
+  const int lane = lane_id();
+  const uint64_t span = (1ull << shift) - 1;
+  const uint32_t sh = shift > 32 ? shift - 32 : 0;
+  const uint64_t lo = dir_lo + (p << shift);
+  const uint64_t hi = lo > ~0ull - span ? ~0ull : lo + span;
+  // lane 0: the leaf holding lo, the leaves covering [lo, hi] (k_leaf_dir)
+  uint64_t pgs[4] = {0, 0, 0, 0}, seps[4] = {0, 0, 0, 0};
+  uint32_t n = 0;
+  uint64_t cover = root;
+  bool ok = false;
+  if (lane == 0) {
+    uint64_t ptr = root;
+    bool hinted = false;
+    if (hint && hint[p]) {
+      ptr = dir_page_ga(hint[p], node);
+      hinted = true;
+    }
+    for (int it = 0; it < 4096; ++it) {
+      if (!ptr_ok(ptr, node, arena_bytes)) break;
+      const uint8_t* pg = arena + ga_offset(ptr);
+      const uint64_t leftmost = pg64_b1(pg, 2);
+      const uint64_t sibling = pg64_b1(pg, 4);
+      const uint64_t highest = pg64(pg, kOffHighest);
+      if (hinted && (leftmost == 0 || pg[kOffLevel] != 1 || lo < pg64(pg, kOffLowest))) {
+        hinted = false;  // not a level-1 page on lo's path any more
+        ptr = root;
+        continue;
+      }
+      if (lo >= highest) {  // turn right (Tree.cpp:626-629)
+        if (sibling == 0) break;
+        ptr = sibling;
+        continue;
+      }
+      if (leftmost != 0) {  // internal: descend towards lo
+        const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
+        const int c = keys_le(pg, cnt, lo);
+        if (hi < highest) cover = ptr;
+        ptr = c == 0 ? leftmost : pg64(pg, kOffRecords + kInternalEntry * (c - 1) + 8);
+        hinted = false;
+        continue;
+      }
+      pgs[0] = ptr;
+      uint64_t h = highest, sib = sibling;
+      n = 1;
+      while (h <= hi && sib != 0 && n <= 4) {
+        if (n == 4 || !ptr_ok(sib, node, arena_bytes)) {
+          n = 5;  // more than four leaves: the covering internal page
+          break;
+        }
+        const uint8_t* sp = arena + ga_offset(sib);
+        pgs[n] = sib;
+        seps[n] = pg64(sp, kOffLowest);
+        h = pg64(sp, kOffHighest);
+        sib = pg64_b1(sp, 4);
+        ++n;
+      }
+      ok = true;
+      break;
+    }
+  }
+  ok = rl32(ok ? 1u : 0u, 0) != 0;
+  n = rl32(n, 0);
+  cover = rl64(cover, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pgs[j] = rl64(pgs[j], 0);
+    seps[j] = rl64(seps[j], 0);
+  }
+  *np_out = 0;
+  if (!ok) return false;
+  uint32_t v = 0;  // word `lane` of the entry (lanes < 16)
+  if (n > 4) {
+    if (lane == 0) v = dir_page_index(cover);  // count 0: start at the covering page
+  } else if (form == kDirFormFp && n == 1) {
+    // the leaf's fingerprints (valid slots; 0 for empty ones)
+    const uint8_t* pg = arena + ga_offset(pgs[0]);
+    uint64_t k = 0, val = 0;
+    uint32_t f = 0, r = 0;
+    if (lane < kLeafCardinality) lane_entry(pg, lane, k, val, f, r);
+    // (prefix_fps: only the slots whose keys lie in the prefix -- what a
+    // get or a locate of a key of this prefix relies on; the copy of the
+    // leaf's other slots only adds candidates)
+    const bool in = !prefix_fps || (k >= lo && k <= hi);
+    const uint32_t fp = lane < kLeafCardinality && val != kValueNull && in ? key_fp(k) : 0u;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int byte = 4 * (lane & 15) + b;
+      const int s = byte >= 4 && byte < 28 ? byte - 4 : byte >= 32 && byte < 62 ? byte - 8 : -1;
+      const uint32_t x = shfl32(fp, s >= 0 ? s : 0);
+      if (s >= 0) v |= (x & 0xFFu) << (8 * b);
+    }
+    if (lane == 0) v = dir_page_index(pgs[0]);
+    if (lane == 7) v = 1u | kDirFp;
+  } else {
+    // the leaf list and its split points (words 0..7)
+    const uint32_t t1 = n > 1 ? (uint32_t)((seps[1] - lo) >> sh) : 0u;
+    const uint32_t t2 = n > 2 ? (uint32_t)((seps[2] - lo) >> sh) : 0u;
+    const uint32_t t3 = n > 3 ? (uint32_t)((seps[3] - lo) >> sh) : 0u;
+    if (lane < 4)
+      v = (uint32_t)lane < n
+              ? dir_page_index(lane == 0 ? pgs[0] : lane == 1 ? pgs[1] : lane == 2 ? pgs[2] : pgs[3])
+              : 0u;
+    if (lane == 4) v = t1;
+    if (lane == 5) v = t2;
+    if (lane == 6) v = t3;
+    uint32_t cw = n;
+    if (form == kDirFormPairs) {
+      // the pairs: leaf j's valid entries inside [lo, hi], leaf then slot order
+      uint32_t np = 0;
+      uint32_t pos[4] = {~0u, ~0u, ~0u, ~0u};  // this lane's (slot's) pair position in leaf j
+      uint32_t pr[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((uint32_t)j >= n) break;
+        const uint8_t* pg = arena + ga_offset(pgs[j]);
+        uint64_t k = 0, val = 0;
+        uint32_t f = 0, r = 0;
+        if (lane < kLeafCardinality) lane_entry(pg, lane, k, val, f, r);
+        const bool in = lane < kLeafCardinality && val != kValueNull && ((f ^ r) & 0xF) == 0 &&
+                        k >= lo && k <= hi;
+        const uint64_t b = ballot(in);
+        if (in) {
+          pos[j] = np + (uint32_t)popc64(b & lanemask_lt());
+          pr[j] = key_fp(k) | (((uint32_t)lane | ((uint32_t)j << 6)) << 8);
+        }
+        np += (uint32_t)popc64(b);
+      }
+      // pair q (q < 16) to lane 8 + q / 2, half q & 1 (positions are dense:
+      // pair q is held by the lane whose pos[j] == q)
+      uint32_t lo16 = 0, hi16 = 0;
+      for (uint32_t q = 0; q < np && q < kDirPairMax; ++q) {
+        uint32_t got = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t b = ballot(pos[j] == q);
+          if (b) got = shfl32(pr[j], ctz64(b));
+        }
+        if (lane == 8 + (int)(q >> 1)) {
+          if (q & 1u)
+            hi16 = got;
+          else
+            lo16 = got;
+        }
+      }
+      if (lane >= 8 && lane < 16) v = (lo16 & 0xFFFFu) | ((hi16 & 0xFFFFu) << 16);
+      cw |= kDirPairs | ((np < 255u ? np : 255u) << 16);
+      *np_out = np;
+    }
+    if (lane == 7) v = cw;
+  }
+  *v_out = v;
+  return true;
+}
+
+// The entries an insert chunk's writers could not keep exact (dir_upkeep.h:
+// prefixes a split page shares with a neighbour, a new key whose prefix's
+// list does not name its leaf) were marked for the summary walk and listed;
+// after the chunk, one wave per listed prefix rebuilds its entry from the
+// tree exactly as k_leaf_dir (+ k_dir_pairs) would (dir_exact_entry): the
+// leaf holding the prefix's first key (walked from the prefix's level-1
+// hint, a B-link start that stays valid), the up to four leaves covering
+// the prefix, and in the pair form the (fingerprint, slot | leaf << 6) pairs
+// of their valid entries inside the prefix, in leaf then slot order; in the
+// fingerprint form an entry whose prefix lies in one leaf carries that
+// leaf's fingerprints.  fix_n[par] holds the chunk's count (past cap: lost
+// repairs, added to *lost in host memory, which the host reads as
+// staleness); the launch zeroes the next chunk's counter.
+__global__ __launch_bounds__(256) void k_dir_repair(const uint8_t* __restrict__ arena,
+                                                    uint64_t arena_bytes, uint16_t node,
+                                                    uint64_t root, uint64_t dir_lo, uint32_t shift,
+                                                    uint64_t n_ent, uint64_t* __restrict__ dir,
+                                                    const uint32_t* __restrict__ hint, int form,
+                                                    const uint32_t* __restrict__ fix,
+                                                    uint32_t* fix_n, uint32_t par, uint32_t cap,
+                                                    uint64_t* lost, uint32_t* err) {
+  const int lane = lane_id();
+  const uint32_t n_fix = fix_n[par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    fix_n[par ^ 1u] = 0;  // the next chunk's list (its writers run after this launch)
+    if (n_fix > cap && lost) {
+      const uint64_t l = __hip_atomic_load(lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(lost, l + (n_fix - cap), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const uint32_t m = n_fix < cap ? n_fix : cap;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  for (uint64_t wi = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); wi < m;
+       wi += nw) {
+    const uint64_t p = fix[wi];
+    if (p >= n_ent) continue;
+    uint32_t* w = reinterpret_cast<uint32_t*>(dir + kDirWords * p);
+    uint32_t v = 0, np = 0;
+    if (!dir_exact_entry(arena, arena_bytes, node, root, dir_lo, shift, p, hint, form, &v, &np)) {
+      if (lane == 0) {  // left to the summary walk from the root; reported
+        atomicOr(err, kErrBadPtr);
+        w[0] = dir_page_index(root);
+        w[7] = 0u;
+      }
+      continue;
+    }
+    if (lane < 16) w[lane] = v;
+  }
+}
+
+// Diagnostics (shm__dir_verify): every entry the walks trust -- a usable
+// pair-form entry, a fingerprint-form entry -- against the exact entry of
+// the tree as it is: out[0] entries checked, out[1] leaf lists or split
+// points that differ, out[2] pair sets that differ, out[3] fingerprint
+// copies that miss a valid slot's fingerprint, out[4..7] the first bad
+// prefixes (+ 1; 0 = none)
+__global__ __launch_bounds__(256) void k_dir_verify(const uint8_t* __restrict__ arena,
+                                                    uint64_t arena_bytes, uint16_t node,
+                                                    uint64_t root, uint64_t dir_lo, uint32_t shift,
+                                                    uint64_t n_ent, const uint64_t* __restrict__ dir,
+                                                    const uint32_t* __restrict__ hint,
+                                                    unsigned long long* out) {
+  const int lane = lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  for (uint64_t p = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); p < n_ent;
+       p += nw) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(dir + kDirWords * p);
+    const uint32_t cw = w[7];
+    const uint32_t npst = (cw >> 16) & 0xFFu;
+    const bool pairs = (cw & kDirPairs) && !(cw & kDirPairsBad) && npst <= kDirPairMax;
+    const bool fp = (cw & kDirFp) != 0;
+    if (!pairs && !fp) continue;
+    uint32_t v = 0, np = 0;
+    const int form = pairs ? kDirFormPairs : kDirFormFp;
+    if (!dir_exact_entry(arena, arena_bytes, node, root, dir_lo, shift, p, hint, form, &v, &np,
+                         true))
+      continue;
+    const uint32_t st = lane < 16 ? w[lane] : 0u;
+    bool bad_list = false, bad_pairs = false, bad_fp = false;
+    if (pairs) {
+      const uint32_t vcw = rl32(v, 7);
+      // leaf count, pages and split points
+      const uint32_t nl = vcw & 0xFFu;
+      const bool used = (lane < 4 && (uint32_t)lane < nl) || (lane >= 4 && lane < 7 && (uint32_t)(lane - 3) < nl);
+      bad_list = ballot(used && st != v) != 0 || nl != (cw & 0xFFu) || (vcw & kDirPairs) == 0;
+      // pair sets: every exact pair stored, same count
+      const uint32_t want = (uint32_t)((vcw >> 16) & 0xFFu);
+      bool miss = false;
+      if (want <= kDirPairMax) {
+        for (uint32_t q = 0; q < want; ++q) {
+          const uint32_t ex = (rl32(v, 8 + (int)(q >> 1)) >> (16 * (q & 1u))) & 0xFFFFu;
+          bool found = false;
+          for (uint32_t x = 0; x < npst; ++x)
+            if (((rl32(st, 8 + (int)(x >> 1)) >> (16 * (x & 1u))) & 0xFFFFu) == ex) found = true;
+          miss = miss || !found;
+        }
+      }
+      // (extra stored pairs -- deleted keys' -- only cost a read; a missing
+      // one would hide a key)
+      bad_pairs = miss || want > kDirPairMax;
+    } else {
+      // the stored fingerprint copy must hold the fingerprint of every valid
+      // slot whose key lies in the prefix, and name the exact leaf
+      const bool one = (rl32(v, 7) & kDirFp) != 0;
+      bad_list = !one || rl32(v, 0) != rl32(st, 0);
+      if (one) {
+        // compare the fingerprint words, masking slots the exact copy has 0
+        const uint32_t ex = lane >= 1 && lane < 16 && lane != 7 ? v : 0u;
+        const uint32_t sv = lane >= 1 && lane < 16 && lane != 7 ? st : 0u;
+        uint32_t mask = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((ex >> (8 * b)) & 0xFFu) mask |= 0xFFu << (8 * b);
+        bad_fp = ballot((ex & mask) != (sv & mask)) != 0;
+      }
+    }
+    if (lane == 0) {
+      atomicAdd(out + 0, 1ull);
+      if (bad_list) atomicAdd(out + 1, 1ull);
+      if (bad_pairs) atomicAdd(out + 2, 1ull);
+      if (bad_fp) atomicAdd(out + 3, 1ull);
+      if (bad_list || bad_pairs || bad_fp)
+        for (int i = 0; i < 4; ++i)
+          if (atomicCAS(out + 4 + i, 0ull, (unsigned long long)p + 1) == 0ull) break;
+    }
+  }
+}
+
+void launch_dir_verify(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                       uint64_t dir_lo, uint32_t shift, uint64_t n_ent, const uint64_t* dir,
+                       const uint32_t* hint, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_dir_verify, dim3(2048), dim3(256), 0, s, arena, arena_bytes, node, root,
+                     dir_lo, shift, n_ent, dir, hint, out);
+}
+
+void launch_dir_repair(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
+                       uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
+                       const uint32_t* hint, int form, const uint32_t* fix, uint32_t* fix_n,
+                       uint32_t par, uint32_t cap, uint64_t* lost, uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_dir_repair, dim3(256), dim3(256), 0, s, arena, arena_bytes, node, root,
+                     dir_lo, shift, n_ent, dir, hint, form, fix, fix_n, par, cap, lost, err);
+}
+
 }  // namespace dev
 }  // namespace shm

@@ -62,6 +62,7 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
   uint64_t out = 0;
   uint32_t slot = 0;
   uint64_t alt = 0;  // a tie's safe start (dir_start_e): an update is found optimistically
+  bool known = false;  // an exact entry placed a new key: out is its leaf, no walk
   if (a.dir && a.target_level == 0) {
     u32x4 e[4];
     bool fpform;
@@ -74,6 +75,9 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
     // place like one found through the fingerprints
     bool pu = false;
     const uint32_t pc = PAIRS && match && !fpform ? dir_pair_cand(e, k, pu) : 0u;
+    // an exact pair entry without the key (and no tie at a split point):
+    // the key is new and belongs to the leaf its split points name
+    known = PAIRS && match && pu && a.dir_exact && alt == 0 && ptr_ok(ptr, a.node, a.arena_bytes);
     for (uint32_t rest = pc; rest && !slot; rest &= rest - 1) {  // lowest pair first
       uint32_t pgi;
       int sl;
@@ -91,7 +95,8 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
         out = ga;
       }
     }
-    // (not found through the pairs: the summary walk below)
+    if (known && !slot) out = ptr;
+    // (not found through the pairs: the summary walk below, unless exact)
     if (match && fpform && ptr_ok(ptr, a.node, a.arena_bytes)) {
       // the prefix lies in one leaf and the entry holds its fingerprints: an
       // op whose key that leaf holds updates it without the summary line (a
@@ -113,9 +118,15 @@ __device__ __forceinline__ void locate_body(const WalkArgs& a) {
         }
         cand &= cand - 1;
       }
+      // an exact fingerprint entry (every slot of the prefix's one leaf)
+      // without the key: a new key of this leaf
+      if (!slot && a.dir_exact) {
+        out = ptr;
+        known = true;
+      }
     }
   }
-  for (int hop = 0; !slot; ++hop) {
+  for (int hop = 0; !slot && !known; ++hop) {
     if (hop > kMaxRounds) {
       err |= kErrLocateHops;
       break;

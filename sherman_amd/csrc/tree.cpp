@@ -143,7 +143,14 @@ struct shm_tree {
   uint64_t dir_builds = 0;
   double dir_last_ms = -1.0, dir_total_ms = 0.0;
   bool dir_maint = false;    // the writers keep the entries current (dir_maint_enabled)
+  // the insert chunks' repair lists (dir_upkeep.h, k_dir_repair): prefix
+  // indices, and a count per chunk parity
+  uint32_t* dir_fix = nullptr;
+  uint32_t* dir_fix_n = nullptr;
+  uint32_t dir_fix_cap = 0;
+  uint64_t dir_lost_at_build = 0;  // the host word kPubDirLost at the last build
   bool dir_off = false;      // no directory could be allocated: walks from the root
+  bool dir_exact = false;    // built with upkeep on, and upkeep on ever since (WalkArgs.dir_exact)
   double dir_debt_ps = 0.0;  // gets' estimated extra cost on shared prefixes since the build
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
@@ -470,9 +477,9 @@ bool dir_maint_enabled() {
   }();
   return on;
 }
-// a get that starts at a shared prefix reads the leaf's summary line: about
-// one 128 B request more than an exact entry's (2.18 requests per get at
-// C2, 51 ps per get at 19.5 G gets/s: DESIGN §3)
+// a get that starts at a stale entry reads the leaf's summary line (and may
+// turn right): about one 128 B request more than an exact entry's (2.18
+// requests per get at C2, 51 ps per get at 19.5 G gets/s: DESIGN §3)
 constexpr double kSharedPrefixGetPs = 25.0;
 // the cost of a build before one was measured: 100 ps per entry (k_leaf_dir
 // + k_dir_pairs at 2^25 entries: 3.1-3.4 ms, profiles/r05)
@@ -481,11 +488,17 @@ constexpr double kBuildPsPerEntry = 100.0;
 double dir_build_ps(const shm_tree* t) {
   return t->dir_last_ms > 0 ? t->dir_last_ms * 1e9 : kBuildPsPerEntry * (double)(1ull << t->dir_bits);
 }
-// the estimated fraction of prefixes left to the summary walk since the
-// last build: two per page added
+// the host word the repair kernel adds its lost repairs to (cumulative)
+uint64_t dir_lost(const shm_tree* t) {
+  return reinterpret_cast<const volatile uint64_t*>(t->h_pin)[kPubWord / 2 + dev::kPubDirLost];
+}
+// the fraction of entries left stale since the last build: the repairs the
+// chunks could not list (k_dir_repair's count past its list)
 double dir_shared_frac(const shm_tree* t) {
-  if (!t->dir_valid || t->next_page <= t->dir_np) return 0.0;
-  const double f = 2.0 * (double)(t->next_page - t->dir_np) / (double)(1ull << t->dir_bits);
+  if (!t->dir_valid) return 0.0;
+  const uint64_t l = dir_lost(t);
+  if (l <= t->dir_lost_at_build) return 0.0;
+  const double f = (double)(l - t->dir_lost_at_build) / (double)(1ull << t->dir_bits);
   return f < 1.0 ? f : 1.0;
 }
 
@@ -496,7 +509,7 @@ bool dir_stale(const shm_tree* t) {
   if (t->dir_maint) {
     if (want_pairs(t) && !t->dir_pairs) return true;   // the form a read / quiet phase wants
     if (dir_bits_for(t, rp) > t->dir_bits) return true;  // a read phase's density, or the tree doubled
-    return t->next_page != t->dir_np && t->dir_debt_ps >= dir_build_ps(t);
+    return dir_lost(t) != t->dir_lost_at_build && t->dir_debt_ps >= dir_build_ps(t);
   }
   if (t->next_page > t->dir_np + t->dir_np / 32) return true;
   // a read phase also wants its denser directory, once
@@ -624,6 +637,8 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   t->dir_valid = true;
   t->hint_ok = true;
   t->dir_debt_ps = 0.0;
+  t->dir_lost_at_build = dir_lost(t);
+  t->dir_exact = t->dir_maint;
   return SHM_OK;
 }
 
@@ -941,6 +956,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.lock_tag = lock_tag;
   set_dir(t, &w.dir, &w.dir_lo, &w.dir_shift, &w.dir_n);
   w.dir_pairs = w.dir && t->dir_pairs ? 1 : 0;
+  w.dir_exact = w.dir && t->dir_exact && t->dir_maint ? 1 : 0;
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
@@ -991,6 +1007,9 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   if (u.dir && t->dir_maint) {  // the chunk's leaf writers keep the entries (dir_upkeep.h)
     u.dir_w = t->dir;
     u.dir_form = t->dir_pairs ? dev::kDirFormPairs : dev::kDirFormFp;
+    u.dir_fix = t->dir_fix;
+    u.dir_fix_n = t->dir_fix_n;
+    u.dir_fix_cap = t->dir_fix_cap;
   }
   u.stamps = t->stamps;
   u.force_abort = (t->force_flags & 1u) ? 1u : 0u;
@@ -1044,6 +1063,14 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   t->force_flags = 0;
   dev::launch_upper(u, s);
   DBG(s, "upper");
+  if (u.dir_w) {
+    // the entries the chunk's writers listed, rebuilt from the tree
+    dev::launch_dir_repair(t->arena, t->arena_bytes, t->cfg.node_id, t->root, u.dir_lo,
+                           u.dir_shift, u.dir_n, t->dir, t->dir_hint, (int)u.dir_form, t->dir_fix,
+                           t->dir_fix_n, u.par, t->dir_fix_cap, u.pub + dev::kPubDirLost,
+                           t->d_err, s);
+    DBG(s, "dir_repair");
+  }
   HIP_OK(hipGetLastError());
   t->err_pending = true;
   if (t->prof_on) {
@@ -1139,7 +1166,7 @@ void free_all(shm_tree* t) {
   F(t->uk); F(t->uv); F(t->dk); F(t->pages); F(t->seg_lb); F(t->bsum64);
   F(t->seg_start); F(t->seg_end); F(t->seg_page); F(t->seg_T); F(t->seg_P); F(t->seg_np);
   F(t->seg_ver); F(t->leaf_hw); F(t->sum); F(t->oslot); F(t->pnew);
-  F(t->ctl); F(t->leaf_rd);
+  F(t->ctl); F(t->leaf_rd); F(t->dir_fix); F(t->dir_fix_n);
   for (int i = 0; i < 2; ++i) { F(t->sep_key[i]); F(t->sep_ptr[i]); F(t->ipage[i]); }
   F(t->h_end); F(t->h_T); F(t->h_P); F(t->h_ver); F(t->h_lk);
   F(t->d_head); F(t->d_base); F(t->int_rd);
@@ -1424,6 +1451,9 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
   rc |= dalloc(&t->oslot, n);
   rc |= dalloc(&t->pnew, t->cap_pages);
   rc |= dalloc(&t->ctl, 1);
+  t->dir_fix_cap = (uint32_t)std::max<uint64_t>(n, 1u << 16);
+  rc |= dalloc(&t->dir_fix, t->dir_fix_cap);
+  rc |= dalloc(&t->dir_fix_n, 32);
   rc |= dalloc(&t->leaf_rd, segcap);
   for (int i = 0; i < 2; ++i) {
     rc |= dalloc(&t->sep_key[i], t->sep_cap);
@@ -1469,6 +1499,7 @@ int shm_tree_create(const shm_config* cfg, shm_tree** out) {
       hipMemsetAsync(t->seg_lb, 0, sizeof(uint64_t) * (dev::seg_tiles(segcap) + 1), s) ||
       hipMemsetAsync(t->bsum64, 0, sizeof(uint64_t) * (dev::seg_tiles(n) + 1), s) ||
       hipMemsetAsync(t->ctl, 0, sizeof(dev::UpperCtl), s) ||
+      hipMemsetAsync(t->dir_fix_n, 0, sizeof(uint32_t) * 32, s) ||
       hipMemsetAsync(t->bins, 0, sizeof(uint32_t) * 4 * dev::kCoarse, s) ||
       hipMemsetAsync(t->leaf_rd, 0, sizeof(uint64_t) * segcap, s) ||
       hipMemsetAsync(t->int_rd, 0, sizeof(uint64_t) * t->sep_cap, s) ||
@@ -1544,6 +1575,8 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
     set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
+    a.dir_exact = a.dir && t->dir_exact && t->dir_maint ? 1 : 0;
+    a.page_check = (t->cfg.flags & SHM_FLAG_PAGE_CHECK) ? 1 : 0;
     if (use_top(t) && t->top_valid) {
       a.top_keys = t->top_keys;
       a.top_pages = t->top_pages;
@@ -2151,8 +2184,34 @@ int shm__dir_config(shm_tree* t, int maint, uint64_t mem_limit) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   if (maint >= 0) t->dir_maint = maint != 0;
+  if (!t->dir_maint) t->dir_exact = false;  // until the next build
   t->dir_mem_limit = mem_limit;
   return SHM_OK;
+}
+
+// diagnostics: every entry the walks trust against the tree as it is now
+// (k_dir_verify): out[0] checked, out[1..3] bad leaf lists / pair sets /
+// fingerprint copies, out[4..7] first bad prefixes + 1
+int shm__dir_verify(shm_tree* t, uint64_t* out) {
+  if (!t || !out) return SHM_EINVAL;
+  std::lock_guard<std::mutex> g(t->mu);
+  memset(out, 0, 8 * sizeof(uint64_t));
+  HIP_OK(hipDeviceSynchronize());
+  if (!t->dir_valid) return SHM_OK;
+  unsigned long long* d = nullptr;
+  if (dalloc(&d, 8)) return SHM_ENOMEM;
+  int rc = SHM_OK;
+  if (hipMemset(d, 0, 64) != hipSuccess) rc = SHM_EIO;
+  if (!rc) {
+    dev::launch_dir_verify(t->arena, t->arena_bytes, t->cfg.node_id, t->root, t->cfg.key_lo,
+                           t->cfg.key_bits - t->dir_bits, 1ull << t->dir_bits, t->dir, t->dir_hint,
+                           d, t->stream);
+    if (hipStreamSynchronize(t->stream) != hipSuccess ||
+        hipMemcpy(out, d, 64, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = SHM_EIO;
+  }
+  (void)hipFree(d);
+  return rc;
 }
 
 int shm_profile_read(shm_tree* t, shm_profile_t* out, int reset) {

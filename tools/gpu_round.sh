@@ -25,7 +25,7 @@ for w in $WHAT; do
     bench) timeout -k 10 500 python -u bench.py > $OUT/bench_c2.json 2> $OUT/bench_c2.err \
            || { tail -30 $OUT/bench_c2.err; exit 1; }
          cat $OUT/bench_c2.json ;;
-    ie) timeout -k 10 500 python -u bench.py --insert-every 8 --no-cpu-baseline > $OUT/bench_ie.json 2> $OUT/bench_ie.err \
+    ie) timeout -k 10 500 python -u bench.py --insert-every 8 > $OUT/bench_ie.json 2> $OUT/bench_ie.err \
            || { tail -30 $OUT/bench_ie.err; exit 1; }
          cat $OUT/bench_ie.json ;;
     c3|c5) timeout -k 10 500 python -u bench.py --workload $w > $OUT/bench_$w.json 2> $OUT/bench_$w.err \
