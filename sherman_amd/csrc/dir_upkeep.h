@@ -3,12 +3,16 @@
 //
 // The directory (leafdir.hip) maps key prefixes to leaves, the role of the
 // reference's IndexCache (include/IndexCache.h:59-259, kept current there by
-// the cache's own inserts and invalidated per entry).  Two writers keep it:
-//   * a new key in an empty slot (upsert.hip, the no-split branch of
-//     leaf_page_store, Tree.cpp:878-912) adds its (fingerprint, slot) pair
+// the cache's own inserts and invalidated per entry).  After each chunk's
+// k_upper, k_dir_upkeep (leafdir.hip, one wave per staged segment: the tree
+// is final then, and the upsert's and k_upper's dependent chains pay
+// nothing -- done inline in them the same work cost C5 +70 us per chunk)
+// applies these rules:
+//   * a new key in an empty slot (the no-split branch of leaf_page_store,
+//     Tree.cpp:878-912, applied by upsert.hip) adds its (fingerprint, slot) pair
 //     to its prefix's pair-form entry, or its fingerprint byte to a
 //     fingerprint-form entry of its leaf (dir_note_new);
-//   * every page a split writes (split_wave.h build_leaf_page, Tree.cpp:
+//   * every page a split wrote (split_wave.h build_leaf_page, Tree.cpp:
 //     914-950) rewrites the entries of the prefixes holding its keys that lie
 //     wholly inside its fences -- one leaf, its keys' slots -- and hands the
 //     one or two prefixes it shares with a neighbour to the summary walk
@@ -59,6 +63,27 @@ __device__ __forceinline__ void dir_note_stale(const UpperArgs& u, uint32_t* w, 
 
 __device__ __forceinline__ uint64_t dir_prefix(const UpperArgs& u, const uint32_t* w) {
   return (uint64_t)(reinterpret_cast<const uint64_t*>(w) - u.dir_w) / kDirWords;
+}
+
+// dir_note_stale for a wave's set of prefixes at once (lanes with `want`
+// hold one prefix each): one round of atomics, one list reservation
+__device__ __forceinline__ void dir_note_stale_lanes(const UpperArgs& u, bool want, uint64_t p) {
+  uint32_t* w = want ? reinterpret_cast<uint32_t*>(u.dir_w + kDirWords * p) : nullptr;
+  bool add = false;
+  if (want) {
+    const uint32_t old = atomicOr(w + 7, kDirFix | kDirPairsBad);  // (bad: pair form only)
+    if (old & kDirFp) atomicAnd(w + 7, ~kDirFp);
+    add = !(old & kDirFix);  // the first to mark it lists it
+  }
+  const uint64_t m = ballot(add);
+  if (!m || !u.dir_fix) return;
+  uint32_t base = 0;
+  if (lane_id() == ctz64(m)) base = atomicAdd(u.dir_fix_n + u.par, (uint32_t)popc64(m));
+  base = rl32(base, ctz64(m));
+  if (add) {
+    const uint32_t i = base + (uint32_t)popc64(m & lanemask_lt());
+    if (i < u.dir_fix_cap) u.dir_fix[i] = (uint32_t)p;
+  }
 }
 
 // key k was stored in the empty slot s of leaf page index pg (one lane)
@@ -121,6 +146,9 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
       if (s >= 0) fpw |= (f & 0xFFu) << (8 * b);
     }
   }
+  // the prefixes it shares with a neighbour (lanes < nst), marked together
+  uint64_t stp = 0;
+  uint32_t nst = 0;
   while (todo) {  // one prefix per round, in key order
     const int first = ctz64(todo);
     const uint64_t p = rl64(pk, first);
@@ -130,7 +158,8 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
     const uint64_t a = lo + (p << sh);
     const bool inside = lowest <= a && highest - 1 >= a + span;
     if (!inside) {  // shared with a neighbour: repaired after the chunk
-      if (lane == 0) dir_note_stale(u, w, p);
+      if ((uint32_t)lane == nst) stp = p;
+      if (nst < (uint32_t)kWave) ++nst;
       continue;
     }
     const uint32_t cnt = (uint32_t)popc64(m);
@@ -163,7 +192,10 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
   // per lane -- an exact entry must never place a new key in the wrong leaf
   // (locate.hip's exact shortcut)
   const uint64_t lo_k = lowest > lo ? lowest : lo;
-  if (highest - 1 < lo || ((lo_k - lo) >> sh) >= u.dir_n) return;
+  if (highest - 1 < lo || ((lo_k - lo) >> sh) >= u.dir_n) {
+    dir_note_stale_lanes(u, (uint32_t)lane < nst, stp);
+    return;
+  }
   const uint64_t pf = (lo_k - lo) >> sh;
   uint64_t pe = ((highest - 1) - lo) >> sh;
   if (pe >= u.dir_n) pe = u.dir_n - 1;
@@ -171,15 +203,16 @@ __device__ __forceinline__ void dir_note_split_page(const UpperArgs& u, uint32_t
   // a key of the page: their leaf lists may name the page the split took
   // the range from (the last page's right end was the old page's), and an
   // exact entry's list must name the leaf of every key of its prefix
-  if (lane == 0) {
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const uint64_t q = e == 0 ? pf : pe;
-      const uint64_t a = lo + (q << sh);
-      if (!(lowest <= a && highest - 1 >= a + span))
-        dir_note_stale(u, reinterpret_cast<uint32_t*>(u.dir_w + kDirWords * q), q);
+  for (int e = 0; e < 2; ++e) {
+    const uint64_t q = e == 0 ? pf : pe;
+    const uint64_t a = lo + (q << sh);
+    if (!(lowest <= a && highest - 1 >= a + span) && nst < (uint32_t)kWave) {
+      if ((uint32_t)lane == nst) stp = q;
+      ++nst;
     }
   }
+  dir_note_stale_lanes(u, (uint32_t)lane < nst, stp);
   // the keys inside the directory's range: lanes [k0, k0 + nk), sorted
   const uint64_t km = ballot(mine);
   const uint32_t nk = (uint32_t)popc64(km);

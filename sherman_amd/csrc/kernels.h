@@ -138,6 +138,15 @@ void launch_dir_repair(const uint8_t* arena, uint64_t arena_bytes, uint16_t node
                        uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
                        const uint32_t* hint, int form, const uint32_t* fix, uint32_t* fix_n,
                        uint32_t par, uint32_t cap, uint64_t* lost, uint32_t* err, hipStream_t s);
+struct UpperArgs;
+// per-op word of the upsert (SegArgs.placed): the op's new key went into an
+// empty slot of its leaf, the slot in the low 6 bits
+constexpr uint32_t kOpPlaced = 0x40000000u;
+// the chunk's directory upkeep after its k_upper (k_dir_upkeep): the placed
+// new keys (ops: pages = k_locate's leaf per op, n_ops_dev their count) and
+// the split segments; n_max bounds both counts (the grid)
+void launch_dir_upkeep(const UpperArgs& u, const uint32_t* oslot, const uint64_t* pages,
+                       const uint64_t* n_ops_dev, uint64_t n_max, hipStream_t s);
 // diagnostics: the trusted entries against the tree (k_dir_verify): out = 8
 // words, zeroed by the caller
 void launch_dir_verify(const uint8_t* arena, uint64_t arena_bytes, uint16_t node, uint64_t root,
@@ -234,6 +243,9 @@ struct SegArgs {
   uint32_t* seg_ver;          // front_version observed
   // per op: bit 31 = already applied in place by k_locate (out_slot)
   const uint32_t* oslot;
+  // the same array, written: a new key the upsert stored in an empty slot
+  // gets kOpPlaced | slot (k_dir_upkeep reads it; nullable)
+  uint32_t* placed;
   // the lock table and the chunk's epoch tag (taken with each page's DMA)
   uint64_t* locks;
   uint32_t num_locks;

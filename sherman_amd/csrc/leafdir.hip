@@ -21,6 +21,7 @@
 // rebuilds the directory when the tree has grown enough to make the extra
 // hops matter.
 #include "device_common.h"
+#include "dir_upkeep.h"
 #include "kernels.h"
 
 namespace shm {
@@ -258,19 +259,6 @@ void launch_dir_pairs(const uint8_t* arena, uint64_t n_pages, uint16_t node, uin
                      shift, n_ent, dir);
 }
 
-// The entries an insert chunk's writers could not keep exact (dir_upkeep.h:
-// prefixes a split page shares with a neighbour, a new key whose prefix's
-// list does not name its leaf) were marked for the summary walk and listed;
-// after the chunk, one wave per listed prefix rebuilds its entry from the
-// tree exactly as k_leaf_dir (+ k_dir_pairs) would: the leaf holding the
-// prefix's first key (walked from the prefix's level-1 hint, a B-link start
-// that stays valid), the up to four leaves covering the prefix, and in the
-// pair form the (fingerprint, slot | leaf << 6) pairs of their valid entries
-// inside the prefix, in leaf then slot order; in the fingerprint form an
-// entry whose prefix lies in one leaf carries that leaf's fingerprints.
-// fix_n[par] holds the chunk's count (past cap: lost repairs, added to *lost
-// in host memory, which the host reads as staleness); the launch zeroes the
-// next chunk's counter.
 // The exact entry of prefix p as a build would write it (one wave): word
 // `lane` of the 64 B entry in *v for lanes < 16; false when the walk failed
 // (a bad pointer).  In the pair form *np_out = the pair count.
@@ -285,68 +273,64 @@ __device__ __forceinline__ bool dir_exact_entry(const uint8_t* __restrict__ aren
   const uint32_t sh = shift > 32 ? shift - 32 : 0;
   const uint64_t lo = dir_lo + (p << shift);
   const uint64_t hi = lo > ~0ull - span ? ~0ull : lo + span;
-  // lane 0: the leaf holding lo, the leaves covering [lo, hi] (k_leaf_dir)
+  // the leaf holding lo, the leaves covering [lo, hi] (k_leaf_dir's walk),
+  // one dependent round per page: the whole page in one 16 B slice per lane
+  // (header and every internal record, load_page_slice), the child by a
+  // ballot over the records
   uint64_t pgs[4] = {0, 0, 0, 0}, seps[4] = {0, 0, 0, 0};
   uint32_t n = 0;
   uint64_t cover = root;
   bool ok = false;
-  if (lane == 0) {
+  {
     uint64_t ptr = root;
     bool hinted = false;
     if (hint && hint[p]) {
       ptr = dir_page_ga(hint[p], node);
       hinted = true;
     }
-    for (int it = 0; it < 4096; ++it) {
+    for (int it = 0; it < 4096; ++it) {  // (wave-uniform)
       if (!ptr_ok(ptr, node, arena_bytes)) break;
-      const uint8_t* pg = arena + ga_offset(ptr);
-      const uint64_t leftmost = pg64_b1(pg, 2);
-      const uint64_t sibling = pg64_b1(pg, 4);
-      const uint64_t highest = pg64(pg, kOffHighest);
-      if (hinted && (leftmost == 0 || pg[kOffLevel] != 1 || lo < pg64(pg, kOffLowest))) {
+      const u32x4 w = load_page_slice(arena, ga_offset(ptr));
+      const Hdr h = parse_hdr(w);
+      if (hinted && (h.leftmost == 0 || h.level != 1 || lo < h.lowest)) {
         hinted = false;  // not a level-1 page on lo's path any more
         ptr = root;
         continue;
       }
-      if (lo >= highest) {  // turn right (Tree.cpp:626-629)
-        if (sibling == 0) break;
-        ptr = sibling;
+      if (lo >= h.highest) {  // turn right (Tree.cpp:626-629)
+        if (h.sibling == 0) break;
+        ptr = h.sibling;
         continue;
       }
-      if (leftmost != 0) {  // internal: descend towards lo
-        const int cnt = (int)(int16_t)(pg[kOffLastIndex] | (pg[kOffLastIndex + 1] << 8)) + 1;
-        const int c = keys_le(pg, cnt, lo);
-        if (hi < highest) cover = ptr;
-        ptr = c == 0 ? leftmost : pg64(pg, kOffRecords + kInternalEntry * (c - 1) + 8);
+      if (h.leftmost != 0) {  // internal: the child of #keys <= lo (Tree.cpp:665-685)
+        const IntRec r = internal_record(w);
+        const int j = lane - 3;
+        const int cnt = h.last_index + 1;
+        const uint64_t le = ballot(j >= 0 && j < cnt && j < kInternalCardinality && r.key <= lo);
+        const int c = popc64(le);
+        if (hi < h.highest) cover = ptr;
+        ptr = c == 0 ? h.leftmost : rl64(r.ptr, 3 + c - 1);
         hinted = false;
         continue;
       }
       pgs[0] = ptr;
-      uint64_t h = highest, sib = sibling;
+      uint64_t hh = h.highest, sib = h.sibling;
       n = 1;
-      while (h <= hi && sib != 0 && n <= 4) {
+      while (hh <= hi && sib != 0 && n <= 4) {
         if (n == 4 || !ptr_ok(sib, node, arena_bytes)) {
           n = 5;  // more than four leaves: the covering internal page
           break;
         }
-        const uint8_t* sp = arena + ga_offset(sib);
+        const Hdr hs = parse_hdr(load_page_slice(arena, ga_offset(sib)));
         pgs[n] = sib;
-        seps[n] = pg64(sp, kOffLowest);
-        h = pg64(sp, kOffHighest);
-        sib = pg64_b1(sp, 4);
+        seps[n] = hs.lowest;
+        hh = hs.highest;
+        sib = hs.sibling;
         ++n;
       }
       ok = true;
       break;
     }
-  }
-  ok = rl32(ok ? 1u : 0u, 0) != 0;
-  n = rl32(n, 0);
-  cover = rl64(cover, 0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    pgs[j] = rl64(pgs[j], 0);
-    seps[j] = rl64(seps[j], 0);
   }
   *np_out = 0;
   if (!ok) return false;
@@ -484,6 +468,80 @@ __global__ __launch_bounds__(256) void k_dir_repair(const uint8_t* __restrict__ 
   }
 }
 
+// The chunk's directory upkeep, after its k_upper (round 6; dir_upkeep.h):
+// one wave per staged segment of the chunk (the leaves that got a new key).
+// A segment applied in place: each new key's pair / fingerprint goes into
+// its prefix's entry (dir_note_new), its slot found in the page.  A split
+// segment: its P pages, from page 0 (the segment's page, or the root's left
+// half when the root grew) along the sibling chain, each rewrites the
+// entries inside its fences and lists the ones it shares
+// (dir_note_split_page).  Off the upsert's and k_upper's dependent chains:
+// the tree is final when this runs, and k_dir_repair follows it.
+__global__ __launch_bounds__(256) void k_dir_upkeep(UpperArgs u, const uint32_t* __restrict__ oslot,
+                                                    const uint64_t* __restrict__ pages,
+                                                    const uint64_t* __restrict__ n_ops_dev) {
+  const int lane = lane_id();
+  const uint64_t n_ops = *n_ops_dev;
+  const uint32_t ns = *u.ns_dev;
+  const uint64_t nwin = ((n_ops > ns ? n_ops : (uint64_t)ns) + kWave - 1) / kWave;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  for (uint64_t win = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+       win < nwin; win += nw) {
+    // (a) the new keys the upsert stored in place, lane = op
+    const uint64_t i = win * kWave + (uint64_t)lane;
+    if (i < n_ops) {
+      const uint32_t o = oslot[i];
+      if ((o & kOpPlaced) && !(o >> 31))
+        dir_note_new(u, u.op_key[i], (uint32_t)(ga_offset(pages[i]) >> 10), (int)(o & 63u));
+    }
+    // (b) the split segments of this window, one after another
+    const uint64_t g = win * kWave + (uint64_t)lane;
+    const bool split = g < ns && u.seg_T[g] != 0 && u.seg_P[g] > 1;
+    uint64_t m = ballot(split);
+    while (m) {
+      const int l = ctz64(m);
+      m &= m - 1;
+      const uint64_t gs = rl64(g, l);
+      const uint32_t P = u.seg_P[gs];
+      uint64_t page = u.seg_page[gs];
+      if (!ptr_ok(page, u.node, u.arena_bytes)) continue;
+      // page 0 is the segment's page, unless that page became the root's
+      // internal page (the root grew: its left half is the leftmost)
+      {
+        const Hdr h = parse_hdr(load_page_slice(u.arena, ga_offset(page)));
+        if (h.leftmost != 0) page = h.leftmost;
+      }
+      for (uint32_t q = 0; q < P && ptr_ok(page, u.node, u.arena_bytes); ++q) {
+        const uint8_t* pg = u.arena + ga_offset(page);
+        const Hdr h = parse_hdr(load_page_slice(u.arena, ga_offset(page)));
+        if (h.leftmost != 0) break;  // not a leaf
+        const uint32_t c = (uint32_t)(h.last_index + 1);
+        uint64_t k = 0, v = 0;
+        uint32_t f = 0, r = 0;
+        if ((uint32_t)lane < c && lane < kLeafCardinality) lane_entry(pg, lane, k, v, f, r);
+        dir_note_split_page(u, (uint32_t)(ga_offset(page) >> 10), h.lowest, h.highest, k,
+                            c < (uint32_t)kLeafCardinality ? c : (uint32_t)kLeafCardinality);
+        page = h.sibling;
+      }
+    }
+  }
+}
+
+void launch_dir_upkeep(const UpperArgs& u, const uint32_t* oslot, const uint64_t* pages,
+                       const uint64_t* n_ops_dev, uint64_t n_max, hipStream_t s) {
+  if (!n_max) return;
+  static unsigned nb = 0;
+  if (!nb) {
+    int cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    nb = (unsigned)(cus > 0 ? cus : 256) * 5;  // every resident wave slot at 5 per SIMD
+  }
+  const uint64_t need = (n_max + 4 * kWave - 1) / (4 * kWave);  // a 64-op window per wave
+  hipLaunchKernelGGL(k_dir_upkeep, dim3((unsigned)(need < nb ? need : nb)), dim3(256), 0, s, u,
+                     oslot, pages, n_ops_dev);
+}
+
 // Diagnostics (shm__dir_verify): every entry the walks trust -- a usable
 // pair-form entry, a fingerprint-form entry -- against the exact entry of
 // the tree as it is: out[0] entries checked, out[1] leaf lists or split
@@ -573,7 +631,14 @@ void launch_dir_repair(const uint8_t* arena, uint64_t arena_bytes, uint16_t node
                        uint64_t dir_lo, uint32_t shift, uint64_t n_ent, uint64_t* dir,
                        const uint32_t* hint, int form, const uint32_t* fix, uint32_t* fix_n,
                        uint32_t par, uint32_t cap, uint64_t* lost, uint32_t* err, hipStream_t s) {
-  hipLaunchKernelGGL(k_dir_repair, dim3(256), dim3(256), 0, s, arena, arena_bytes, node, root,
+  static unsigned nb = 0;
+  if (!nb) {
+    int cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    nb = (unsigned)(cus > 0 ? cus : 256) * 5;  // every resident wave slot at 5 per SIMD
+  }
+  hipLaunchKernelGGL(k_dir_repair, dim3(nb), dim3(256), 0, s, arena, arena_bytes, node, root,
                      dir_lo, shift, n_ent, dir, hint, form, fix, fix_n, par, cap, lost, err);
 }
 

@@ -5,7 +5,6 @@
 #pragma once
 #include "device_common.h"
 #include "kernels.h"
-#include "dir_upkeep.h"
 
 namespace shm {
 namespace dev {
@@ -153,8 +152,6 @@ __device__ __forceinline__ uint64_t build_leaf_page(const UpperArgs& a, WaveLds&
   if (a.leaf_hw && lane == 0) a.leaf_hw[ga_offset(s.dest) >> 10] = (uint8_t)c;  // slots [0, c)
   // every slot < c is valid (value != 0: deletes never reach a split page)
   put_leaf_sum(a.sum, ga_offset(s.dest), highest, (uint32_t)lane < c ? key_fp(key) : 0u);
-  // the directory entries of the prefixes this page now holds (dir_upkeep.h)
-  dir_note_split_page(a, (uint32_t)(ga_offset(s.dest) >> 10), lowest, highest, key, c);
   return lowest;
 }
 

@@ -1048,6 +1048,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   a.seg_newpages = t->seg_np;
   a.seg_ver = t->seg_ver;
   a.oslot = t->oslot;
+  a.placed = u.dir_w ? t->oslot : nullptr;  // new keys' slots for k_dir_upkeep
   a.locks = t->locks;
   a.num_locks = t->cfg.num_locks;
   a.tag = lock_tag;
@@ -1064,7 +1065,10 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   dev::launch_upper(u, s);
   DBG(s, "upper");
   if (u.dir_w) {
-    // the entries the chunk's writers listed, rebuilt from the tree
+    // the chunk's directory upkeep (new keys' pairs / fingerprints, split
+    // pages' prefixes), then the entries it listed rebuilt from the tree
+    dev::launch_dir_upkeep(u, t->oslot, t->pages, cnt + 0, n, s);
+    DBG(s, "dir_upkeep");
     dev::launch_dir_repair(t->arena, t->arena_bytes, t->cfg.node_id, t->root, u.dir_lo,
                            u.dir_shift, u.dir_n, t->dir, t->dir_hint, (int)u.dir_form, t->dir_fix,
                            t->dir_fix_n, u.par, t->dir_fix_cap, u.pub + dev::kPubDirLost,

@@ -136,6 +136,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
   uint32_t ef[E], er[E];
   chunk_entries<E>(D, ek, ev, ef, er);
   bool mine[E], valid[E], dirty[E], fresh[E];  // fresh: a new key took the slot
+  uint32_t eop[E];  // the op that took slot j (fresh)
   uint32_t cnt = 0;  // valid entries of slot q (the same in all its lanes)
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -143,6 +144,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
     valid[j] = mine[j] && ev[j] != kValueNull;
     dirty[j] = false;
     fresh[j] = false;
+    eop[j] = 0;
     cnt += (uint32_t)popc64((ballot(valid[j]) >> (q * L)) & kGroupMask);
   }
 
@@ -215,6 +217,7 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         valid[j] = true;
         dirty[j] = true;
         fresh[j] = fresh[j] || isnew;
+        if (isnew) eop[j] = qst + t;
       }
     }
   }
@@ -234,8 +237,8 @@ __device__ __forceinline__ uint32_t apply_group(const SegArgs& a, const uint32_t
         // that gained keys, none for pure updates)
         if (fresh[j]) {
           set_leaf_fp(a.sum, ga_offset(qpage), ebase + j, ek[j]);
-          // and the key's directory entry (dir_upkeep.h)
-          dir_note_new(u, ek[j], (uint32_t)(ga_offset(qpage) >> 10), ebase + j);
+          // for the directory upkeep after the chunk (k_dir_upkeep)
+          if (a.placed) a.placed[eop[j]] = kOpPlaced | (uint32_t)(ebase + j);
         }
       }
   }

@@ -28,6 +28,9 @@ for w in $WHAT; do
     ie) timeout -k 10 500 python -u bench.py --insert-every 8 > $OUT/bench_ie.json 2> $OUT/bench_ie.err \
            || { tail -30 $OUT/bench_ie.err; exit 1; }
          cat $OUT/bench_ie.json ;;
+    pchk) timeout -k 10 500 python -u bench.py --page-check 1 --no-cpu-baseline > $OUT/bench_pchk.json 2> $OUT/bench_pchk.err \
+           || { tail -30 $OUT/bench_pchk.err; exit 1; }
+         cat $OUT/bench_pchk.json ;;
     c3|c5) timeout -k 10 500 python -u bench.py --workload $w > $OUT/bench_$w.json 2> $OUT/bench_$w.err \
            || { tail -30 $OUT/bench_$w.err; exit 1; }
          cat $OUT/bench_$w.json ;;
