@@ -329,8 +329,8 @@ typedef struct shm_dir_stats_t {
   uint64_t pages_since_build; /* pages splits added since */
   double last_build_ms;       /* device time of the last build (-1: none yet) */
   double total_build_ms;      /* of every build */
-  uint32_t maintained;        /* 1: insert chunks keep the entries current */
-  uint32_t reserved;
+  uint32_t maintained;        /* 1: insert chunks may keep the entries current */
+  uint32_t exact;             /* 1: every usable entry equals a fresh build's */
 } shm_dir_stats_t;
 int shm_dir_stats(shm_tree *t, shm_dir_stats_t *out);
 

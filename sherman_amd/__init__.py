@@ -93,7 +93,7 @@ class ShmDirStats(ctypes.Structure):
     _fields_ = [("form", u32), ("bits", u32), ("entries", u64), ("bytes", u64), ("builds", u64),
                 ("pages_at_build", u64), ("pages_since_build", u64),
                 ("last_build_ms", ctypes.c_double), ("total_build_ms", ctypes.c_double),
-                ("maintained", u32), ("reserved", u32)]
+                ("maintained", u32), ("exact", u32)]
 
 
 DIR_FORMS = {0: "none", 1: "fingerprints", 2: "pairs"}
@@ -560,15 +560,16 @@ class Tree:
         entries, device bytes, builds and their device time (shm_dir_stats)."""
         st = ShmDirStats()
         _check(lib().shm_dir_stats(self.h, ctypes.byref(st)), "dir_stats")
-        d = {f: getattr(st, f) for f, _ in ShmDirStats._fields_ if f != "reserved"}
+        d = {f: getattr(st, f) for f, _ in ShmDirStats._fields_}
         d["form"] = DIR_FORMS.get(d["form"], str(d["form"]))
         return d
 
     def dir_config(self, maint=None, mem_limit=0):
-        """Test hook (shm__dir_config): directory upkeep by the writers on /
-        off (None: as is) and a byte cap on directory allocations."""
-        _check(_hooks().shm__dir_config(self.h, -1 if maint is None else int(bool(maint)),
-                                        mem_limit), "dir_config")
+        """Test hook (shm__dir_config): directory upkeep by the chunks on /
+        off (None: as is; "always": every chunk, also those with no search
+        since the last one) and a byte cap on directory allocations."""
+        m = -1 if maint is None else 2 if maint == "always" else int(bool(maint))
+        _check(_hooks().shm__dir_config(self.h, m, mem_limit), "dir_config")
 
     def dir_verify(self):
         """Diagnostics (shm__dir_verify): every directory entry the walks

@@ -210,6 +210,12 @@ struct UpperCtl {
 constexpr int kPubApplied = 4;
 // UpperArgs.pub word 6: directory repairs lost so far (k_dir_repair, cumulative)
 constexpr int kPubDirLost = 6;
+// words 7 / 8: the directory upkeep's work so far (new keys + split pages,
+// cumulative) and the count of chunks whose upkeep finished (k_dir_repair
+// publishes both from the device counters at dir_fix_n + kDirWorkWord)
+constexpr int kPubDirWork = 7;
+constexpr int kPubDirUpkeeps = 8;
+constexpr int kDirWorkWord = 2;
 // a leaf split into at most this many pages is built by one wave (pages
 // 1.. first, page 0 last, no fan-in); larger ones are spread over the grid
 constexpr uint32_t kSmallSplit = 4;

@@ -443,9 +443,18 @@ __global__ __launch_bounds__(256) void k_dir_repair(const uint8_t* __restrict__ 
   const uint32_t n_fix = fix_n[par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     fix_n[par ^ 1u] = 0;  // the next chunk's list (its writers run after this launch)
-    if (n_fix > cap && lost) {
-      const uint64_t l = __hip_atomic_load(lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(lost, l + (n_fix - cap), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lost) {
+      if (n_fix > cap) {
+        const uint64_t l = __hip_atomic_load(lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(lost, l + (n_fix - cap), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      // the upkeep's work so far and the count of upkeeps done, for the
+      // host's idle rule (tree.cpp insert_apply); k_dir_upkeep finished
+      uint64_t* ctr = reinterpret_cast<uint64_t*>(fix_n + kDirWorkWord);
+      const uint64_t done = ctr[1] + 1;
+      ctr[1] = done;
+      __hip_atomic_store(lost + 1, ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(lost + 2, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   const uint32_t m = n_fix < cap ? n_fix : cap;
@@ -485,15 +494,19 @@ __global__ __launch_bounds__(256) void k_dir_upkeep(UpperArgs u, const uint32_t*
   const uint32_t ns = *u.ns_dev;
   const uint64_t nwin = ((n_ops > ns ? n_ops : (uint64_t)ns) + kWave - 1) / kWave;
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  uint64_t work = 0;  // new keys + split pages this wave handled
   for (uint64_t win = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
        win < nwin; win += nw) {
     // (a) the new keys the upsert stored in place, lane = op
     const uint64_t i = win * kWave + (uint64_t)lane;
+    bool placed = false;
     if (i < n_ops) {
       const uint32_t o = oslot[i];
-      if ((o & kOpPlaced) && !(o >> 31))
+      placed = (o & kOpPlaced) && !(o >> 31);
+      if (placed)
         dir_note_new(u, u.op_key[i], (uint32_t)(ga_offset(pages[i]) >> 10), (int)(o & 63u));
     }
+    work += (uint64_t)__popcll(ballot(placed));
     // (b) the split segments of this window, one after another
     const uint64_t g = win * kWave + (uint64_t)lane;
     const bool split = g < ns && u.seg_T[g] != 0 && u.seg_P[g] > 1;
@@ -522,9 +535,13 @@ __global__ __launch_bounds__(256) void k_dir_upkeep(UpperArgs u, const uint32_t*
         dir_note_split_page(u, (uint32_t)(ga_offset(page) >> 10), h.lowest, h.highest, k,
                             c < (uint32_t)kLeafCardinality ? c : (uint32_t)kLeafCardinality);
         page = h.sibling;
+        ++work;
       }
     }
   }
+  if (work && lane == 0)
+    atomicAdd(reinterpret_cast<unsigned long long*>(u.dir_fix_n + kDirWorkWord),
+              (unsigned long long)work);
 }
 
 void launch_dir_upkeep(const UpperArgs& u, const uint32_t* oslot, const uint64_t* pages,

@@ -149,8 +149,12 @@ struct shm_tree {
   uint32_t* dir_fix_n = nullptr;
   uint32_t dir_fix_cap = 0;
   uint64_t dir_lost_at_build = 0;  // the host word kPubDirLost at the last build
+  uint64_t dir_work_seen = 0;      // the host words kPubDirWork / kPubDirUpkeeps at the last look
+  uint64_t dir_upk_seen = 0;
+  uint32_t dir_idle_upkeeps = 0;   // finished upkeeps in a row that found nothing to do
   bool dir_off = false;      // no directory could be allocated: walks from the root
   bool dir_exact = false;    // built with upkeep on, and upkeep on ever since (WalkArgs.dir_exact)
+  bool dir_maint_always = false;  // shm__dir_config maint 2: every chunk keeps it (tests)
   double dir_debt_ps = 0.0;  // gets' estimated extra cost on shared prefixes since the build
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
@@ -419,6 +423,9 @@ constexpr uint32_t kReadPhase = 4;
 // load's last rebuild fell early).  A mirror that merely lags (the host ahead
 // of the device) shows no newer tag, so it never looks quiet
 constexpr uint32_t kQuietChunks = 2;
+// finished directory upkeeps in a row with no new key and no split page after
+// which the chunks stop keeping the directory (insert_apply)
+constexpr uint32_t kIdleUpkeeps = 2;
 
 // Directory entries per tree page, as a power of two (SHM_DIR_EXTRA_BITS
 // overrides both): eight 64 B entries per page while the tree is written
@@ -506,7 +513,7 @@ bool dir_stale(const shm_tree* t) {
   if (t->dir_off) return false;
   if (!t->dir_valid) return true;
   const bool rp = read_phase(t);
-  if (t->dir_maint) {
+  if (t->dir_maint && t->dir_exact) {
     if (want_pairs(t) && !t->dir_pairs) return true;   // the form a read / quiet phase wants
     if (dir_bits_for(t, rp) > t->dir_bits) return true;  // a read phase's density, or the tree doubled
     return dir_lost(t) != t->dir_lost_at_build && t->dir_debt_ps >= dir_build_ps(t);
@@ -519,7 +526,7 @@ bool dir_stale(const shm_tree* t) {
 
 // a search of n keys: its estimated extra cost on the shared prefixes
 void dir_note_gets(shm_tree* t, uint64_t n) {
-  if (t->dir_maint) t->dir_debt_ps += (double)n * dir_shared_frac(t) * kSharedPrefixGetPs;
+  if (t->dir_maint && t->dir_exact) t->dir_debt_ps += (double)n * dir_shared_frac(t) * kSharedPrefixGetPs;
 }
 
 // the last build's device time once its end event completed (wait: block
@@ -638,6 +645,7 @@ int refresh_dir(shm_tree* t, hipStream_t s) {
   t->hint_ok = true;
   t->dir_debt_ps = 0.0;
   t->dir_lost_at_build = dir_lost(t);
+  t->dir_idle_upkeeps = 0;
   t->dir_exact = t->dir_maint;
   return SHM_OK;
 }
@@ -925,6 +933,7 @@ int insert_order(shm_tree* t, hipStream_t s, const uint64_t* keys, const uint64_
 int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
                  shm_tree::ProfRec& pr) {
   const uint64_t lock_tag = (uint64_t)tag << 32;
+  const bool searched = t->reads_since_write > 0;
   t->reads_since_write = 0;
   if (t->pub_batch != t->pub_seen) {  // a newer chunk published since the last look
     if (t->next_page == t->np_seen) {
@@ -935,6 +944,26 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
     }
     t->pub_seen = t->pub_batch;
   }
+  // the chunk keeps the directory exact (dir_upkeep.h: two launches after
+  // its k_upper) only where gets read it between chunks and the chunks
+  // still add keys: a write-only stream (C5) or one whose upkeeps found
+  // nothing to do kIdleUpkeeps times in a row (C3's updates) runs round 5's
+  // rules instead -- its directory stops being exact until the next build --
+  // rather than pay the launches for nothing
+  {  // the upkeeps finished since the last look: did any find work?
+    const volatile uint64_t* p =
+        reinterpret_cast<const volatile uint64_t*>(t->h_pin) + kPubWord / 2;
+    const uint64_t done = p[dev::kPubDirUpkeeps];  // first: the work word is at least this new
+    const uint64_t work = p[dev::kPubDirWork];
+    if (done != t->dir_upk_seen) {
+      t->dir_idle_upkeeps = work == t->dir_work_seen ? t->dir_idle_upkeeps + (uint32_t)(done - t->dir_upk_seen) : 0;
+      t->dir_upk_seen = done;
+      t->dir_work_seen = work;
+    }
+  }
+  const bool upkeep = t->dir_maint && t->dir_exact && t->dir_valid &&
+                      ((searched && t->dir_idle_upkeeps < kIdleUpkeeps) || t->dir_maint_always);
+  if (!upkeep) t->dir_exact = false;
   // the byte marks repeat every 255 chunks: clear them when they wrap, so
   // no page still carries this chunk's mark from 255 chunks ago
   if (dev::new_mark(tag) == 1)
@@ -956,7 +985,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   w.lock_tag = lock_tag;
   set_dir(t, &w.dir, &w.dir_lo, &w.dir_shift, &w.dir_n);
   w.dir_pairs = w.dir && t->dir_pairs ? 1 : 0;
-  w.dir_exact = w.dir && t->dir_exact && t->dir_maint ? 1 : 0;
+  w.dir_exact = w.dir && t->dir_exact ? 1 : 0;
   dev::launch_locate(w, n, s);
   DBG(s, "locate");
   uint32_t* d_ns = reinterpret_cast<uint32_t*>(t->d_counts + 8);
@@ -1004,7 +1033,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   u.n_del = cnt + 1;
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
-  if (u.dir && t->dir_maint) {  // the chunk's leaf writers keep the entries (dir_upkeep.h)
+  if (u.dir && upkeep) {  // the chunk's directory upkeep after its k_upper (dir_upkeep.h)
     u.dir_w = t->dir;
     u.dir_form = t->dir_pairs ? dev::kDirFormPairs : dev::kDirFormFp;
     u.dir_fix = t->dir_fix;
@@ -1579,7 +1608,7 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     a.out_found = found_out ? found_out + off : nullptr;
     a.n = m;
     set_dir(t, &a.dir, &a.dir_lo, &a.dir_shift, &a.dir_n);
-    a.dir_exact = a.dir && t->dir_exact && t->dir_maint ? 1 : 0;
+    a.dir_exact = a.dir && t->dir_exact ? 1 : 0;
     a.page_check = (t->cfg.flags & SHM_FLAG_PAGE_CHECK) ? 1 : 0;
     if (use_top(t) && t->top_valid) {
       a.top_keys = t->top_keys;
@@ -2178,16 +2207,19 @@ int shm_dir_stats(shm_tree* t, shm_dir_stats_t* out) {
   out->last_build_ms = t->dir_last_ms;
   out->total_build_ms = t->dir_total_ms;
   out->maintained = t->dir_maint ? 1u : 0u;
+  out->exact = t->dir_valid && t->dir_exact ? 1u : 0u;
   return SHM_OK;
 }
 
-// test hook: directory upkeep on / off for this tree (maint < 0: as is) and
+// test hook: directory upkeep on / off for this tree (maint < 0: as is; 2:
+// on for every chunk, also those with no search before them) and
 // a cap on the bytes a directory allocation may take (0: none), as a device
 // short of memory would impose
 int shm__dir_config(shm_tree* t, int maint, uint64_t mem_limit) {
   if (!t) return SHM_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   if (maint >= 0) t->dir_maint = maint != 0;
+  if (maint >= 0) t->dir_maint_always = maint == 2;
   if (!t->dir_maint) t->dir_exact = false;  // until the next build
   t->dir_mem_limit = mem_limit;
   return SHM_OK;

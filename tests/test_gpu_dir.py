@@ -70,7 +70,7 @@ def lib_ok():
     return True
 
 
-def loaded(n0, maint=True, arena=512 << 20, max_batch=1 << 18):
+def loaded(n0, maint="always", arena=512 << 20, max_batch=1 << 18):
     t = shm.Tree(arena_bytes=arena, max_batch=max_batch)
     t.dir_config(maint=maint)
     orc = OracleTree(arena)
@@ -247,7 +247,7 @@ def test_insert_every_cycles_build_once(lib_ok):
     phase then wants the denser directory) -- and every get and every new
     key equal the oracle."""
     n0 = 1 << 20
-    t, orc, base = loaded(n0, arena=1 << 30, max_batch=1 << 20)
+    t, orc, base = loaded(n0, maint=True, arena=1 << 30, max_batch=1 << 20)
     rng = np.random.default_rng(10)
     qs = [base[rng.integers(0, n0, 1 << 16)] for _ in range(4)]
     for _ in range(5):
@@ -271,6 +271,68 @@ def test_insert_every_cycles_build_once(lib_ok):
     crossed = next_pow2(t.stats()["pages_used"] + 1) != next_pow2(pages0 + 1)
     assert d["builds"] - b0 <= (1 if crossed else 0), (d, crossed)
     assert d["form"] == "pairs" and d["last_build_ms"] > 0, d
+    orc.close()
+    t.close()
+
+
+def test_upkeep_policy_idle_and_write_only_streams(lib_ok):
+    """The default policy (tree.cpp insert_apply): a chunk keeps the
+    directory only when gets read it since the last chunk and recent upkeeps
+    found work.  Update-only chunks between searches (C3's mix) stop the
+    upkeep after kIdleUpkeeps idle ones; a chunk with no search before it
+    (C5's stream) stops it at once.  Either way the directory is then no
+    longer exact, the exact shortcuts stay off, and every get still equals
+    the oracle; a chunk that adds keys while searched keeps it exact."""
+    n0 = 1 << 17
+    t, orc, base = loaded(n0, maint=True, arena=256 << 20, max_batch=1 << 17)
+    rng = np.random.default_rng(13)
+    probe = np.concatenate([base[rng.integers(0, n0, 1 << 14)], gen_keys(t, 10**9, 1000)])
+    for _ in range(5):
+        gpu_search(t, probe)
+    assert t.dir_stats()["exact"] == 1
+    # a searched chunk of new keys: kept exact
+    nid = n0 + 1
+    new = gen_keys(t, nid, 5000)
+    nid += new.size
+    t.insert_batch(dev(new), dev(new ^ U64(1)))
+    orc.apply_batch(new, new ^ U64(1))
+    t.synchronize()
+    assert t.dir_stats()["exact"] == 1
+    assert_dir_exact(t)
+    # update-only chunks, searched between: idle upkeeps stop the upkeep
+    for r in range(5):
+        gv, gf, _ = gpu_search(t, probe)
+        assert_same(probe, *orc.search_batch(probe), gv, gf)
+        upd = base[rng.integers(0, n0, 4000)]
+        t.insert_batch(dev(upd), dev(upd ^ U64(100 + r)))
+        orc.apply_batch(upd, upd ^ U64(100 + r))
+        t.synchronize()
+    assert t.dir_stats()["exact"] == 0
+    gv, gf, _ = gpu_search(t, probe)
+    assert_same(probe, *orc.search_batch(probe), gv, gf)
+    # a fresh build makes it exact again; a chunk with no search before it
+    # (the second one) stops the upkeep at once
+    t.dir_config(maint=True)
+    more = gen_keys(t, nid, 40000)
+    nid += more.size
+    t.insert_batch(dev(more), dev(more ^ U64(2)))
+    orc.apply_batch(more, more ^ U64(2))
+    for _ in range(5):
+        gpu_search(t, probe)
+    assert t.dir_stats()["exact"] == 1
+    for c in range(2):
+        new = gen_keys(t, nid, 3000)
+        nid += new.size
+        t.insert_batch(dev(new), dev(new ^ U64(3)))
+        orc.apply_batch(new, new ^ U64(3))
+        t.synchronize()
+    assert t.dir_stats()["exact"] == 0
+    ok_, ov = orc.dump()
+    gv, gf, _ = gpu_search(t, ok_)
+    assert bool(gf.all()) and np.array_equal(gv, ov)
+    miss = gen_keys(t, 10**9 + 7, 2000)
+    gv, gf, _ = gpu_search(t, miss)
+    assert_same(miss, *orc.search_batch(miss), gv, gf)
     orc.close()
     t.close()
 
