@@ -89,9 +89,11 @@ def test_c2_full_size_get_parity(lib_ok):
     assert torch.equal(v, want2), int((v != want2).sum())
     assert torch.equal(f.bool(), ~miss)
     # split-heavy chunks of new keys at full size (key(i) for ids past 2^26,
-    # value 2i), then gets before any rebuild: the chunks' leaf writers kept
-    # the pair-form entries (dir_upkeep.h), so every stored key is still
-    # answered exactly -- old, new and their moved slots -- with no rebuild
+    # value 2i), a get batch after each (the gets that make the chunks keep
+    # the directory: tree.cpp insert_apply's policy), then gets before any
+    # rebuild: the chunks kept the pair-form entries (dir_upkeep.h), so every
+    # stored key is still answered exactly -- old, new and their moved slots
+    # -- with no rebuild
     builds = d["builds"]
     pages = t.stats()["pages_used"]
     nk = torch.empty(4 << 20, dtype=torch.int64, device="cuda")
@@ -99,6 +101,9 @@ def test_c2_full_size_get_parity(lib_ok):
     nv = torch.arange(n + 1, n + 1 + nk.numel(), device="cuda", dtype=torch.int64) * 2
     for c in range(0, nk.numel(), 1 << 20):
         t.insert_batch(nk[c:c + (1 << 20)], nv[c:c + (1 << 20)])
+        t.search_batch(nk[c:c + (1 << 20)], v, f)
+        t.synchronize()
+        assert torch.equal(v, nv[c:c + (1 << 20)]) and bool(f.all())
     assert t.stats()["pages_used"] > pages + 10000  # leaves split
     t.profile(False, index_stats=True)
     t.search_batch(q, v, f)  # the old keys
@@ -111,7 +116,7 @@ def test_c2_full_size_get_parity(lib_ok):
     t.profile(False)
     assert torch.equal(v, nv[sel]) and bool(f.all())
     d2 = t.dir_stats()
-    assert d2["builds"] == builds and d2["form"] == "pairs", d2
+    assert d2["builds"] == builds and d2["form"] == "pairs" and d2["exact"], d2
     assert idx["dir_fp_hits"] >= 0.95 * idx["gets"], idx
     t.close()
 
