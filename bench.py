@@ -783,12 +783,14 @@ def main():
         # C1 on the host cores, after every GPU measurement (the oracle's
         # build has run beside them)
         cpu = c1.bench(args.cpu_seconds)
-    walk_ev_ms = prof["walk_ms"] / max(prof["calls"], 1)  # HIP events around the launch
+    walk_ev_ms = prof["walk_ms"] / max(prof["calls"], 1)  # HIP events of the dispatch
     # the headline duration is the HIP events' (VERDICT / ADVICE r5: the
     # device clock span below -- first block start to last wave's stores
     # issued -- leaves out the dispatch ramp and the store drain, and
-    # undercut the rocprof kernel trace by 3-4 %; the events include a
-    # launch gap and came within 2 % of the trace, on the safe side)
+    # undercut the rocprof kernel trace by 3-4 %).  Round 6: the events ride
+    # on the walk's own dispatch (hipExtLaunchKernel), so they time the
+    # kernel as the trace does; event records around the launch added
+    # 2-3 us of marker packets (4.7 % over the trace, profiles/r06 first pass)
     walk_clk_ms = prof["walk_kernel_ms"] / max(prof["calls"], 1) if prof["walk_kernel_ms"] > 0 else None
     walk_ms = walk_ev_ms
     ins_ms = prof["insert_ms"] / max(prof["insert_calls"], 1)
@@ -895,7 +897,7 @@ def main():
                 "reference_bytes_GBps": round(q_per_launch * ALG_BYTES_PER_GET /
                                               (walk_ms * 1e-3) / 1e9, 1) if walk_ms else None,
                 "walk_ms_per_launch": round(walk_ms, 4),
-                "walk_ms_basis": "HIP events around each launch on its stream (profile pass)",
+                "walk_ms_basis": "HIP events carried by each walk dispatch on its stream (hipExtLaunchKernel start / stop events, profile pass)",
                 "walk_clock_ms_per_launch": round(walk_clk_ms, 4) if walk_clk_ms else None,
                 "order_ms_per_launch": round(order_ms, 4),
                 "queries_per_launch": int(q_per_launch),

@@ -24,6 +24,8 @@
 // The per-page scalar work (waits, header broadcasts, per-key ballots) of a
 // page-at-a-time walk is paid once per G pages.
 #include "device_common.h"
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 #include "lds_dma.h"
 #include "leaf_chunk.h"
@@ -634,16 +636,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5))) void k
 
 uint64_t get_sum_blocks(uint64_t n) { return (n + kGetSumTPB - 1) / kGetSumTPB; }
 
-void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s) {
-  if (n == 0) return;
+void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if (n == 0) {
+    // the profile's events still complete
+    if (ev0) (void)hipEventRecord(ev0, s);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    return;
+  }
   constexpr int TPB = kGetSumTPB;
-  const size_t lds = (size_t)a.top_n * 12;
+  const uint32_t lds = (uint32_t)a.top_n * 12;
+  const dim3 grid((unsigned)((n + TPB - 1) / TPB));
+  // ev0 / ev1 (the profile): the dispatch's own start and end
   if (a.page_check)
-    hipLaunchKernelGGL((k_get_sum<TPB, true>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds,
-                       s, a);
+    hipExtLaunchKernelGGL((k_get_sum<TPB, true>), grid, dim3(TPB), lds, s, ev0, ev1, 0u, a);
   else
-    hipLaunchKernelGGL((k_get_sum<TPB, false>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB),
-                       lds, s, a);
+    hipExtLaunchKernelGGL((k_get_sum<TPB, false>), grid, dim3(TPB), lds, s, ev0, ev1, 0u, a);
 }
 
 // ---- the top of the tree for the LDS replica ---------------------------------

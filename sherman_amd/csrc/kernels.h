@@ -107,7 +107,8 @@ constexpr int kGetSumTPB = 256;
 uint64_t get_sum_blocks(uint64_t n);
 // batched get over the leaf summaries, lane = query (get.hip): directory
 // entry, summary line, matching entries; results in input order
-void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s);
+void launch_get_sum(const WalkArgs& a, uint64_t n, hipStream_t s, hipEvent_t ev0 = nullptr,
+                    hipEvent_t ev1 = nullptr);
 // rebuild the summaries of pages [1, pages) from the page bytes (a loaded
 // image), one wave per page
 void launch_sum_rebuild(const uint8_t* arena, uint64_t pages, uint8_t* sum, hipStream_t s);

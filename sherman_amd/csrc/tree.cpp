@@ -1652,7 +1652,10 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     // leaf DMA policy: an ordered walk reads each leaf once per batch, so
     // non-temporal loads keep the directory in L2 (C2 +5 %)
     a.nt = gathered ? 1 : 0;
-    if (t->prof_on) HIP_OK(hipEventRecord(pr.e[1], s));
+    // the walk's profile events: around the page walk's launch; the summary
+    // walk's own dispatch carries them (hipExtLaunchKernel: its start and
+    // end, the span a kernel trace reports, with no marker packets between)
+    if (t->prof_on && gathered) HIP_OK(hipEventRecord(pr.e[1], s));
     // ordered: the page walk (k_get); unordered: the summary walk (k_get_sum,
     // three lines per get)
     if (t->prof_on && !gathered && t->prof_clk) {
@@ -1665,10 +1668,10 @@ static int search_impl(shm_tree* t, hipStream_t s, Order& ord, const uint64_t* k
     if (gathered)
       dev::launch_get(a, m, s);
     else
-      dev::launch_get_sum(a, m, s);
+      dev::launch_get_sum(a, m, s, t->prof_on ? pr.e[1] : nullptr, t->prof_on ? pr.e[2] : nullptr);
     DBG(s, "walk(get)");
     if (t->prof_on) {
-      HIP_OK(hipEventRecord(pr.e[2], s));
+      if (gathered) HIP_OK(hipEventRecord(pr.e[2], s));
       t->prof_pending.push_back(pr);
     }
     if (gathered) {
