@@ -1080,7 +1080,7 @@ def rewarm(tree, dev, seconds=0.5):
 
 def _profile_traffic(name, field, batch, keys_log2, kernel=None):
     """HBM bytes per launch measured by the committed PMC passes
-    (profiles/<name>, tools/refresh_profiles.py) when they were taken at this
+    (profiles/<name>, tools/roofline_pass.sh + tools/commit_roofline.py) when they were taken at this
     batch and key count (and of this kernel), else None."""
     try:
         pmc = json.load(open(os.path.join(ROOT, "profiles", name)))
