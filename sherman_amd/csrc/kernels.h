@@ -502,10 +502,14 @@ void launch_unpermute(const uint64_t* in, const uint32_t* perm, uint64_t n,
 // own_out[0, cap) instead of out[own * cap, ...), i.e. straight into the
 // receive buffer the local get reads, so it never enters the collective
 // (VERDICT r4 #2); spos still names slot own * cap + pos.
+// the routed get's slot placement (util.hip k_route_slots); ctr: the claim
+// words, route_ctr_words(P) u32 zeroed once at allocation
+constexpr uint32_t kCtrStride = 64;  // 256 B: one claim word per line
+inline uint64_t route_ctr_words(uint32_t P) { return (uint64_t)(P + 2) * kCtrStride; }
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
-                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
-                        uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own = 0,
-                        uint64_t* own_out = nullptr);
+                        uint32_t* cursor, uint32_t* ctr, uint64_t* out, uint32_t* spos,
+                        uint64_t* ovk, uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own = 0,
+                        uint64_t* own_out = nullptr, bool fill = true);
 // out[i] = in[spos[i]]; with own_src non-null, slots of run `own` (own * cap
 // .. + cap) are read from own_src (the local get's results, never exchanged)
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,

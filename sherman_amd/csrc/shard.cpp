@@ -367,6 +367,8 @@ struct GetSlot {
   uint64_t pcap = 0;          // slot capacity per peer (allocated)
   uint64_t ncap = 0;          // this batch's: min(pcap, get_slot_cap(n, P))
   uint32_t* cw = nullptr;     // [P] keys routed to each peer, [P] overflow count, [P + 1 ..] received counts
+  uint32_t* ctr = nullptr;    // the placement's claim words (route_ctr_words), zero at rest
+  uint64_t filled = 0;        // the capacity the runs were last padded at (0: never)
   uint64_t *pk = nullptr, *pr = nullptr, *pv = nullptr, *pb = nullptr;  // P * pcap
   uint32_t* spos = nullptr;   // input -> slot
   uint64_t* ovk = nullptr;    // overflow list: keys, their inputs
@@ -435,7 +437,7 @@ namespace {
 
 void free_shard(shm_shard* h) {
   for (GetSlot& s : h->slot) {
-    dfree(s.cw); dfree(s.pk); dfree(s.pr); dfree(s.pv); dfree(s.pb); dfree(s.spos);
+    dfree(s.cw); dfree(s.ctr); dfree(s.pk); dfree(s.pr); dfree(s.pv); dfree(s.pb); dfree(s.spos);
     dfree(s.ovk); dfree(s.ovi); dfree(s.ocnt); dfree(s.okb); dfree(s.operm); dfree(s.ores);
     dfree(s.ork); dfree(s.orv);
     if (s.ev_keys) (void)hipEventDestroy(s.ev_keys);
@@ -460,6 +462,8 @@ int alloc_shard(shm_shard* h) {
     s.pcap = P == 1 ? cap : std::min<uint64_t>(cap, get_slot_cap(cap, P));
     const uint64_t slots = (uint64_t)P * s.pcap;
     rc |= dalloc(&s.cw, 2 * (uint64_t)P + 2);
+    rc |= dalloc(&s.ctr, shm::dev::route_ctr_words(P));
+    if (s.ctr && hipMemset(s.ctr, 0, 4 * shm::dev::route_ctr_words(P)) != hipSuccess) rc |= SHM_EIO;
     rc |= dalloc(&s.pk, slots);
     rc |= dalloc(&s.pr, slots);
     rc |= dalloc(&s.pv, slots);
@@ -712,9 +716,13 @@ int shm_shard_search_begin(shm_shard* h, const uint64_t* keys, uint64_t n, void*
   s.busy = true;
   if (P == 1 && !h->force_route) return SHM_OK;  // nothing to route: _end is the local get
   // (forced: the own run crosses the transport like the peers')
-  shm::dev::launch_route_slots(s.keys, s.n, P, s.ncap, s.cw, s.pk, s.spos, s.ovk, s.ovi,
+  // the runs are padded once per capacity: later batches leave earlier keys
+  // of the same owner in the tails (searched, never gathered)
+  const bool fill = s.filled != s.ncap;
+  s.filled = s.ncap;
+  shm::dev::launch_route_slots(s.keys, s.n, P, s.ncap, s.cw, s.ctr, s.pk, s.spos, s.ovk, s.ovi,
                                shm__error_word(h->local), s.stream, me,
-                               h->force_route ? nullptr : s.pr + (uint64_t)me * s.ncap);
+                               h->force_route ? nullptr : s.pr + (uint64_t)me * s.ncap, fill);
   HIP_OK2(hipGetLastError());
   RC_OK(s.x->group_start());
   RC_OK(s.x->a2a_peers(s.pk, s.pr, s.ncap, 8, s.stream));
@@ -863,14 +871,42 @@ int shm_shard_range_values(shm_shard* h, uint64_t* vals_out, uint64_t vals_cap, 
 // placement can be checked on one GPU without P ranks (tests/test_gpu_shard.py).
 // cursor: P + 1 u32 of device scratch; ovk / ovi nullable (then the overflow
 // bit goes to t's error word).
+// the claim words of the hooks' placements (zero at rest; one call at a time)
+uint32_t* hook_ctr() {
+  static uint32_t* c = nullptr;
+  if (!c) {
+    const uint64_t bytes = 4 * shm::dev::route_ctr_words(64);
+    if (hipMalloc((void**)&c, bytes) != hipSuccess) return c = nullptr;
+    if (hipMemset(c, 0, bytes) != hipSuccess) {
+      (void)hipFree(c);
+      c = nullptr;
+    }
+  }
+  return c;
+}
 int shm__route_slots(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
                      uint32_t* cursor, uint64_t* slots, uint32_t* spos, uint64_t* ovk,
                      uint32_t* ovi, void* stream) {
   if (!t || !cursor || !slots || !spos || P == 0 || P > 64 || (n && !keys) ||
       (uint64_t)P * cap >= ~0u)
     return SHM_EINVAL;
-  shm::dev::launch_route_slots(keys, n, P, cap, cursor, slots, spos, ovk, ovi,
+  uint32_t* ctr = hook_ctr();
+  if (!ctr) return SHM_ENOMEM;
+  shm::dev::launch_route_slots(keys, n, P, cap, cursor, ctr, slots, spos, ovk, ovi,
                                shm__error_word(t), (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+}
+// ... and the shard's own form of it: the runs padded only when fill
+int shm__route_slots_ex(shm_tree* t, const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
+                        uint32_t* cursor, uint64_t* slots, uint32_t* spos, uint64_t* ovk,
+                        uint32_t* ovi, int fill, void* stream) {
+  if (!t || !cursor || !slots || !spos || P == 0 || P > 64 || (n && !keys) ||
+      (uint64_t)P * cap >= ~0u)
+    return SHM_EINVAL;
+  uint32_t* ctr = hook_ctr();
+  if (!ctr) return SHM_ENOMEM;
+  shm::dev::launch_route_slots(keys, n, P, cap, cursor, ctr, slots, spos, ovk, ovi,
+                               shm__error_word(t), (hipStream_t)stream, 0, nullptr, fill != 0);
   return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
 }
 int shm__route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* vals_out,

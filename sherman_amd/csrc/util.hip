@@ -407,37 +407,51 @@ __global__ __launch_bounds__(kT) void k_route_fill(uint64_t* out, uint64_t cap, 
     out[i] = kKeyMax;
 }
 
-// A block places 4096 keys (16 per thread): per round and wave, ranks among
-// the lanes of one owner by ballots (as k_route_scatter); per owner, ONE
-// global cursor claim for the whole block (a cursor word claimed per wave
-// serialises ~16 K atomics on one address per batch: 270 us at world 1).
+// A block of 1024 threads places 4096 keys (4 per thread): per round and
+// wave, ranks among the lanes of one owner by ballots (as k_route_scatter);
+// per owner, ONE global claim for the whole block.  Sixteen waves per block,
+// four per SIMD (round 5's 256-thread blocks of 16 keys per thread left one
+// wave per SIMD waiting on its loads and its block's claim).  The claim words
+// sit on lines of their own (ctr, kCtrStride words apart): a returning
+// device-scope atomic on one word saturates at ~88 per us (MI355X_MICROARCH
+// "dequeue"), and the 2048 claims of a 2^20-key batch at P = 8 on one line
+// took ~20 us (tools/route_p8.py); per line they are 256.  The last block
+// to finish copies the counts to cursor[0..P] (P runs, then the overflow
+// count: what the exchange and the host read) and returns the claim words
+// to zero, so no launch resets them.
 // A key past its run's capacity goes to the overflow list (ovk[j] = key,
 // ovi[j] = its input position; one claim per wave and round) and the
 // shard's second round returns its value (shard.cpp); without an overflow
 // list (ovk == nullptr) it finds nothing and kErrOverflow is reported.
-constexpr int kSlotPer = 16;
-constexpr int kSlotTile = kT * kSlotPer;
+constexpr int kSlotT = 1024;
 
-__global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__ keys, uint64_t n,
-                                                    uint32_t P, uint64_t cap,
-                                                    uint32_t* __restrict__ cursor,
-                                                    uint64_t* __restrict__ out,
-                                                    uint32_t* __restrict__ spos, uint64_t* ovk,
-                                                    uint32_t* ovi, uint32_t* err, uint32_t own_p,
-                                                    uint64_t* own_out) {
-  constexpr int kW = kT / kWave;
+template <int kSlotPer>
+__global__ __launch_bounds__(kSlotT) void k_route_slots(const uint64_t* __restrict__ keys,
+                                                        uint64_t n, uint32_t P, uint64_t cap,
+                                                        uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ ctr,
+                                                        uint64_t* __restrict__ out,
+                                                        uint32_t* __restrict__ spos, uint64_t* ovk,
+                                                        uint32_t* ovi, uint32_t* err, uint32_t own_p,
+                                                        uint64_t* own_out) {
+  constexpr int kW = kSlotT / kWave;
+  constexpr int kSlotTile = kSlotT * kSlotPer;
   __shared__ uint32_t wc[kSlotPer][kW][kRouteMaxShards];
+  __shared__ uint32_t last;
   const int t = threadIdx.x, w = t >> 6, lane = lane_id();
-  for (int j = t; j < kSlotPer * kW * kRouteMaxShards; j += kT) (&wc[0][0][0])[j] = 0;
-  __syncthreads();
+  for (int j = t; j < kSlotPer * kW * kRouteMaxShards; j += kSlotT) (&wc[0][0][0])[j] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kSlotTile;
   uint64_t kk[kSlotPer];
+#pragma unroll
+  for (int r = 0; r < kSlotPer; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSlotT + t;
+    kk[r] = i < n ? keys[i] : 0;
+  }
+  __syncthreads();
   uint32_t own[kSlotPer], rank[kSlotPer];
 #pragma unroll
   for (int r = 0; r < kSlotPer; ++r) {
-    const uint64_t i = base + (uint64_t)r * kT + t;
-    const bool valid = i < n;
-    kk[r] = valid ? keys[i] : 0;
+    const bool valid = base + (uint64_t)r * kSlotT + t < n;
     own[r] = valid ? owner_of(kk[r], P) : ~0u;
     rank[r] = 0;
     uint64_t pending = ballot(valid);
@@ -450,23 +464,42 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
     }
   }
   __syncthreads();
-  if ((uint32_t)t < P) {  // the block's claim on owner t's run, then (round, wave) bases
-    uint32_t tot = 0;
-    for (int r = 0; r < kSlotPer; ++r)
-      for (int x = 0; x < kW; ++x) tot += wc[r][x][t];
-    uint32_t run = tot ? atomicAdd(cursor + t, tot) : 0u;
-    for (int r = 0; r < kSlotPer; ++r)
-      for (int x = 0; x < kW; ++x) {
-        const uint32_t v = wc[r][x][t];
-        wc[r][x][t] = run;
-        run += v;
-      }
+  // one wave per owner: its 64 (round, wave) counts scanned across the
+  // lanes, the block's one claim on the owner's run, the bases written back
+  // (a thread per owner summing them in turn spent ~3 us in LDS latency)
+  constexpr int kQ = kSlotPer * kW;  // (round, wave) counts per owner
+  static_assert(kQ < kWave || kQ % kWave == 0, "whole lanes per (round, wave)");
+  constexpr int kE = kQ >= kWave ? kQ / kWave : 1;  // per lane
+  for (uint32_t p = (uint32_t)w; p < P; p += kW) {
+    uint32_t v[kE], sum = 0;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const int q = lane * kE + e;
+      v[e] = q < kQ ? wc[q / kW][q % kW][p] : 0u;
+      sum += v[e];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += y;
+    }
+    const uint32_t tot = rl32(incl, kWave - 1);
+    uint32_t run = 0;
+    if (lane == 0 && tot) run = atomicAdd(ctr + p * kCtrStride, tot);
+    run = rl32(run, 0) + incl - sum;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const int q = lane * kE + e;
+      if (q < kQ) wc[q / kW][q % kW][p] = run;
+      run += v[e];
+    }
   }
   __syncthreads();
   bool over = false;
 #pragma unroll
   for (int r = 0; r < kSlotPer; ++r) {
-    const uint64_t i = base + (uint64_t)r * kT + t;
+    const uint64_t i = base + (uint64_t)r * kSlotT + t;
     bool ov = false;
     if (own[r] != ~0u) {
       const uint32_t pos = wc[r][w][own[r]] + rank[r];
@@ -485,7 +518,7 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
     const uint64_t om = ballot(ov);  // wave-uniform
     if (om && ovk) {
       uint32_t ob = 0;
-      if (lane == 0) ob = atomicAdd(cursor + P, (uint32_t)popc64(om));
+      if (lane == 0) ob = atomicAdd(ctr + P * kCtrStride, (uint32_t)popc64(om));
       ob = rl32(ob, 0);
       if (ov) {
         const uint32_t j = ob + (uint32_t)popc64(om & lanemask_lt());
@@ -496,39 +529,91 @@ __global__ __launch_bounds__(kT) void k_route_slots(const uint64_t* __restrict__
     over |= ov;
   }
   if (over && !ovk) atomicOr(err, kErrOverflow);
+  // every claim of this block returned: the last block publishes the counts
+  __syncthreads();
+  if (t == 0) last = atomicAdd(ctr + (P + 1) * kCtrStride, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (last && (uint32_t)t <= P + 1) {
+    // read and reset in one atomic, at the point every claim went through
+    const uint32_t v = atomicExch(ctr + t * kCtrStride, 0u);
+    if ((uint32_t)t <= P) cursor[t] = v;
+  }
 }
 
+// fill: pad the runs with kKeyMax first (a slot's first batch, or one whose
+// capacity changed); otherwise the runs' tails keep the keys an earlier
+// batch placed there at the same capacity -- keys of the same owner's
+// range, searched and never gathered, exactly as padding.  ctr: (P + 2) *
+// kCtrStride words, zero at rest (route_ctr_words)
 void launch_route_slots(const uint64_t* keys, uint64_t n, uint32_t P, uint64_t cap,
-                        uint32_t* cursor, uint64_t* out, uint32_t* spos, uint64_t* ovk,
-                        uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own,
-                        uint64_t* own_out) {
+                        uint32_t* cursor, uint32_t* ctr, uint64_t* out, uint32_t* spos,
+                        uint64_t* ovk, uint32_t* ovi, uint32_t* err, hipStream_t s, uint32_t own,
+                        uint64_t* own_out, bool fill) {
   const uint64_t slots = (uint64_t)P * cap;
-  hipLaunchKernelGGL(k_route_fill, grid1(slots + 1), dim3(kT), 0, s, out, cap, cursor, P, own,
-                     own_out);
+  if (fill)
+    hipLaunchKernelGGL(k_route_fill, grid1(slots + 1), dim3(kT), 0, s, out, cap, cursor, P, own,
+                       own_out);
+  // four keys per thread: 256 blocks for 2^20 keys (one or two keys per
+  // thread, or eight, measured no better at P = 8: tools/route_p8.py)
   if (n)
-    hipLaunchKernelGGL(k_route_slots, grid1(n, kSlotTile), dim3(kT), 0, s, keys, n, P, cap, cursor,
-                       out, spos, ovk, ovi, err, own, own_out);
+    hipLaunchKernelGGL(k_route_slots<4>, grid1(n, kSlotT * 4), dim3(kSlotT), 0, s, keys, n, P,
+                       cap, cursor, ctr, out, spos, ovk, ovi, err, own, own_out);
+  else if (!fill)
+    (void)hipMemsetAsync(cursor, 0, sizeof(uint32_t) * (P + 1), s);
 }
 
 // out[i] = in[spos[i]] (0 for a key cut by a full run: the overflow round
-// fills it afterwards), found[i] = out[i] != 0 (Tree.cpp:445-448)
+// fills it afterwards), found[i] = out[i] != 0 (Tree.cpp:445-448).  Four
+// inputs per thread when the buffers allow 16 B accesses: one spos load, four
+// gathers in flight, two 16 B value stores and one 4 B found store
+__device__ __forceinline__ uint64_t gather_one(const uint64_t* in, uint32_t x, uint64_t own_lo,
+                                               uint64_t cap, const uint64_t* own_src) {
+  if (x == ~0u) return kValueNull;
+  return own_src && x - own_lo < cap ? own_src[x] : in[x];
+}
 __global__ void k_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n,
                                uint64_t* out, uint8_t* found, uint64_t own_lo, uint64_t cap,
                                const uint64_t* own_src) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t x = spos[i];
-  uint64_t v = kValueNull;
-  if (x != ~0u) v = own_src && x - own_lo < cap ? own_src[x] : in[x];
+  const uint64_t v = gather_one(in, spos[i], own_lo, cap, own_src);
   out[i] = v;
   if (found) found[i] = v != kValueNull ? 1 : 0;
+}
+__global__ void k_route_gather4(const uint64_t* in, const uint32_t* spos, uint64_t n4,
+                                uint64_t* out, uint8_t* found, uint64_t own_lo, uint64_t cap,
+                                const uint64_t* own_src) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n4) return;
+  const uint4 x = reinterpret_cast<const uint4*>(spos)[j];
+  const uint64_t v0 = gather_one(in, x.x, own_lo, cap, own_src);
+  const uint64_t v1 = gather_one(in, x.y, own_lo, cap, own_src);
+  const uint64_t v2 = gather_one(in, x.z, own_lo, cap, own_src);
+  const uint64_t v3 = gather_one(in, x.w, own_lo, cap, own_src);
+  ulonglong2* o = reinterpret_cast<ulonglong2*>(out) + 2 * j;
+  o[0] = make_ulonglong2(v0, v1);
+  o[1] = make_ulonglong2(v2, v3);
+  if (found)
+    reinterpret_cast<uint32_t*>(found)[j] = (v0 != kValueNull ? 1u : 0u) |
+                                            (v1 != kValueNull ? 1u << 8 : 0u) |
+                                            (v2 != kValueNull ? 1u << 16 : 0u) |
+                                            (v3 != kValueNull ? 1u << 24 : 0u);
 }
 void launch_route_gather(const uint64_t* in, const uint32_t* spos, uint64_t n, uint64_t* out,
                          uint8_t* found, hipStream_t s, uint32_t own, uint64_t cap,
                          const uint64_t* own_src) {
-  if (n)
-    hipLaunchKernelGGL(k_route_gather, grid1(n), dim3(kT), 0, s, in, spos, n, out, found,
-                       (uint64_t)own * cap, cap, own_src);
+  if (!n) return;
+  const uint64_t lo = (uint64_t)own * cap;
+  const bool vec = ((reinterpret_cast<uintptr_t>(spos) | reinterpret_cast<uintptr_t>(out)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(found) & 3) == 0;
+  const uint64_t n4 = vec ? n / 4 : 0;
+  if (n4)
+    hipLaunchKernelGGL(k_route_gather4, grid1(n4), dim3(kT), 0, s, in, spos, n4, out, found, lo,
+                       cap, own_src);
+  if (n > 4 * n4)
+    hipLaunchKernelGGL(k_route_gather, grid1(n - 4 * n4), dim3(kT), 0, s, in, spos + 4 * n4,
+                       n - 4 * n4, out + 4 * n4, found ? found + 4 * n4 : nullptr, lo, cap,
+                       own_src);
 }
 
 // the overflow round's results: out[ovi[perm[j]]] = in[j] (perm: the
