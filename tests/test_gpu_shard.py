@@ -121,6 +121,76 @@ def test_routed_gpu_shards_match_unsharded_oracle(backend, world, cabi):
         verify_against_unsharded(d, world)
 
 
+def test_slot_padding_once_per_capacity():
+    """The shard's placement pads its runs with kKeyMax only when a slot's
+    capacity changes (shm__route_slots_ex fill); later batches leave earlier
+    keys in the runs' tails.  Those must be keys of the run's own owner (so
+    the owner's walk never sees a key outside its range), the counts each
+    batch publishes must be its own (the claim words return to zero after
+    every launch), and the gathered results must equal a plain search."""
+    import ctypes
+
+    import sherman_amd as shm
+    from sherman_amd.shard import owner_of
+
+    L = shm.lib()
+    L.shm__route_slots_ex.restype = ctypes.c_int
+    L.shm__route_slots_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    L.shm__route_gather.restype = ctypes.c_int
+    L.shm__route_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    P = 8
+    rng = np.random.default_rng(77)
+    keys = np.unique(rng.integers(1, (1 << 64) - 2, 60000, dtype=np.uint64))
+    t = shm.Tree(arena_bytes=64 << 20, max_batch=1 << 16)
+    kd = torch.from_numpy(keys.view(np.int64)).to(dev)
+    t.insert_batch(kd, kd ^ 0x77)
+    cursor = torch.zeros(P + 1, dtype=torch.int32, device=dev)
+    ovk = torch.zeros(1 << 15, dtype=torch.int64, device=dev)
+    ovi = torch.zeros(1 << 15, dtype=torch.int32, device=dev)
+    filled = None
+    for rnd, n in enumerate([20000, 20000, 12000, 20000, 20000]):
+        cap = n // P + 6 * int(np.sqrt(n // P)) + 256
+        if filled is None or filled[0] != cap:
+            slots = torch.empty(P * cap, dtype=torch.int64, device=dev)
+            fill = 1
+        else:
+            slots, fill = filled[1], 0
+        filled = (cap, slots)
+        q = np.concatenate([keys[rng.integers(0, keys.size, n - 500)],
+                            rng.integers(1, (1 << 64) - 2, 500, dtype=np.uint64)])
+        qd = torch.from_numpy(q.view(np.int64)).to(dev)
+        spos = torch.empty(n, dtype=torch.int32, device=dev)
+        assert L.shm__route_slots_ex(t.h, qd.data_ptr(), n, P, cap, cursor.data_ptr(),
+                                     slots.data_ptr(), spos.data_ptr(), ovk.data_ptr(),
+                                     ovi.data_ptr(), fill, None) == 0
+        res = torch.empty_like(slots)
+        t.search_batch(slots, res)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        fnd = torch.empty(n, dtype=torch.uint8, device=dev)
+        assert L.shm__route_gather(res.data_ptr(), spos.data_ptr(), n, out.data_ptr(),
+                                   fnd.data_ptr(), None) == 0
+        v, f = torch.empty_like(qd), torch.empty(n, dtype=torch.uint8, device=dev)
+        t.search_batch(qd, v, f)
+        torch.cuda.synchronize()
+        assert torch.equal(out, v) and torch.equal(fnd, f), rnd
+        cur = cursor.cpu().numpy()
+        qo = owner_of(qd.cpu(), P).numpy()
+        assert np.array_equal(cur[:P], np.bincount(qo, minlength=P)), rnd  # this batch's own
+        assert cur[P] == 0
+        sl = slots.cpu().numpy().view(np.uint64).reshape(P, cap)
+        so = owner_of(torch.from_numpy(sl.reshape(-1).view(np.int64)), P).numpy().reshape(P, cap)
+        pad = sl == np.uint64((1 << 64) - 1)
+        # every slot: kKeyMax padding or a key of the run's owner
+        assert bool(np.all(pad | (so == np.arange(P)[:, None]))), rnd
+    t.close()
+
+
 @pytest.mark.parametrize("P", [2, 3, 8])
 def test_slot_routed_get_p_shards_on_one_gpu(P):
     """The C-ABI shard's get placement for P > 1 without P ranks: P trees on
