@@ -496,6 +496,7 @@ def main():
             slot_status = torch.zeros(2, dtype=torch.int64, device=dev)
             torch.cuda.synchronize()
 
+        rq_caps = []  # routed async scans: (vals_cap, peer_cap)
         pipe = slots and args.pipeline and s_ins is not None
         ticket = [None]  # the ordered, not yet applied batch (pipeline)
         if pipe:
@@ -558,8 +559,20 @@ def main():
             elif route is None:
                 scan_out["r"] = PendingRange(None, *tree.range_query_batch(lo, hi))
                 tree.insert_batch_async(pk, pv)
+            elif cshard is not None and rq_caps:
+                # routed scans with no host read-back: fixed runs per peer
+                # sized from the first (synchronous) batch; every step's
+                # status is checked after the run
+                c, _, v, st = cshard.range_query_async(lo, hi, rq_caps[0], rq_caps[1], n_cap)
+                scan_out["r"] = PendingRange(None, c, v)
+                scan_out.setdefault("rstat", []).append(st)
+                route.insert(pk, pv)
             else:
-                scan_out["r"] = PendingRange(None, *route.range_query(lo, hi, n_cap))
+                c, v = route.range_query(lo, hi, n_cap)
+                scan_out["r"] = PendingRange(None, c, v)
+                if cshard is not None:
+                    t_ = int(v.numel())
+                    rq_caps[:] = [t_ + t_ // 2 + (1 << 16), (t_ * 5) // (4 * world) + (1 << 13)]
                 route.insert(pk, pv)
 
         def done_streams(i):
@@ -708,6 +721,10 @@ def main():
             ovf, err = (int(x) for x in scan_out["slots"].cpu().tolist())
             # no scan of any step so far passed its slot, no device error
             assert err == 0 and ovf == 0, (ovf, err)
+        for st in scan_out.pop("rstat", []):
+            tot_, flags = (int(x) for x in st.cpu().tolist())
+            # every routed async batch complete: no run past its peer cap
+            assert flags == 0, (tot_, flags)
         c, _ = scan_out["r"].result()
         hit_rate = float(c.float().mean().item())  # mean values per scan
     else:

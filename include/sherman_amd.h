@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SHM_ABI_VERSION 10
+#define SHM_ABI_VERSION 11
 
 /* status codes (negative errno style) */
 #define SHM_OK 0
@@ -413,6 +413,21 @@ int shm_shard_range_query(shm_shard *s, const uint64_t *from, const uint64_t *to
                           uint64_t n_cap, uint64_t *counts_out, uint64_t *offsets_out,
                           uint64_t *vals_out, uint64_t vals_cap, uint64_t *total_out,
                           void *stream);
+/* The same batch with no host synchronisation: the values
+ * travel in fixed runs of peer_cap values per peer each way (the same on
+ * every rank), padded on the device, so nothing is read back to size the
+ * exchange.  counts_out / offsets_out as above; status (2 device words,
+ * written on the stream): status[0] = the batch's total values, status[1] =
+ * flags -- 1: a run to or from a peer passed peer_cap (values lost), 2: the
+ * scan pass's buffer was short, 4: total > vals_cap (values past vals_cap
+ * dropped), 8: a device error of the scans.  Nonzero flags: the batch's
+ * values are incomplete; repeat it with shm_shard_range_query (before any
+ * tree change).  Sizing: peer_cap ~ 1.25 x the values a rank's scans find
+ * on one shard, + a few thousand. */
+int shm_shard_range_query_async(shm_shard *s, const uint64_t *from, const uint64_t *to,
+                                uint64_t n, uint64_t n_cap, uint64_t *counts_out,
+                                uint64_t *offsets_out, uint64_t *vals_out, uint64_t vals_cap,
+                                uint64_t peer_cap, uint64_t *status, void *stream);
 /* the last shm_shard_range_query batch's values (its offsets_out must still
  * be live), local only: valid until the next call on the shard */
 int shm_shard_range_values(shm_shard *s, uint64_t *vals_out, uint64_t vals_cap, void *stream);

@@ -120,7 +120,7 @@ class ShmProfile(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 10  # SHM_ABI_VERSION in include/sherman_amd.h
+ABI_VERSION = 11  # SHM_ABI_VERSION in include/sherman_amd.h
 
 # (name, restype, argtypes) — every symbol declared in include/sherman_amd.h
 _SIGNATURES = [
@@ -169,6 +169,8 @@ _SIGNATURES = [
     ("shm_shard_insert", ctypes.c_int, [vp, vp, vp, u64, vp]),
     ("shm_shard_range_query", ctypes.c_int,
      [vp, vp, vp, u64, u64, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
+    ("shm_shard_range_query_async", ctypes.c_int,
+     [vp, vp, vp, u64, u64, vp, vp, vp, u64, u64, vp, vp]),
     ("shm_shard_synchronize", ctypes.c_int, [vp]),
     ("shm_shard_range_values", ctypes.c_int, [vp, vp, u64, vp]),
     ("shm_lock_bench", ctypes.c_int, [vp, vp, u64, vp]),
@@ -773,6 +775,28 @@ class CShard:
                                               _stream_ptr(stream))
         _check(rc, "shard_range_query")
         return counts, vals[:total]
+
+    def range_query_async(self, lo, hi, vals_cap, peer_cap, n_cap=None, stream=None,
+                          status=None):
+        """range_query with no host synchronisation (shm_shard_range_query_async):
+        the values travel in fixed runs of peer_cap per peer.  Returns
+        (counts, offsets, vals[vals_cap], status): status[0] the total,
+        status[1] flags (nonzero: incomplete, repeat with range_query before
+        any tree change), all written on `stream`."""
+        import torch
+        n, dev = lo.numel(), lo.device
+        if n_cap is None:
+            n_cap = self.tree.max_batch // self.world
+        counts = torch.empty(n, dtype=torch.int64, device=dev)
+        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        vals = torch.empty(max(vals_cap, 1), dtype=torch.int64, device=dev)
+        if status is None:
+            status = torch.zeros(2, dtype=torch.int64, device=dev)
+        _check(lib().shm_shard_range_query_async(self.h, _ptr(lo), _ptr(hi), n, n_cap,
+                                                 _ptr(counts), _ptr(offs), _ptr(vals), vals_cap,
+                                                 peer_cap, _ptr(status), _stream_ptr(stream)),
+               "shard_range_query_async")
+        return counts, offs, vals, status
 
     def synchronize(self):
         _check(lib().shm_shard_synchronize(self.h), "shard_synchronize")

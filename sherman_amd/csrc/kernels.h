@@ -541,7 +541,10 @@ void launch_range_sums(const uint64_t* rc, const uint64_t* bc, uint64_t n, uint6
 // vals[offsets[j] ...] in shard order, bounded by vals_cap
 void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_t* bsc,
                            uint64_t n, uint64_t cap, uint32_t P, const uint64_t* offsets,
-                           uint64_t* vals, uint64_t vals_cap, hipStream_t s);
+                           uint64_t* vals, uint64_t vals_cap, hipStream_t s, uint64_t pitch = 0);
+void launch_range_pitch(const uint64_t* rvals, const uint64_t* rw, uint32_t P, uint64_t pitch,
+                        uint64_t* out, uint64_t rvcap, uint64_t vals_cap, uint64_t* status,
+                        hipStream_t s);
 
 // Tree::lock_bench over the HBM lock table: each key's word taken (atomicCAS
 // to tag | 1) and released (tag), bounded spins (kErrLock)

@@ -407,6 +407,8 @@ struct ExclCtx {
   uint64_t rvcap = 0;
   uint64_t* bv = nullptr;     // the values received back
   uint64_t bvcap = 0;
+  uint64_t* pvs = nullptr;    // async scans: the values to send, peer_cap per peer
+  uint64_t pvscap = 0;
   uint64_t* rw = nullptr;     // [2P + 8] small words read back once per scan batch
   // the last batch, for shm_shard_range_values after SHM_ENOSPC
   uint64_t last_n = 0, last_ncap = 0, last_total = 0;
@@ -445,7 +447,7 @@ void free_shard(shm_shard* h) {
   ExclCtx& e = h->ex;
   dfree(e.icnt); dfree(e.kb); dfree(e.vb); dfree(e.perm); dfree(e.pk); dfree(e.pv); dfree(e.rk);
   dfree(e.rv); dfree(e.ork); dfree(e.orv); dfree(e.plo); dfree(e.phi); dfree(e.rlo); dfree(e.rhi);
-  dfree(e.rc); dfree(e.roff); dfree(e.bc); dfree(e.bsc); dfree(e.rvals); dfree(e.bv); dfree(e.rw);
+  dfree(e.rc); dfree(e.roff); dfree(e.bc); dfree(e.bsc); dfree(e.rvals); dfree(e.bv); dfree(e.pvs); dfree(e.rw);
   if (e.ev_ins) (void)hipEventDestroy(e.ev_ins);
   if (h->side) (void)hipStreamDestroy(h->side);
   // xp[0] may own the base communicator: destroy the splits first
@@ -788,23 +790,18 @@ int shm_shard_insert(shm_shard* h, const uint64_t* keys, const uint64_t* vals, u
   return shm__insert_batch_padded(h->local, e.rk, e.rv, (uint64_t)P * e.icap, s);
 }
 
-int shm_shard_range_query(shm_shard* h, const uint64_t* from, const uint64_t* to, uint64_t n,
-                          uint64_t n_cap, uint64_t* counts_out, uint64_t* offsets_out,
-                          uint64_t* vals_out, uint64_t vals_cap, uint64_t* total_out,
-                          void* stream) {
-  if (!h || !total_out || n > n_cap || (n && (!from || !to || !counts_out || !offsets_out)) ||
-      (vals_cap && !vals_out))
-    return SHM_EINVAL;
+}  // extern "C"
+
+namespace {
+// steps 1-3 of a routed range scan batch, all on the device: pieces to their
+// shards, the local scans of the received pieces (values packed in rvals,
+// row p = rank p's), counts back, per-peer totals (rw), counts_out,
+// offsets_out and the received runs' offsets (bsc)
+int range_scan_pieces(shm_shard* h, const uint64_t* from, const uint64_t* to, uint64_t n,
+                      uint64_t n_cap, uint64_t* counts_out, uint64_t* offsets_out, hipStream_t s) {
   const uint32_t P = h->world;
   const uint64_t m = (uint64_t)P * n_cap;
-  if (m > h->cap) return SHM_E2BIG;
-  RC_OK(flush(h));
   ExclCtx& e = h->ex;
-  e.last_ok = false;
-  hipStream_t s = (hipStream_t)stream;
-  RC_OK(ensure_pieces(h, m, s));
-  // about n_cap non-empty pieces of ~100 values (C5): grown when a batch needs more
-  if (!e.rvals) RC_OK(ensure(e.rvals, e.rvcap, std::max<uint64_t>(n_cap * 160, 1u << 20), s));
   uint64_t* rw = e.rw;  // [0, P) sent, [P, 2P) received, scanner {total, err}, scans {total, err}, bsc {total, err}
   // 1. pieces, row p to rank p
   shm::dev::launch_range_pieces(from, to, n, n_cap, P, h->bnd, e.plo, e.phi, s);
@@ -822,6 +819,31 @@ int shm_shard_range_query(shm_shard* h, const uint64_t* from, const uint64_t* to
   HIP_OK2(hipGetLastError());
   RC_OK(shm__scan_u64(h->local, counts_out, offsets_out, n, rw + 2 * P + 2, s));
   RC_OK(shm__scan_u64(h->local, e.bc, e.bsc, m, rw + 2 * P + 4, s));
+  return SHM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int shm_shard_range_query(shm_shard* h, const uint64_t* from, const uint64_t* to, uint64_t n,
+                          uint64_t n_cap, uint64_t* counts_out, uint64_t* offsets_out,
+                          uint64_t* vals_out, uint64_t vals_cap, uint64_t* total_out,
+                          void* stream) {
+  if (!h || !total_out || n > n_cap || (n && (!from || !to || !counts_out || !offsets_out)) ||
+      (vals_cap && !vals_out))
+    return SHM_EINVAL;
+  const uint32_t P = h->world;
+  const uint64_t m = (uint64_t)P * n_cap;
+  if (m > h->cap) return SHM_E2BIG;
+  RC_OK(flush(h));
+  ExclCtx& e = h->ex;
+  e.last_ok = false;
+  hipStream_t s = (hipStream_t)stream;
+  RC_OK(ensure_pieces(h, m, s));
+  // about n_cap non-empty pieces of ~100 values (C5): grown when a batch needs more
+  if (!e.rvals) RC_OK(ensure(e.rvals, e.rvcap, std::max<uint64_t>(n_cap * 160, 1u << 20), s));
+  uint64_t* rw = e.rw;
+  RC_OK(range_scan_pieces(h, from, to, n, n_cap, counts_out, offsets_out, s));
   // 4. the one host synchronisation: the value counts each way
   std::vector<uint64_t> w(2 * P + 6);
   RC_OK(shm_read_words(h->local, rw, 8ull * (2 * P + 6), w.data(), s));
@@ -854,6 +876,42 @@ int shm_shard_range_query(shm_shard* h, const uint64_t* from, const uint64_t* to
   if (total > vals_cap) return SHM_ENOSPC;
   shm::dev::launch_range_assemble(e.bv, e.bc, e.bsc, n, n_cap, P, offsets_out, vals_out, vals_cap,
                                   s);
+  return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
+}
+
+int shm_shard_range_query_async(shm_shard* h, const uint64_t* from, const uint64_t* to,
+                                uint64_t n, uint64_t n_cap, uint64_t* counts_out,
+                                uint64_t* offsets_out, uint64_t* vals_out, uint64_t vals_cap,
+                                uint64_t peer_cap, uint64_t* status, void* stream) {
+  if (!h || !status || n > n_cap || (n && (!from || !to || !counts_out || !offsets_out)) ||
+      (vals_cap && !vals_out) || peer_cap == 0)
+    return SHM_EINVAL;
+  const uint32_t P = h->world;
+  const uint64_t m = (uint64_t)P * n_cap;
+  if (m > h->cap) return SHM_E2BIG;
+  RC_OK(flush(h));
+  ExclCtx& e = h->ex;
+  e.last_ok = false;
+  hipStream_t s = (hipStream_t)stream;
+  RC_OK(ensure_pieces(h, m, s));
+  // fixed runs of peer_cap values per peer each way: the scan pass's buffer
+  // holds every run that fits (a longer one is flagged, not grown)
+  const uint64_t runs = (uint64_t)P * peer_cap;
+  RC_OK(ensure(e.rvals, e.rvcap, runs, s));
+  RC_OK(ensure(e.pvs, e.pvscap, runs, s));
+  RC_OK(ensure(e.bv, e.bvcap, runs, s));
+  RC_OK(range_scan_pieces(h, from, to, n, n_cap, counts_out, offsets_out, s));
+  // 4. the runs padded to peer_cap on the device, exchanged whole
+  shm::dev::launch_range_pitch(e.rvals, e.rw, P, peer_cap, e.pvs, e.rvcap, vals_cap, status, s);
+  HIP_OK2(hipGetLastError());
+  RC_OK(e.x->a2a(e.pvs, e.bv, peer_cap, 8, s));
+  e.last_n = n;
+  e.last_ncap = n_cap;
+  e.last_total = 0;  // on the device (status[0])
+  e.last_off = offsets_out;
+  e.last_ok = false;  // shm_shard_range_values needs the host total: not after this call
+  shm::dev::launch_range_assemble(e.bv, e.bc, e.bsc, n, n_cap, P, offsets_out, vals_out, vals_cap,
+                                  s, peer_cap);
   return hipGetLastError() == hipSuccess ? SHM_OK : SHM_EIO;
 }
 

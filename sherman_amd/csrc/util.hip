@@ -726,32 +726,75 @@ void launch_range_sums(const uint64_t* rc, const uint64_t* bc, uint64_t n, uint6
 
 // Scan j's values, in shard order (= key order across shards): piece (p, j)
 // holds bc[p][j] values at bv[bsc[p][j]] (bsc: exclusive scan of bc in
-// row-major order, the layout of the received value runs); they go to
-// vals[offsets[j] + sum of its earlier pieces], values past vals_cap dropped.
-// One wave per scan.
+// row-major order, the layout of the received value runs; pitch != 0: row
+// p's run starts at bv[p * pitch] and holds at most pitch values, the
+// exchange without a host read-back); they go to vals[offsets[j] + sum of
+// its earlier pieces], values past vals_cap dropped.  One wave per scan.
 __global__ __launch_bounds__(kT) void k_range_assemble(const uint64_t* bv, const uint64_t* bc,
                                                        const uint64_t* bsc, uint64_t n,
                                                        uint64_t cap, uint32_t P,
                                                        const uint64_t* offsets, uint64_t* vals,
-                                                       uint64_t vals_cap) {
+                                                       uint64_t vals_cap, uint64_t pitch) {
   const uint64_t j = ((uint64_t)blockIdx.x * kT + threadIdx.x) / kWave;
   if (j >= n) return;
   const int lane = lane_id();
   uint64_t dst = offsets[j];
   for (uint32_t p = 0; p < P; ++p) {
     const uint64_t c = bc[(uint64_t)p * cap + j];
-    const uint64_t src = bsc[(uint64_t)p * cap + j];
-    for (uint64_t k = (uint64_t)lane; k < c; k += kWave)
+    const uint64_t x = bsc[(uint64_t)p * cap + j];
+    // pitched: the piece's place inside row p's run, cut at the run's end
+    const uint64_t rel = pitch ? x - bsc[(uint64_t)p * cap] : 0;
+    const uint64_t src = pitch ? (uint64_t)p * pitch + rel : x;
+    const uint64_t cc = pitch ? (rel >= pitch ? 0 : c < pitch - rel ? c : pitch - rel) : c;
+    for (uint64_t k = (uint64_t)lane; k < cc; k += kWave)
       if (dst + k < vals_cap) vals[dst + k] = bv[src + k];
     dst += c;
   }
 }
 void launch_range_assemble(const uint64_t* bv, const uint64_t* bc, const uint64_t* bsc,
                            uint64_t n, uint64_t cap, uint32_t P, const uint64_t* offsets,
-                           uint64_t* vals, uint64_t vals_cap, hipStream_t s) {
+                           uint64_t* vals, uint64_t vals_cap, hipStream_t s, uint64_t pitch) {
   if (n)
     hipLaunchKernelGGL(k_range_assemble, grid1(n * kWave), dim3(kT), 0, s, bv, bc, bsc, n, cap, P,
-                       offsets, vals, vals_cap);
+                       offsets, vals, vals_cap, pitch);
+}
+
+// The routed scan's value exchange without a host read-back: the scanner's
+// packed values (row p = the values for rank p's scans, rw[p] of them, rows
+// in order) copied to fixed runs of pitch values per peer, sent whole.  Block
+// 0 also writes the batch's status for the caller: status[0] = its scans'
+// total (rw[2P + 2]), status[1] = flags (1: a run to or from a peer passed
+// pitch, 2: the scan pass dropped values past its buffer, 4: total > vals_cap,
+// 8: a device error word of the scans).  Grid-stride copy, rows by blockIdx.y.
+__global__ __launch_bounds__(kT) void k_range_pitch(const uint64_t* rvals, const uint64_t* rw,
+                                                    uint32_t P, uint64_t pitch, uint64_t* out,
+                                                    uint64_t rvcap, uint64_t vals_cap,
+                                                    uint64_t* status) {
+  const uint32_t p = blockIdx.y;
+  uint64_t off = 0;
+  for (uint32_t q = 0; q < p; ++q) off += rw[q];
+  const uint64_t c = rw[p] < pitch ? rw[p] : pitch;
+  for (uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x; k < c; k += (uint64_t)gridDim.x * kT)
+    if (off + k < rvcap) out[(uint64_t)p * pitch + k] = rvals[off + k];
+  if (p == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t f = 0;
+    for (uint32_t q = 0; q < P; ++q)
+      if (rw[q] > pitch || rw[P + q] > pitch) f |= 1;
+    if (rw[2 * P] > rvcap) f |= 2;
+    if (rw[2 * P + 2] > vals_cap) f |= 4;
+    if (rw[2 * P + 1] || rw[2 * P + 3] || rw[2 * P + 5]) f |= 8;
+    status[0] = rw[2 * P + 2];
+    status[1] = f;
+  }
+}
+void launch_range_pitch(const uint64_t* rvals, const uint64_t* rw, uint32_t P, uint64_t pitch,
+                        uint64_t* out, uint64_t rvcap, uint64_t vals_cap, uint64_t* status,
+                        hipStream_t s) {
+  uint64_t bx = (pitch + kT - 1) / kT;
+  if (bx > 64) bx = 64;
+  if (bx == 0) bx = 1;
+  hipLaunchKernelGGL(k_range_pitch, dim3((unsigned)bx, P), dim3(kT), 0, s, rvals, rw, P, pitch,
+                     out, rvcap, vals_cap, status);
 }
 
 // ---- Tree::lock_bench (src/Tree.cpp:310-321): take and release the lock word

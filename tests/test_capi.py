@@ -47,7 +47,7 @@ def test_config_layout_and_defaults():
     assert cfg.key_lo == 0 and cfg.key_bits == 64
     assert cfg.flags == shm.SHM_FLAG_LEAF_DIR | shm.SHM_FLAG_AUTO_SORT_GETS
     assert cfg.max_batch == 1 << 20 and cfg.num_locks == 16384  # kNumOfLock (Common.h:87-93)
-    assert shm.lib().shm_abi_version() == shm.ABI_VERSION == 10
+    assert shm.lib().shm_abi_version() == shm.ABI_VERSION == 11
     assert shm.lib().shm_strerror(shm.SHM_EINVAL).startswith(b"invalid")
 
 

@@ -131,11 +131,24 @@ def run_rank(r, trees, group, stream, out, errs):
             for name, (lo, hi) in (("wide", scan_batch(r, P)), ("narrow", narrow_scans(r))):
                 c, sv = cs.range_query(d(lo), d(hi), n_cap=64, stream=stream)
                 scans[name] = (c, sv)
+            # the same scans with no host read-back (fixed runs per peer), and
+            # once with runs too short for them (flagged, not silently cut)
+            asy = {}
+            for name, (lo, hi) in (("wide", scan_batch(r, P)), ("narrow", narrow_scans(r))):
+                ac, _, av, st = cs.range_query_async(d(lo), d(hi), vals_cap=1 << 19,
+                                                     peer_cap=1 << 18, n_cap=64, stream=stream)
+                asy[name] = (ac, av, st)
+            lo, hi = scan_batch(r, P)
+            _, _, _, st_short = cs.range_query_async(d(lo), d(hi), vals_cap=1 << 16, peer_cap=1,
+                                                     n_cap=64, stream=stream)
             cs.synchronize()
             stream.synchronize()
             out[r] = ({k: (a.cpu().numpy().view(U64), b.cpu().numpy()) for k, (a, b) in res.items()},
                       {k: (a.cpu().numpy(), b.cpu().numpy().view(U64)) for k, (a, b) in scans.items()},
-                      km)
+                      km,
+                      {k: (a.cpu().numpy(), b.cpu().numpy().view(U64), c.cpu().numpy())
+                       for k, (a, b, c) in asy.items()},
+                      st_short.cpu().numpy())
             cs.close()
     except BaseException as e:  # noqa: BLE001 - reported by the main thread
         errs.append((r, repr(e)))
@@ -196,7 +209,12 @@ def test_local_group_p8_routed_paths():
     assert np.array_equal(uv[o], rv)
     key_of = dict(zip(rv.tolist(), rk.tolist()))
     for r in range(P):
-        res, scans, _ = out[r]
+        res, scans, _, asy, st_short = out[r]
+        for name, (c, sv) in scans.items():
+            ac, av, st = asy[name]
+            assert st[1] == 0 and st[0] == sv.size, (r, name, st)
+            assert np.array_equal(ac, c) and np.array_equal(av[:sv.size], sv), (r, name)
+        assert st_short[1] & 1, (r, st_short)  # runs past peer_cap are flagged
         qs = rank_queries(r)
         for name, q in list(qs.items()) + [("inflight_zipf", qs["zipf"]),
                                             ("inflight_shard0", qs["shard0"])]:
