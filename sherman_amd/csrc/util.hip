@@ -448,20 +448,27 @@ __global__ __launch_bounds__(kSlotT) void k_route_slots(const uint64_t* __restri
     kk[r] = i < n ? keys[i] : 0;
   }
   __syncthreads();
+  // ranks among the wave's lanes of one owner from the owner's bit planes:
+  // one ballot per bit (3 at P = 8), each lane keeping the lanes that agree
+  // with its owner on every bit, and lane o < P the lanes whose owner is o
+  // (its count).  A pass per owner present in the wave (readlane, ballot,
+  // LDS store per pass) took 5-6 of the kernel's 12.4 us at P = 8
+  // (tools/route_p8.py, the passes skipped: 6.8 us)
+  const int nb = P > 1 ? 32 - __clz((int)(P - 1)) : 0;
   uint32_t own[kSlotPer], rank[kSlotPer];
 #pragma unroll
   for (int r = 0; r < kSlotPer; ++r) {
     const bool valid = base + (uint64_t)r * kSlotT + t < n;
     own[r] = valid ? owner_of(kk[r], P) : ~0u;
-    rank[r] = 0;
-    uint64_t pending = ballot(valid);
-    while (pending) {  // one pass per owner present in this wave
-      const uint32_t o = rl32(own[r], ctz64(pending));
-      const uint64_t m = ballot(own[r] == o);
-      if (own[r] == o) rank[r] = popc64(m & lanemask_lt());
-      if (lane == 0) wc[r][w][o] = popc64(m);
-      pending &= ~m;
+    const uint64_t vm = ballot(valid);
+    uint64_t mine = vm, mine_o = vm;
+    for (int b = 0; b < nb; ++b) {
+      const uint64_t bb = ballot(valid && ((own[r] >> b) & 1u));
+      mine &= ((own[r] >> b) & 1u) ? bb : ~bb;
+      mine_o &= ((lane >> b) & 1) ? bb : ~bb;
     }
+    rank[r] = valid ? popc64(mine & lanemask_lt()) : 0u;
+    if ((uint32_t)lane < P) wc[r][w][lane] = popc64(mine_o);
   }
   __syncthreads();
   // one wave per owner: its 64 (round, wave) counts scanned across the
