@@ -155,6 +155,7 @@ struct shm_tree {
   bool dir_off = false;      // no directory could be allocated: walks from the root
   bool dir_exact = false;    // built with upkeep on, and upkeep on ever since (WalkArgs.dir_exact)
   bool dir_maint_always = false;  // shm__dir_config maint 2: every chunk keeps it (tests)
+  bool dir_last_upkept = false;   // the previous chunk kept the directory
   double dir_debt_ps = 0.0;  // gets' estimated extra cost on shared prefixes since the build
   // LDS replica of the top of the tree (SHM_FLAG_TOP_LDS without the
   // directory; launch_top), rebuilt with the same staleness rule
@@ -1034,6 +1035,10 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   set_dir(t, &u.dir, &u.dir_lo, &u.dir_shift, &u.dir_n);
   if (u.dir) u.dir_hint = t->dir_hint;
   if (u.dir && upkeep) {  // the chunk's directory upkeep after its k_upper (dir_upkeep.h)
+    // the first kept chunk after chunks that were not: its parity's list
+    // count may still hold the count of the last kept chunk of that parity
+    // (each repair zeroes only the other parity's, for the chunk after it)
+    if (!t->dir_last_upkept) HIP_OK(hipMemsetAsync(t->dir_fix_n + u.par, 0, sizeof(uint32_t), s));
     u.dir_w = t->dir;
     u.dir_form = t->dir_pairs ? dev::kDirFormPairs : dev::kDirFormFp;
     u.dir_fix = t->dir_fix;
@@ -1093,6 +1098,7 @@ int insert_apply(shm_tree* t, hipStream_t s, uint64_t n, uint32_t tag,
   t->force_flags = 0;
   dev::launch_upper(u, s);
   DBG(s, "upper");
+  t->dir_last_upkept = u.dir_w != nullptr;
   if (u.dir_w) {
     // the chunk's directory upkeep (new keys' pairs / fingerprints, split
     // pages' prefixes), then the entries it listed rebuilt from the tree
