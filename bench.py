@@ -946,7 +946,10 @@ def main():
                                 "bytes": dirst["bytes"], "builds": dirst["builds"],
                                 "last_build_ms": round(dirst["last_build_ms"], 4),
                                 "total_build_ms": round(dirst["total_build_ms"], 4),
-                                "maintained_by_inserts": bool(dirst["maintained"])}
+                                "maintained_by_inserts": bool(dirst["maintained"]),
+                                "exact": bool(dirst["exact"])}
+            out["dir_bytes"] = dirst["bytes"]  # the same two, at the top level
+            out["dir_build_ms"] = round(dirst["last_build_ms"], 4)
         if brk is not None:
             out["insert_every"] = brk
         if args.workload == "c2":
