@@ -87,6 +87,14 @@ def gpu_worker(rank, world, port, outdir, backend, cabi=False):
         assert torch.equal(v2, vals.flip(0)) and torch.equal(f2, found.flip(0))
     slo, shi = scan_batch(rank, world)
     counts, svals = router.range_query(d(slo), d(shi))
+    if cabi:
+        # the same scans with no host read-back (fixed runs per peer over the
+        # transport: RCCL here), equal to the synchronous form
+        ac, _, av, st = cs.range_query_async(d(slo), d(shi), vals_cap=1 << 18, peer_cap=1 << 17)
+        torch.cuda.synchronize()
+        tot, flags = (int(x) for x in st.cpu().tolist())
+        assert flags == 0 and tot == svals.numel(), (tot, flags, svals.numel())
+        assert torch.equal(ac, counts) and torch.equal(av[:tot], svals)
     torch.cuda.synchronize()
     rc = tree.check()["keys"]  # raises on a broken invariant
     keys, values = tree_contents(tree)
