@@ -606,6 +606,20 @@ def test_edge_cases(lib_ok):
     gpu_insert(t, np.concatenate([ks, ks]), np.concatenate([ks, ks + U64(1)]))
     v, f = gpu_search(t, ks)
     assert f.all() and np.array_equal(v, ks + U64(1))
+    # the largest storable key (kKeyMax - 1) and its neighbours, in every
+    # directory form: the write phase's, then the read phase's pairs (five
+    # searches), then after a chunk that touches them
+    top = np.array([(1 << 64) - 2, (1 << 64) - 3, 1 << 63], dtype=U64)
+    gpu_insert(t, top, np.array([21, 22, 23], dtype=U64))
+    probe = np.concatenate([top, np.array([(1 << 64) - 4, (1 << 63) + 1], dtype=U64)])
+    want_v = np.array([21, 22, 23, 0, 0], dtype=U64)
+    for _ in range(6):
+        v, f = gpu_search(t, probe)
+        assert np.array_equal(v, want_v) and np.array_equal(f, (want_v != 0).astype(np.uint8))
+    gpu_insert(t, top[:1], np.array([0], dtype=U64))  # delete kKeyMax - 1
+    gpu_insert(t, np.array([(1 << 64) - 4], dtype=U64), np.array([24], dtype=U64))
+    v, f = gpu_search(t, probe)
+    assert np.array_equal(v, np.array([0, 22, 23, 24, 0], dtype=U64))
     t.check()
     t.close()
 
