@@ -411,3 +411,66 @@ def test_page_check_flag_on_the_fast_path(lib_ok):
     assert t.last_error()["bits"] == 0
     orc.close()
     t.close()
+
+
+@pytest.mark.parametrize("seed", [2024, 7])
+def test_random_phases_against_the_oracle(lib_ok, seed):
+    """A randomised stream under the default policy: chunks of new keys,
+    updates, deletes and re-inserts, clustered runs that split, with 0 to 6
+    get batches between them (so the chunks are kept, idle or unkept and the
+    directory turns exact and back, changes form and density), the odd range
+    batch and update-only chunk.  Every get, every scan and the final
+    contents equal the oracle's, and whenever the library reports the
+    directory exact, every entry it trusts is (shm__dir_verify)."""
+    n0 = 1 << 16
+    t, orc, base = loaded(n0, maint=True, arena=256 << 20, max_batch=1 << 16)
+    rng = np.random.default_rng(seed)
+    nid = n0 + 1
+    deleted = np.zeros(0, dtype=U64)
+    exact_seen = 0
+    for r in range(50):
+        stored, _ = orc.dump()
+        kind = rng.integers(0, 4)
+        if kind == 0:  # updates only
+            k = stored[rng.integers(0, stored.size, 3000)]
+            v = k ^ U64(r + 11)
+        else:
+            anchors = stored[rng.integers(0, stored.size, int(rng.integers(5, 60)))]
+            runs = np.unique((anchors[:, None] +
+                              np.arange(1, int(rng.integers(2, 50)), dtype=U64)[None, :]).ravel())
+            spread = gen_keys(t, nid, int(rng.integers(0, 4000)))
+            nid += spread.size
+            dele = stored[rng.integers(0, stored.size, int(rng.integers(0, 800)))]
+            back = deleted[:int(rng.integers(0, 300))]
+            k = np.concatenate([runs, spread, dele, back])
+            v = np.concatenate([runs ^ U64(r + 1), spread ^ U64(5), np.zeros(dele.size, dtype=U64),
+                                back ^ U64(9)])
+            deleted = np.unique(np.concatenate([deleted[back.size:], dele]))
+        if k.size:
+            t.insert_batch(dev(k), dev(v))
+            orc.apply_batch(k, v)
+        if t.dir_stats()["exact"]:
+            assert_dir_exact(t)
+            exact_seen += 1
+        stored, _ = orc.dump()
+        probe = np.concatenate([k[:2000], stored[rng.integers(0, stored.size, 3000)],
+                                gen_keys(t, 10**9 + 1000 * r, 300)])
+        for _ in range(int(rng.integers(0, 7))):
+            gv, gf, _ = gpu_search(t, probe)
+            assert_same(probe, *orc.search_batch(probe), gv, gf)
+        if r % 7 == 3:
+            lo = stored[rng.integers(0, stored.size, 64)]
+            hi = lo + U64(1 << 50)
+            hi[hi < lo] = U64((1 << 64) - 2)
+            c, sv = t.range_query_batch(dev(lo), dev(hi))
+            oc, ov = orc.range_query_batch(lo, hi)
+            assert np.array_equal(c.cpu().numpy().view(U64), oc)
+            assert np.array_equal(np.sort(sv.cpu().numpy().view(U64)), np.sort(ov))
+    assert exact_seen > 0  # the stream did pass through exact phases
+    rc, oc = orc.check()
+    assert rc == 0 and t.check()["keys"] == oc["keys"]
+    ok_, ov = orc.dump()
+    gv, gf, _ = gpu_search(t, ok_)
+    assert bool(gf.all()) and np.array_equal(gv, ov)
+    orc.close()
+    t.close()
