@@ -361,10 +361,13 @@ int shm_route_unpermute_found(shm_tree *t, const uint64_t *in, const uint32_t *p
  * GPU; every rank makes the same calls in the same order (collectives).
  * Every rank's tree has the same max_batch (checked at create).
  * A routed get: each key into its owner's run of fixed-size slots
- * (1.25 n / P + 256 keys, kKeyMax padding), ncclAllToAll of the slots and
- * of the per-peer counts, local shm_search_batch, results back the same
- * way, gathered to input order; no host wait before the key exchange (every
- * rank passes the same n).  Keys past their run's slot are answered by an
+ * (n / P + 6 sqrt(n / P) + 256 keys; the runs' tails padded with kKeyMax
+ * once per size, later batches leaving earlier keys of the same owner
+ * there), grouped ncclSend / ncclRecv of the runs and of the per-peer
+ * counts, local shm_search_batch, results back the same way, gathered to
+ * input order; no host wait before the key exchange.  Every rank passes the
+ * same n: the slots' size derives from it, and ranks that disagree exchange
+ * runs of different sizes.  Keys past their run's slot are answered by an
  * exact second round that end() runs after one read-back of the counts: no
  * lookup is dropped.  A routed insert: stable bucketing, each owner's run
  * in a slot of max_batch / P (kKeyMax padding the receiver skips; a batch

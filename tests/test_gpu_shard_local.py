@@ -237,3 +237,121 @@ def test_local_group_p8_routed_paths():
     group.close()
     for t in trees:
         t.close()
+
+
+FZ_P = 4
+FZ_ROUNDS = 12
+
+
+def fuzz_round_batches(rank, rnd, pool):
+    """Rank rank's round-rnd batch: keys drawn from a shared pool (so ranks
+    collide), a skewed slice owned by one shard, deletes (value 0)."""
+    rng = np.random.default_rng(1000 * rnd + rank)
+    n = int(rng.integers(200, 3000))
+    k = pool[rng.integers(0, pool.size, n)]
+    hot = np.uint64(rng.integers(0, FZ_P)) << np.uint64(62)  # one shard's range
+    k[: n // 5] = hot | (k[: n // 5] & np.uint64((1 << 62) - 1))
+    v = rng.integers(1, 1 << 40, n, dtype=np.uint64)
+    v[rng.random(n) < 0.1] = 0
+    return k, v
+
+
+def fuzz_rank(r, trees, group, stream, pool, out, errs):
+    import sherman_amd as shm
+    try:
+        dev = torch.device("cuda:0")
+
+        def d(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+
+        res = []
+        with torch.cuda.stream(stream):
+            cs = shm.CShard.local(trees[r], group, r)
+            for rnd in range(FZ_ROUNDS):
+                k, v = fuzz_round_batches(r, rnd, pool)
+                cs.insert(d(k), d(v), stream=stream)
+                # every rank passes the same get batch size (the slots' size
+                # derives from it: include/sherman_amd.h), different keys
+                nq = int(np.random.default_rng(7000 + rnd).integers(100, 4000))
+                rng = np.random.default_rng(5000 + 100 * rnd + r)
+                q = pool[rng.integers(0, pool.size, nq)]
+                vals = torch.empty(q.size, dtype=torch.int64, device=dev)
+                found = torch.empty(q.size, dtype=torch.uint8, device=dev)
+                cs.search(d(q), vals, found, stream=stream)
+                scan = None
+                if rnd % 3 == 2:
+                    lo = np.sort(pool[rng.integers(0, pool.size, 16)])
+                    hi = lo + np.uint64(1 << 58)
+                    hi[hi < lo] = np.uint64((1 << 64) - 2)
+                    ac, _, av, st = cs.range_query_async(d(lo), d(hi), vals_cap=1 << 16,
+                                                         peer_cap=1 << 15, n_cap=64, stream=stream)
+                    scan = (lo, hi, ac, av, st)
+                cs.synchronize()
+                stream.synchronize()
+                res.append((q, vals.cpu().numpy().view(U64), found.cpu().numpy(),
+                            None if scan is None else
+                            (scan[0], scan[1], scan[2].cpu().numpy().view(U64),
+                             scan[3].cpu().numpy().view(U64), scan[4].cpu().numpy())))
+            cs.close()
+        out[r] = res
+    except BaseException as e:  # noqa: BLE001 - reported by the main thread
+        errs.append((r, repr(e)))
+
+
+def test_local_group_random_rounds_vs_oracle():
+    """Twelve rounds at P = 4 on the in-process transport: every rank inserts
+    a random batch (keys from one shared pool, so ranks collide; a fifth of
+    each batch forced into one shard's range, which overflows its slot; 10 %
+    deletes), then gets a random batch, and every third round scans with the
+    no-read-back form.  After each round every rank's gets and scans equal
+    one unsharded oracle that applied the round's batches rank-major."""
+    import sherman_amd as shm
+    from oracle.pyoracle import OracleTree
+    from sherman_amd.shard import shard_range
+
+    assert torch.cuda.is_available(), "GPU test without a GPU"
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(99)
+    pool = np.unique(rng.integers(1, (1 << 64) - 2, 20000, dtype=np.uint64))
+    trees = []
+    for r in range(FZ_P):
+        lo, bits = shard_range(r, FZ_P)
+        trees.append(shm.Tree(arena_bytes=32 << 20, max_batch=MAX_BATCH, device=0, node_id=r,
+                              key_lo=lo, key_bits=bits))
+    group = shm.LocalGroup(FZ_P)
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    out, errs = [None] * FZ_P, []
+    th = [threading.Thread(target=fuzz_rank, args=(r, trees, group, stream, pool, out, errs))
+          for r in range(FZ_P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank thread hung"
+    assert not errs, errs
+    ref = OracleTree(64 << 20)
+    for rnd in range(FZ_ROUNDS):
+        for r in range(FZ_P):
+            ref.apply_batch(*fuzz_round_batches(r, rnd, pool))
+        for r in range(FZ_P):
+            q, gv, gf, scan = out[r][rnd]
+            ov, of = ref.search_batch(q)
+            assert np.array_equal(gv, ov) and np.array_equal(gf, of), (rnd, r)
+            if scan is not None:
+                lo, hi, c, v, st = scan
+                assert st[1] == 0, (rnd, r, st)
+                oc, ovv = ref.range_query_batch(lo, hi)
+                assert np.array_equal(c, oc), (rnd, r)
+                assert int(st[0]) == ovv.size, (rnd, r)
+                # per scan the same values (the sharded trees' leaves hold
+                # them in another slot order than the one oracle tree's)
+                off = np.concatenate([[0], np.cumsum(oc)]).astype(np.int64)
+                for i in range(lo.size):
+                    a_, b_ = off[i], off[i + 1]
+                    assert np.array_equal(np.sort(v[a_:b_]), np.sort(ovv[a_:b_])), (rnd, r, i)
+    ref.close()
+    group.close()
+    for t in trees:
+        assert t.check()["keys"] >= 0
+        t.close()
