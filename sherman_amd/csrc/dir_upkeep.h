@@ -1,13 +1,14 @@
-// dir_upkeep.h — the leaf directory kept current by the insert chunk's leaf
-// writers (tree.cpp dir_maint_enabled has the policy).
+// dir_upkeep.h — the leaf directory kept current after each insert chunk
+// (tree.cpp insert_apply has the policy: which chunks keep
+// it).
 //
 // The directory (leafdir.hip) maps key prefixes to leaves, the role of the
 // reference's IndexCache (include/IndexCache.h:59-259, kept current there by
-// the cache's own inserts and invalidated per entry).  After each chunk's
-// k_upper, k_dir_upkeep (leafdir.hip, one wave per staged segment: the tree
-// is final then, and the upsert's and k_upper's dependent chains pay
-// nothing -- done inline in them the same work cost C5 +70 us per chunk)
-// applies these rules:
+// the cache's own inserts and invalidated per entry).  After each kept
+// chunk's k_upper, k_dir_upkeep (leafdir.hip: a lane per op for the new
+// keys, a wave per split segment; the tree is final then, and the upsert's
+// and k_upper's dependent chains pay nothing -- done inline in them the same
+// work cost C5 +70 us per chunk) applies these rules:
 //   * a new key in an empty slot (the no-split branch of leaf_page_store,
 //     Tree.cpp:878-912, applied by upsert.hip) adds its (fingerprint, slot) pair
 //     to its prefix's pair-form entry, or its fingerprint byte to a

@@ -271,7 +271,7 @@ struct UpperArgs;
 // by the upsert kernel itself, upsert.hip) or 0 (every split left to k_upper)
 void launch_leaf_upsert(const SegArgs& a, const UpperArgs& u, hipStream_t s);
 
-// the directory form an insert chunk's leaf writers keep (UpperArgs.dir_form,
+// the directory form a kept chunk's upkeep writes (UpperArgs.dir_form,
 // dir_upkeep.h)
 constexpr uint32_t kDirFormNone = 0, kDirFormFp = 1, kDirFormPairs = 2;
 
@@ -329,12 +329,12 @@ struct UpperArgs {
   // nullable: the directory's level-1 / level-2 path pages (launch_leaf_dir),
   // start pages of parent_of walks
   const uint32_t* dir_hint;
-  // nullable: the same directory, kept current by this chunk's leaf writers
-  // in form dir_form (dir_upkeep.h: 1 fingerprint, 2 pair form)
+  // nullable: the same directory, kept current after this chunk by
+  // k_dir_upkeep in form dir_form (dir_upkeep.h: 1 fingerprint, 2 pair form)
   uint64_t* dir_w;
   uint32_t dir_form;
-  // the chunk's repair list (nullable): prefixes whose entries its writers
-  // could not keep exact, for k_dir_repair after the chunk; dir_fix_n[par]
+  // the chunk's repair list (nullable): prefixes whose entries the upkeep
+  // could not keep exact, for k_dir_repair after it; dir_fix_n[par]
   // counts them (past dir_fix_cap they are lost: the entry stays marked)
   uint32_t* dir_fix;
   uint32_t* dir_fix_n;
